@@ -1,0 +1,14 @@
+"""MI355X-native 802.11 channel estimation (LT_LS, PS_Linear/Cubic/Sinc,
+PS_MMSE, equalization) behind the reference's estimator API.
+
+The package name starts with a digit, so import it with
+``importlib.import_module("80211parallelestimation_amd")``.
+"""
+from .wce import (  # noqa: F401
+    ALL, DC, EQUALIZE, LS_ALL, LT_LS, MMSE_REF, MMSE_TEXTBOOK, NBLK, NSC, PILOTS, PS_CUBIC, PS_LINEAR,
+    PS_MMSE, PS_SINC, Context, DeviceArray, Event, Frames, Outputs, Stream, WceError, device_count, load,
+    synchronize, WiFi_channel_estimation_LT_LS, WiFi_channel_estimation_PS_Cubic,
+    WiFi_channel_estimation_PS_Linear, WiFi_channel_estimation_PS_MMSE, WiFi_channel_estimation_PS_Sinc,
+)
+
+__version__ = "0.1.0"

@@ -1,0 +1,331 @@
+// wce_api.cpp -- C ABI (include/wce.h): context lifetime, argument checks,
+// launches, and thin HIP runtime helpers.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "wce_internal.h"
+
+using wce::State;
+
+struct wce_ctx {
+    int device = 0;
+    State *d_state = nullptr;   // device-resident shared state (the broadcast unit)
+    bool ready = false;
+    bool has_host = false;
+    State host;                 // host copy when built locally
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char *what)
+{
+    g_err = what;
+    return code;
+}
+
+static int hipfail(hipError_t e, const char *what)
+{
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return WCE_EHIP;
+}
+
+#define HIPCHECK(x, what)                         \
+    do {                                          \
+        hipError_t e_ = (x);                      \
+        if (e_ != hipSuccess) return hipfail(e_, what); \
+    } while (0)
+
+static int check_device(int device)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(WCE_ENODEV, "no HIP device");
+    if (device < 0 || device >= n) return fail(WCE_EINVAL, "device index out of range");
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(WCE_ENODEV, "libwce is built for gfx950 (MI355X) only");
+    return WCE_OK;
+}
+
+namespace {
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+}  // namespace
+
+extern "C" {
+
+const char *wce_last_error(void) { return g_err.c_str(); }
+const char *wce_version(void) { return "wce 0.1.0 (gfx950)"; }
+
+int wce_ctx_create_empty(wce_ctx **out, int device)
+{
+    if (!out) return fail(WCE_EINVAL, "null ctx pointer");
+    int rc = check_device(device);
+    if (rc) return rc;
+    wce_ctx *c = new (std::nothrow) wce_ctx();
+    if (!c) return fail(WCE_ENOMEM, "ctx alloc");
+    c->device = device;
+    DeviceGuard g(device);
+    hipError_t e = hipMalloc(&c->d_state, sizeof(State));
+    if (e != hipSuccess) { delete c; return hipfail(e, "hipMalloc(state)"); }
+    e = hipMemset(c->d_state, 0, sizeof(State));
+    if (e != hipSuccess) { (void)hipFree(c->d_state); delete c; return hipfail(e, "hipMemset(state)"); }
+    *out = c;
+    return WCE_OK;
+}
+
+int wce_ctx_create(wce_ctx **out, int device, const wce_complex *tx_pre, const wce_complex *rx_pre, double ow2,
+                   int mode)
+{
+    if (!out || !tx_pre || !rx_pre) return fail(WCE_EINVAL, "null argument");
+    if (mode != WCE_MMSE_REF && mode != WCE_MMSE_TEXTBOOK) return fail(WCE_EINVAL, "bad mmse mode");
+    if (!(ow2 > 0)) return fail(WCE_EINVAL, "ow2 must be > 0");
+    wce_ctx *c = nullptr;
+    int rc = wce_ctx_create_empty(&c, device);
+    if (rc) return rc;
+    wce::ldc txl[wce::NSC], rxl[wce::NSC], hlt[wce::NSC];
+    for (int k = 0; k < wce::NSC; k++) {
+        txl[k].re = tx_pre[k].re; txl[k].im = tx_pre[k].im;
+        rxl[k].re = rx_pre[k].re; rxl[k].im = rx_pre[k].im;
+    }
+    wce::host_lt_ls(txl, rxl, hlt);
+    rc = wce::host_build_state(&c->host, wce::host_reference_F(), wce::host_reference_invF(), hlt, txl, ow2, mode);
+    if (rc) { wce_ctx_destroy(c); return fail(rc, "state build"); }
+    c->has_host = true;
+    DeviceGuard g(device);
+    hipError_t e = hipMemcpy(c->d_state, &c->host, sizeof(State), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { wce_ctx_destroy(c); return hipfail(e, "upload state"); }
+    c->ready = true;
+    *out = c;
+    return WCE_OK;
+}
+
+int wce_ctx_destroy(wce_ctx *c)
+{
+    if (!c) return WCE_OK;
+    if (c->d_state) {
+        DeviceGuard g(c->device);
+        (void)hipFree(c->d_state);
+    }
+    delete c;
+    return WCE_OK;
+}
+
+int wce_ctx_state(wce_ctx *c, void **ptr, size_t *bytes)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (ptr) *ptr = c->d_state;
+    if (bytes) *bytes = sizeof(State);
+    return WCE_OK;
+}
+
+int wce_ctx_mark_ready(wce_ctx *c)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    DeviceGuard g(c->device);
+    int32_t magic = 0;
+    HIPCHECK(hipDeviceSynchronize(), "sync");
+    HIPCHECK(hipMemcpy(&magic, reinterpret_cast<char *>(c->d_state) + offsetof(State, magic), sizeof(magic),
+                       hipMemcpyDeviceToHost), "read state magic");
+    if (magic != wce::STATE_MAGIC) return fail(WCE_ESTATE, "state buffer does not hold a valid state");
+    c->ready = true;
+    return WCE_OK;
+}
+
+int wce_ctx_get_shared(wce_ctx *c, wce_complex *h_lt, wce_complex *C, double *a, double *b)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    State *h = new (std::nothrow) State;
+    if (!h) return fail(WCE_ENOMEM, "alloc");
+    DeviceGuard g(c->device);
+    hipError_t e = hipMemcpy(h, c->d_state, sizeof(State), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) { delete h; return hipfail(e, "download state"); }
+    if (h_lt) std::memcpy(h_lt, h->h_lt, sizeof(wce_complex) * wce::NSC);
+    if (C) std::memcpy(C, h->C, sizeof(h->C));
+    if (a) *a = h->acoef;
+    if (b) *b = h->bcoef;
+    delete h;
+    return WCE_OK;
+}
+
+static int check_frames(const wce_frames *in, bool need_blocks)
+{
+    if (!in) return fail(WCE_EINVAL, "null frames");
+    if (in->n_frames < 0) return fail(WCE_EINVAL, "n_frames < 0");
+    if (in->n_frames == 0) return WCE_OK;
+    if (!in->tx || !in->rx) return fail(WCE_EINVAL, "tx/rx required");
+    if (in->block < 0 || in->block >= wce::NBLK) return fail(WCE_EINVAL, "block out of range");
+    if (in->block_stride < wce::NSC && (need_blocks || in->block > 0))
+        return fail(WCE_EINVAL, "block_stride < 53");
+    const int64_t span = (int64_t)(need_blocks ? wce::NBLK - 1 : in->block) * in->block_stride + wce::NSC;
+    if (in->n_frames > 1 && in->frame_stride < span) return fail(WCE_EINVAL, "frame_stride too small");
+    if (in->rx_pre && in->n_frames > 1 && in->pre_stride < wce::NSC) return fail(WCE_EINVAL, "pre_stride < 53");
+    return WCE_OK;
+}
+
+int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_stride, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    int rc = check_frames(in, false);
+    if (rc) return rc;
+    if (in->n_frames == 0) return WCE_OK;
+    if (!W || (in->n_frames > 1 && w_stride < wce::NSC)) return fail(WCE_EINVAL, "bad W");
+    wce::SolveArgs a{};
+    a.tx = reinterpret_cast<const double *>(in->tx);
+    a.rx = reinterpret_cast<const double *>(in->rx);
+    a.fs = in->frame_stride; a.bs = in->block_stride; a.n = in->n_frames; a.blk = in->block;
+    a.w = reinterpret_cast<double *>(W);
+    a.ws = w_stride;
+    DeviceGuard g(c->device);
+    rc = wce::launch_mmse_solve(c->d_state, a, stream);
+    return rc ? fail(rc, "mmse_solve launch") : WCE_OK;
+}
+
+int wce_mmse_apply(wce_ctx *c, const wce_complex *W, wce_complex *H, int64_t stride, int64_t n, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    if (n < 0) return fail(WCE_EINVAL, "n < 0");
+    if (n == 0) return WCE_OK;
+    if (!W || !H || (n > 1 && stride < wce::NSC)) return fail(WCE_EINVAL, "bad W/H");
+    DeviceGuard g(c->device);
+    int rc = wce::launch_mmse_apply(c->d_state, reinterpret_cast<const double *>(W), reinterpret_cast<double *>(H),
+                                    stride, n, stream);
+    return rc ? fail(rc, "mmse_apply launch") : WCE_OK;
+}
+
+int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
+{
+    if (!c || !out) return fail(WCE_EINVAL, "null argument");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    if (mask & ~0x3Fu) return fail(WCE_EINVAL, "unknown estimator bits");
+    const bool eq = (mask & WCE_EQUALIZE) != 0;
+    int rc = check_frames(in, eq);
+    if (rc) return rc;
+    if (in->n_frames == 0 || mask == 0) return WCE_OK;
+    const int64_t n = in->n_frames;
+    if (n > 1 && out->out_stride < wce::NSC && (mask & 0x1F)) return fail(WCE_EINVAL, "out_stride < 53");
+    if ((mask & WCE_EST_LT_LS) && !out->lt_ls) return fail(WCE_EINVAL, "lt_ls output missing");
+    if ((mask & WCE_EST_PS_LINEAR) && !out->ps_linear) return fail(WCE_EINVAL, "ps_linear output missing");
+    if ((mask & WCE_EST_PS_CUBIC) && !out->ps_cubic) return fail(WCE_EINVAL, "ps_cubic output missing");
+    if ((mask & WCE_EST_PS_SINC) && !out->ps_sinc) return fail(WCE_EINVAL, "ps_sinc output missing");
+    if ((mask & WCE_EST_PS_MMSE) && !out->ps_mmse) return fail(WCE_EINVAL, "ps_mmse output missing");
+    uint32_t eq_src = out->eq_source ? out->eq_source : WCE_EST_PS_LINEAR;
+    if (eq) {
+        if (!out->eq) return fail(WCE_EINVAL, "eq output missing");
+        if (eq_src != WCE_EST_PS_LINEAR && eq_src != WCE_EST_PS_CUBIC && eq_src != WCE_EST_PS_SINC)
+            return fail(WCE_EINVAL, "eq_source must be a PS interpolation estimator");
+        if (out->eq_block_stride < wce::NSC ||
+            (n > 1 && out->eq_frame_stride < (wce::NBLK - 1) * out->eq_block_stride + wce::NSC))
+            return fail(WCE_EINVAL, "eq strides too small");
+    }
+    DeviceGuard g(c->device);
+    if (mask & (WCE_EST_LS_ALL | WCE_EQUALIZE)) {
+        wce::LsArgs a{};
+        a.tx = reinterpret_cast<const double *>(in->tx);
+        a.rx = reinterpret_cast<const double *>(in->rx);
+        a.rx_pre = reinterpret_cast<const double *>(in->rx_pre);
+        a.tx_pre = reinterpret_cast<const double *>(in->tx_pre);
+        a.fs = in->frame_stride; a.bs = in->block_stride; a.ps = in->pre_stride; a.n = n; a.blk = in->block;
+        a.mask = mask & (WCE_EST_LS_ALL | WCE_EQUALIZE);
+        a.lt = reinterpret_cast<double *>(out->lt_ls);
+        a.lin = reinterpret_cast<double *>(out->ps_linear);
+        a.cub = reinterpret_cast<double *>(out->ps_cubic);
+        a.snc = reinterpret_cast<double *>(out->ps_sinc);
+        a.eq = reinterpret_cast<double *>(out->eq);
+        a.os = out->out_stride; a.eqfs = out->eq_frame_stride; a.eqbs = out->eq_block_stride;
+        a.eq_src = eq_src;
+        if (eq) a.mask |= eq_src;   // the blend needs that PS estimate
+        rc = wce::launch_ls(c->d_state, a, stream);
+        if (rc) return fail(rc, "ls launch");
+    }
+    if (mask & WCE_EST_PS_MMSE) {
+        rc = wce_mmse_solve(c, in, out->ps_mmse, out->out_stride, stream);
+        if (rc) return rc;
+        rc = wce_mmse_apply(c, out->ps_mmse, out->ps_mmse, out->out_stride, n, stream);
+        if (rc) return rc;
+    }
+    return WCE_OK;
+}
+
+int wce_synth_frames(wce_ctx *c, wce_complex *tx, wce_complex *rx, wce_complex *rx_pre, int64_t frame_stride,
+                     int64_t block_stride, int64_t pre_stride, int64_t first_frame, int64_t n_frames, uint64_t seed,
+                     const wce_complex *h_shared, double amplitude, double ow2, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    if (!rx || n_frames < 0 || first_frame < 0) return fail(WCE_EINVAL, "bad synth args");
+    if (block_stride < wce::NSC || frame_stride < (wce::NBLK - 1) * block_stride + wce::NSC)
+        return fail(WCE_EINVAL, "synth strides too small");
+    if (rx_pre && pre_stride < wce::NSC) return fail(WCE_EINVAL, "pre_stride < 53");
+    wce::SynthArgs a{};
+    a.tx = reinterpret_cast<double *>(tx);
+    a.rx = reinterpret_cast<double *>(rx);
+    a.rx_pre = reinterpret_cast<double *>(rx_pre);
+    a.fs = frame_stride; a.bs = block_stride; a.ps = pre_stride; a.first = first_frame; a.n = n_frames;
+    a.seed = seed;
+    a.h_shared = reinterpret_cast<const double *>(h_shared);
+    a.amp = amplitude; a.ow2 = ow2;
+    DeviceGuard g(c->device);
+    int rc = wce::launch_synth(c->d_state, a, stream);
+    return rc ? fail(rc, "synth launch") : WCE_OK;
+}
+
+// ---------------------------------------------------------------- runtime helpers
+int wce_device_count(int *count)
+{
+    if (!count) return fail(WCE_EINVAL, "null");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = (e == hipSuccess) ? n : 0;
+    return WCE_OK;
+}
+int wce_set_device(int d) { HIPCHECK(hipSetDevice(d), "hipSetDevice"); return WCE_OK; }
+int wce_malloc(void **p, size_t bytes) { HIPCHECK(hipMalloc(p, bytes), "hipMalloc"); return WCE_OK; }
+int wce_free(void *p) { HIPCHECK(hipFree(p), "hipFree"); return WCE_OK; }
+int wce_memcpy_htod(void *d, const void *s, size_t b) { HIPCHECK(hipMemcpy(d, s, b, hipMemcpyHostToDevice), "htod"); return WCE_OK; }
+int wce_memcpy_dtoh(void *d, const void *s, size_t b) { HIPCHECK(hipMemcpy(d, s, b, hipMemcpyDeviceToHost), "dtoh"); return WCE_OK; }
+int wce_memset(void *d, int v, size_t b) { HIPCHECK(hipMemset(d, v, b), "hipMemset"); return WCE_OK; }
+int wce_stream_create(void **s)
+{
+    hipStream_t st;
+    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    *s = st;
+    return WCE_OK;
+}
+int wce_stream_destroy(void *s) { HIPCHECK(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy"); return WCE_OK; }
+int wce_stream_synchronize(void *s) { HIPCHECK(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize"); return WCE_OK; }
+int wce_event_create(void **ev)
+{
+    hipEvent_t e;
+    HIPCHECK(hipEventCreate(&e), "hipEventCreate");
+    *ev = e;
+    return WCE_OK;
+}
+int wce_event_destroy(void *ev) { HIPCHECK(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy"); return WCE_OK; }
+int wce_event_record(void *ev, void *s) { HIPCHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)s), "hipEventRecord"); return WCE_OK; }
+int wce_event_elapsed_ms(float *ms, void *a, void *b)
+{
+    HIPCHECK(hipEventSynchronize((hipEvent_t)b), "hipEventSynchronize");
+    HIPCHECK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
+    return WCE_OK;
+}
+
+}  // extern "C"

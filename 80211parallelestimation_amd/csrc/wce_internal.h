@@ -1,0 +1,82 @@
+// wce_internal.h -- layout shared by the host code (g++ / hipcc) and the
+// gfx950 kernels.  Not part of the public ABI (include/wce.h is).
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/wce.h"
+
+namespace wce {
+
+constexpr int NSC = WCE_NSC;      // 53 useful subcarriers (utils.h:13)
+constexpr int NBLK = WCE_NBLK;    // 15 OFDM blocks (utils.h:15)
+constexpr int NPAD = 64;          // one wave64 lane per subcarrier
+constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
+constexpr int32_t STATE_MAGIC = 0x80211;
+
+// The frame-independent shared state: everything one rank broadcasts to the
+// others (one RCCL broadcast, 47 KB).  Complex values are {re, im} fp64.
+struct State {
+    double C[NSC * NSC * 2];   // MMSE covariance operator, row-major (44,944 B)
+    double h_lt[NPAD * 2];     // LT_LS of the shared preamble (main.c:66-75)
+    double tx_pre[NPAD * 2];   // shared tx preamble FFT
+    double sinc[4][NPAD];      // sinc((k - P_p)/14) in double (utils.c:727-733)
+    double acoef, bcoef;       // Ryy = a X C X' + b I
+    double ow2;                // noise variance (inputs.h:18)
+    uint64_t xmask;            // bit k set: subcarrier k enters X
+    int32_t mode;              // WCE_MMSE_REF / WCE_MMSE_TEXTBOOK
+    int32_t magic;             // STATE_MAGIC once valid
+    int32_t pad[2];
+};
+static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
+
+// Host-side builders (wce_state.cpp, compiled by g++ for x87 long double).
+// `ldc` = long double _Complex as {re, im} pairs of long double.
+struct ldc { long double re, im; };
+
+// F[t][f] = cexp(-2*I*PI*t*f/53) exactly as main.c:18-26 evaluates it.
+void host_fmatrix(ldc *F);
+// The reference's adjugate inverse (utils.c:141-170 / 440-459 / 543-569) in
+// 80-bit arithmetic, cofactors spread over threads.
+void host_inverse_cofactor(const ldc *A, int n, ldc *Y, int nthreads);
+// Cached inverse of the standard F (computed once per process).
+const ldc *host_reference_invF();
+const ldc *host_reference_F();
+// main.c:66-75 in long double.
+void host_lt_ls(const ldc *tx_pre, const ldc *rx_pre, ldc *H);
+// Fill a host State from F / invF / H_LS (long double) for `mode`.
+int host_build_state(State *st, const ldc *F, const ldc *invF, const ldc *H_LS,
+                     const ldc *tx_pre, double ow2, int mode);
+
+// Kernel launchers (wce_kernels.hip).
+struct LsArgs {
+    const double *tx, *rx, *rx_pre, *tx_pre;
+    int64_t fs, bs, ps, n;
+    int32_t blk;
+    uint32_t mask;
+    double *lt, *lin, *cub, *snc, *eq;
+    int64_t os, eqfs, eqbs;
+    uint32_t eq_src;
+    uint32_t pad;
+};
+struct SolveArgs {
+    const double *tx, *rx;
+    int64_t fs, bs, n;
+    int32_t blk;
+    int32_t pad;
+    double *w;
+    int64_t ws;
+};
+struct SynthArgs {
+    double *tx, *rx, *rx_pre;
+    int64_t fs, bs, ps, first, n;
+    uint64_t seed;
+    const double *h_shared;
+    double amp, ow2;
+};
+
+int launch_ls(const State *st, const LsArgs &a, void *stream);
+int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream);
+int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream);
+int launch_synth(const State *st, const SynthArgs &a, void *stream);
+
+}  // namespace wce

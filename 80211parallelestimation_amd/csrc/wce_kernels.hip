@@ -1,0 +1,444 @@
+// wce_kernels.hip -- gfx950 (CDNA4) kernels of the 802.11 channel-estimation
+// engine.  Written for wave64 / MI355X only.
+//
+//   ls_kernel          LT_LS + PS_Linear/Cubic/Sinc + equalization,
+//                      one wave per frame, HBM streaming (main.c:66-146,
+//                      WiFi_Equalization.m).
+//   mmse_solve_kernel  per-frame Ryy = a X C X' + b I, Cholesky with the rx
+//                      vector bordered on as row 53 (forward solve for free),
+//                      blocked back-substitution; the 54x54 lower triangle
+//                      lives in registers on an 8x8 lane grid (block-cyclic),
+//                      LDS only carries the pivot column broadcast.
+//                      (main.c:148-212 / WiFi_channel_estimation_PS_MMSE.m)
+//   mmse_apply_kernel  H = C W for 16-frame tiles on v_mfma_f64_16x16x4_f64.
+//   synth_kernel       counter-RNG synthetic frames (bench / tests).
+#include <hip/hip_runtime.h>
+#include "wce_internal.h"
+
+namespace wce {
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b)
+{
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+__device__ __forceinline__ double2 cdiv(double2 a, double2 b)
+{
+    const double inv = 1.0 / (b.x * b.x + b.y * b.y);
+    return make_double2((a.x * b.x + a.y * b.y) * inv, (a.y * b.x - a.x * b.y) * inv);
+}
+// acc -= l * conj(c)   (4 DFMA)
+__device__ __forceinline__ void cmsub_conj(double2 &acc, double2 l, double2 c)
+{
+    acc.x = fma(-l.x, c.x, acc.x);
+    acc.x = fma(-l.y, c.y, acc.x);
+    acc.y = fma(-l.y, c.x, acc.y);
+    acc.y = fma(l.x, c.y, acc.y);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double2 readlane_c(double2 v, int lane)
+{
+    return make_double2(readlane_f64(v.x, lane), readlane_f64(v.y, lane));
+}
+__device__ __forceinline__ double2 shfl_xor_c(double2 v, int m)
+{
+    return make_double2(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64));
+}
+__device__ __forceinline__ double2 shfl_c(double2 v, int src)
+{
+    return make_double2(__shfl(v.x, src, 64), __shfl(v.y, src, 64));
+}
+__device__ __forceinline__ double2 ld2(const double *p, int64_t idx)
+{
+    return reinterpret_cast<const double2 *>(p)[idx];
+}
+__device__ __forceinline__ void st2(double *p, int64_t idx, double2 v)
+{
+    reinterpret_cast<double2 *>(p)[idx] = v;
+}
+
+// =====================================================================
+// LS family + equalization: one wave per frame, lane k = subcarrier k.
+// =====================================================================
+constexpr int LS_WAVES = 4;   // waves per 256-thread workgroup
+
+__global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * LS_WAVES;
+    const bool act = lane < NSC;
+    const int k = act ? lane : 0;
+    const double *txp = a.tx_pre ? a.tx_pre : st->tx_pre;
+    const double2 tpk = ld2(txp, k);
+    const double cq = tpk.x - tpk.y;           // real "conj" of main.c:69-70
+    const double2 hlt_shared = ld2(st->h_lt, k);
+    const double s0 = st->sinc[0][k], s1 = st->sinc[1][k], s2 = st->sinc[2][k], s3 = st->sinc[3][k];
+    const uint32_t mask = a.mask;
+    const bool need_lt = (mask & (WCE_EST_LT_LS | WCE_EQUALIZE)) != 0;
+    const bool need_ps = (mask & (WCE_EST_PS_LINEAR | WCE_EST_PS_CUBIC | WCE_EST_PS_SINC | WCE_EQUALIZE)) != 0;
+    // linear interpolation segment (main.c:86-99): k < 19 seg 0, k < 33 seg 1, else seg 2
+    const int seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
+    const double alpha = (double)(k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) * (1.0 / 14.0);
+    const double dk0 = (double)(k - WCE_P0), dk1 = (double)(k - WCE_P1), dk2 = (double)(k - WCE_P2);
+    const int pil = lane < 4 ? (lane == 0 ? WCE_P0 : lane == 1 ? WCE_P1 : lane == 2 ? WCE_P2 : WCE_P3) : 0;
+
+    for (int64_t f = (int64_t)blockIdx.x * LS_WAVES + (threadIdx.x >> 6); f < a.n; f += nw) {
+        const int64_t base = f * a.fs + (int64_t)a.blk * a.bs;
+        double2 h0 = make_double2(0, 0), h1 = h0, h2 = h0, h3 = h0;
+        if (need_ps) {
+            double2 hp = make_double2(0, 0);
+            if (lane < 4) hp = cdiv(ld2(a.rx, base + pil), ld2(a.tx, base + pil));  // main.c:82-84
+            h0 = shfl_c(hp, 0); h1 = shfl_c(hp, 1); h2 = shfl_c(hp, 2); h3 = shfl_c(hp, 3);
+        }
+        double2 hlt = hlt_shared;
+        if (need_lt && a.rx_pre) {
+            const double2 rp = ld2(a.rx_pre, f * a.ps + k);
+            hlt = cdiv(make_double2(cq * rp.x, cq * rp.y), make_double2(cq * tpk.x, cq * tpk.y));
+        }
+        if (k == 26) hlt = make_double2(0, 0);   // main.c:74
+        double2 hlin = make_double2(0, 0);
+        if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {
+            const double2 lo = seg == 0 ? h0 : (seg == 1 ? h1 : h2);
+            const double2 hi = seg == 0 ? h1 : (seg == 1 ? h2 : h3);
+            hlin = cadd(lo, cscale(csub(hi, lo), alpha));
+        }
+        double2 hcub = make_double2(0, 0);
+        if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
+            const double r = 1.0 / 14.0;
+            const double2 f01 = cscale(csub(h1, h0), r), f12 = cscale(csub(h2, h1), r), f23 = cscale(csub(h3, h2), r);
+            const double2 f012 = cscale(csub(f12, f01), r), f123 = cscale(csub(f23, f12), r);
+            const double2 f0123 = cscale(csub(f123, f012), r);
+            hcub = cadd(cadd(cadd(h0, cscale(f01, dk0)), cscale(cscale(f012, dk0), dk1)),
+                        cscale(cscale(cscale(f0123, dk0), dk1), dk2));
+        }
+        double2 hsnc = make_double2(0, 0);
+        if (mask & WCE_EST_PS_SINC)            // main.c:135-145
+            hsnc = cadd(cadd(cadd(cscale(h0, s0), cscale(h1, s1)), cscale(h2, s2)), cscale(h3, s3));
+        if (act) {
+            const int64_t o = f * a.os + k;
+            if ((mask & WCE_EST_LT_LS) && a.lt) st2(a.lt, o, hlt);
+            if ((mask & WCE_EST_PS_LINEAR) && a.lin) st2(a.lin, o, hlin);
+            if ((mask & WCE_EST_PS_CUBIC) && a.cub) st2(a.cub, o, hcub);
+            if ((mask & WCE_EST_PS_SINC) && a.snc) st2(a.snc, o, hsnc);
+        }
+        if ((mask & WCE_EQUALIZE) && a.eq && act) {   // WiFi_Equalization.m:1-9
+            const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
+            const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
+#pragma unroll 5
+            for (int b = 0; b < NBLK; b++) {
+                const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
+                const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
+                const double2 rv = ld2(a.rx, rb + b * a.bs);
+                st2(a.eq, eb + b * a.eqbs, k == 26 ? make_double2(0, 0) : cdiv(rv, hu));
+            }
+        }
+    }
+}
+
+// =====================================================================
+// MMSE solve.  One wave per frame, lane = 8p + q holds A[p+8a][q+8b] for the
+// 28 register blocks a >= b (a, b < 7): the block-cyclic 8x8 grid spreads the
+// shrinking trailing matrix evenly over lanes.  Row 53 holds conj(rx), so the
+// factorisation of [[Ryy, rx], [rx', *]] leaves conj(L^-1 rx) in that row.
+// =====================================================================
+constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
+
+struct SolveLds {
+    double2 col[64];      // pivot-column broadcast L[:, k]
+    double2 x[64];        // masked tx of the frame (X diagonal), 0 past 53
+    double2 rx[64];
+    double2 blk[64];      // diagonal 8x8 block during back-substitution
+    double2 z[64];        // solution
+    double rd[64];        // 1 / L[k][k]
+};
+
+template <int KB>
+__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane)
+{
+    constexpr int NK = (KB == 6) ? (NSC - 48) : 8;
+#pragma unroll 1
+    for (int kq = 0; kq < NK; ++kq) {
+        const double d = readlane_f64(A[KB][KB].x, 9 * kq);   // pivot lives in lane (kq, kq)
+        const double sq = sqrt(d);
+        const double rs = 1.0 / sq;
+        if (q == kq) {
+#pragma unroll
+            for (int aa = KB; aa < RB; ++aa) {
+                A[aa][KB] = cscale(A[aa][KB], rs);
+                s.col[p + 8 * aa] = A[aa][KB];
+            }
+        }
+        if (lane == 0) s.rd[8 * KB + kq] = rs;
+        __syncthreads();
+        double2 Lr[RB], Lc[RB];
+#pragma unroll
+        for (int aa = KB; aa < RB; ++aa) Lr[aa] = s.col[p + 8 * aa];
+#pragma unroll
+        for (int bb = KB; bb < RB; ++bb) Lc[bb] = s.col[q + 8 * bb];
+        if (q > kq) {
+#pragma unroll
+            for (int aa = KB; aa < RB; ++aa) cmsub_conj(A[aa][KB], Lr[aa], Lc[KB]);
+        }
+#pragma unroll
+        for (int aa = KB + 1; aa < RB; ++aa)
+#pragma unroll
+            for (int bb = KB + 1; bb <= aa; ++bb) cmsub_conj(A[aa][bb], Lr[aa], Lc[bb]);
+        __syncthreads();
+    }
+}
+
+template <int BLK>
+__device__ __forceinline__ void back_block(double2 (&A)[RB][RB], double2 (&P)[RB], SolveLds &s, int p, int q,
+                                           int lane)
+{
+    constexpr int NROW = (BLK == 6) ? (NSC - 48) : 8;
+    // w[8*BLK + q] = y - sum of the contributions of the rows already solved
+    double2 w = P[BLK];
+    w = cadd(w, shfl_xor_c(w, 8));
+    w = cadd(w, shfl_xor_c(w, 16));
+    w = cadd(w, shfl_xor_c(w, 32));
+    s.blk[lane] = A[BLK][BLK];
+    __syncthreads();
+#pragma unroll 1
+    for (int t = NROW - 1; t >= 0; --t) {
+        const int i = 8 * BLK + t;
+        const double2 z = cscale(readlane_c(w, t), s.rd[i]);    // lane t = (0, t) holds w_t
+        if (lane == 0) s.z[i] = z;
+        const double2 l = s.blk[8 * t + q];                      // L[i][8*BLK + q]
+        cmsub_conj(w, z, l);                                     // w_q -= conj(L[i][q]) z_i
+    }
+    __syncthreads();
+    const double2 zp = s.z[8 * BLK + p];                         // rows >= 53 read 0
+#pragma unroll
+    for (int bb = 0; bb < BLK; ++bb) cmsub_conj(P[bb], zp, A[BLK][bb]);
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    __shared__ SolveLds s;
+    const int lane = threadIdx.x;
+    const int p = lane >> 3, q = lane & 7;
+    const int64_t f = blockIdx.x;
+    if (f >= a.n) return;
+    const int64_t base = f * a.fs + (int64_t)a.blk * a.bs;
+    {
+        const bool act = lane < NSC;
+        const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
+        const double2 r = act ? ld2(a.rx, base + lane) : make_double2(0, 0);
+        const bool inx = act && ((st->xmask >> lane) & 1ull);
+        s.x[lane] = inx ? t : make_double2(0, 0);
+        s.rx[lane] = r;
+        s.z[lane] = make_double2(0, 0);
+    }
+    __syncthreads();
+    const double ac = st->acoef, bc = st->bcoef;
+    double2 A[RB][RB];
+    double2 xr[RB], xc[RB];
+#pragma unroll
+    for (int aa = 0; aa < RB; ++aa) { xr[aa] = s.x[p + 8 * aa]; xc[aa] = s.x[q + 8 * aa]; }
+#pragma unroll
+    for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+        for (int bb = 0; bb <= aa; ++bb) {
+            const int i = p + 8 * aa, j = q + 8 * bb;
+            double2 v = make_double2(0, 0);
+            if (ac != 0.0 && i < NSC && j < NSC) {
+                const double2 c = ld2(st->C, i * NSC + j);
+                v = cscale(cmul(cmul(xr[aa], c), cconj(xc[bb])), ac);
+            }
+            if (i == j && i < NSC) v.x += bc;
+            if (aa == RB - 1 && i == NSC && j < NSC) v = cconj(s.rx[j]);   // bordered rx row
+            A[aa][bb] = v;
+        }
+    chol_panel<0>(A, s, p, q, lane);
+    chol_panel<1>(A, s, p, q, lane);
+    chol_panel<2>(A, s, p, q, lane);
+    chol_panel<3>(A, s, p, q, lane);
+    chol_panel<4>(A, s, p, q, lane);
+    chol_panel<5>(A, s, p, q, lane);
+    chol_panel<6>(A, s, p, q, lane);
+    // row 53 now holds conj(y), y = L^-1 rx
+    double2 P[RB];
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) P[bb] = (p == 5) ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
+    back_block<6>(A, P, s, p, q, lane);
+    back_block<5>(A, P, s, p, q, lane);
+    back_block<4>(A, P, s, p, q, lane);
+    back_block<3>(A, P, s, p, q, lane);
+    back_block<2>(A, P, s, p, q, lane);
+    back_block<1>(A, P, s, p, q, lane);
+    back_block<0>(A, P, s, p, q, lane);
+    if (lane < NSC) st2(a.w, f * a.ws + lane, cmul(s.x[lane], s.z[lane]));
+}
+
+// =====================================================================
+// H = C W on f64 MFMA.  v_mfma_f64_16x16x4_f64: lane l supplies
+// A[m = l&15][k = l>>4], B[k = l>>4][n = l&15]; D[m = (l>>4) + 4r][n = l&15].
+// Here m = frame (16 per tile), k = input subcarrier j, n = output
+// subcarrier i; complex = 4 real MFMAs.  W may alias H: every W fragment of a
+// tile is loaded before the first store of that tile.
+// =====================================================================
+typedef double v4d __attribute__((ext_vector_type(4)));
+constexpr int KSTEPS = 14;   // 56 >= 53
+constexpr int APPLY_WAVES = 4;
+
+__global__ __launch_bounds__(256) void mmse_apply_kernel(const State *__restrict__ st, const double *W, double *H,
+                                                         int64_t stride, int64_t n)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
+    if (f0 >= n) return;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t fa = f0 + ml;
+    double ar[KSTEPS], ai[KSTEPS], nai[KSTEPS];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        double2 v = (fa < n && j < NSC) ? ld2(W, fa * stride + j) : make_double2(0, 0);
+        ar[s] = v.x; ai[s] = v.y; nai[s] = -v.y;
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int i = 16 * nt + ml;
+        v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl;
+            const double2 c = (i < NSC && j < NSC) ? ld2(st->C, i * NSC + j) : make_double2(0, 0);
+            accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
+            accr = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[s], c.y, accr, 0, 0, 0);
+            acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
+            acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
+        }
+        if (i < NSC) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t fr = f0 + kl + 4 * r;
+                if (fr < n) st2(H, fr * stride + i, make_double2(accr[r], acci[r]));
+            }
+        }
+    }
+}
+
+// =====================================================================
+// Synthetic frames: splitmix64 counter RNG keyed by (seed, frame, stream).
+// =====================================================================
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ double u01(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+// approximately N(0,1): Irwin-Hall of 4 uniforms, unit variance
+__device__ __forceinline__ double gauss(uint64_t key)
+{
+    const double s = u01(mix64(key)) + u01(mix64(key ^ 0x1111)) + u01(mix64(key ^ 0x2222)) + u01(mix64(key ^ 0x3333));
+    return (s - 2.0) * 1.7320508075688772;
+}
+
+// 802.11 pilot polarity p_0..p_14 (IEEE 802.11-2016 17.3.5.10) and pilot base.
+__constant__ double c_polarity[NBLK] = {1, 1, 1, 1, -1, -1, -1, 1, -1, -1, -1, -1, 1, 1, -1};
+__constant__ double c_pilot_base[4] = {1, 1, 1, -1};
+constexpr int NTAP = 6;
+
+__global__ __launch_bounds__(256) void synth_kernel(SynthArgs a, const double *__restrict__ tx_pre)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t fl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (fl >= a.n || lane >= NSC) return;
+    const int k = lane;
+    const uint64_t fg = (uint64_t)(a.first + fl);
+    const uint64_t key = mix64(a.seed ^ mix64(fg));
+    double2 h;
+    if (a.h_shared) {
+        h = ld2(a.h_shared, k);
+    } else {
+        h = make_double2(0, 0);
+        double norm = 0;
+        for (int t = 0; t < NTAP; t++) norm += exp(-0.5 * t);
+        const double g0 = 0.0105 / sqrt(norm);
+        for (int t = 0; t < NTAP; t++) {
+            const double sc = g0 * exp(-0.25 * t) * 0.7071067811865476;
+            const double2 ht = make_double2(sc * gauss(key ^ (0x100 + 2 * t)), sc * gauss(key ^ (0x101 + 2 * t)));
+            double sn, cs;
+            sincospi(-2.0 * t * (k - 26) / 64.0, &sn, &cs);
+            h = cadd(h, cmul(ht, make_double2(cs, sn)));
+        }
+    }
+    const double sig = sqrt(a.ow2 * 0.5);
+    int pidx = -1;
+#pragma unroll
+    for (int pp = 0; pp < 4; pp++) if (k == PILOT[pp]) pidx = pp;
+    for (int b = 0; b < NBLK; b++) {
+        double tv;
+        if (k == 26) tv = 0.0;
+        else if (pidx >= 0) tv = a.amp * c_pilot_base[pidx] * c_polarity[b];
+        else tv = (mix64(key ^ (0x10000ull + (uint64_t)(b * 64 + k))) & 1) ? a.amp : -a.amp;
+        const double2 t = make_double2(tv, 0);
+        const uint64_t nk = key ^ (0x40000ull + (uint64_t)(b * 64 + k) * 2);
+        const double2 r = cadd(cmul(h, t), make_double2(sig * gauss(nk), sig * gauss(nk ^ 0x5555)));
+        const int64_t o = fl * a.fs + (int64_t)b * a.bs + k;
+        if (a.tx) st2(a.tx, o, t);
+        st2(a.rx, o, r);
+    }
+    if (a.rx_pre) {
+        const double2 tp = ld2(tx_pre, k);
+        const uint64_t nk = key ^ 0x80000ull ^ (uint64_t)k;
+        const double sp = sig * 0.7071067811865476;
+        st2(a.rx_pre, fl * a.ps + k, cadd(cmul(h, tp), make_double2(sp * gauss(nk), sp * gauss(nk ^ 0x5555))));
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP; }
+
+int launch_ls(const State *st, const LsArgs &a, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    int64_t waves = a.n;
+    int64_t blocks = (waves + LS_WAVES - 1) / LS_WAVES;
+    if (blocks > 256 * 16) blocks = 256 * 16;    // grid-stride the rest
+    hipLaunchKernelGGL(ls_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    if (a.n > 0x7fffffffll) return WCE_EINVAL;
+    hipLaunchKernelGGL(mmse_solve_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream)
+{
+    if (n <= 0) return WCE_OK;
+    const int64_t tiles = (n + 15) / 16;
+    const int64_t blocks = (tiles + APPLY_WAVES - 1) / APPLY_WAVES;
+    hipLaunchKernelGGL(mmse_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, W, H,
+                       stride, n);
+    return hip_status(hipGetLastError());
+}
+
+int launch_synth(const State *st, const SynthArgs &a, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    const int64_t blocks = (a.n + 3) / 4;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, st->tx_pre);
+    return hip_status(hipGetLastError());
+}
+
+}  // namespace wce

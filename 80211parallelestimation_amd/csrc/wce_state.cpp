@@ -1,0 +1,264 @@
+// wce_state.cpp -- host-side construction of the shared (frame-independent)
+// estimator state, compiled by g++ so that 80-bit long double _Complex
+// arithmetic lowers to the same libgcc __mulxc3/__divxc3 calls the reference
+// uses.  Frame-independent work lives here; per-frame work is on the GPU.
+//
+//   F            main.c:18-26
+//   invF         utils.c:141-170 (inverse), 440-459 (GetMinor),
+//                543-569 (determinant_impl_rec): adjugate with an unpivoted
+//                Schur determinant.  Only accurate to ~1.5e-7 relative, and
+//                the REF MMSE inherits that error, so parity at 1e-10 needs
+//                these exact 80-bit values: they are recomputed with the
+//                reference's operation order (bit-identical, tested).
+//   H_LT         main.c:66-75
+//   C_ref        main.c:183-203: F * ((invF*H_LS) q^T) * FH
+//   C_txt        WiFi_channel_estimation_PS_MMSE.m:20-27
+//   sinc table   main.c:135-143 + utils.c:727-733
+#include "wce_internal.h"
+
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+extern "C" __complex__ double cexp(__complex__ double);
+
+namespace wce {
+
+typedef __complex__ long double cld;
+
+static inline cld mk(long double r, long double i) { cld z; __real__ z = r; __imag__ z = i; return z; }
+static inline cld from(const ldc &a) { return mk(a.re, a.im); }
+static inline ldc to(cld z) { ldc a; a.re = __real__ z; a.im = __imag__ z; return a; }
+// glibc creal/cimag take double _Complex: the reference's creal(x) rounds to double.
+static inline double creal_d(cld z) { return (double)__real__ z; }
+static inline double cimag_d(cld z) { return (double)__imag__ z; }
+
+void host_fmatrix(ldc *F)
+{
+    // -2*I*PI*t*f/SAMPUTIL with I = 1.0iF: the real part is -0.0 for every
+    // (t, f); the imaginary part is ((-2*PI)*t*f)/53 evaluated in double.
+    for (int f = 0; f < NSC; f++)
+        for (int t = 0; t < NSC; t++) {
+            __complex__ double arg;
+            __real__ arg = -0.0;
+            __imag__ arg = ((-2.0 * M_PI) * (double)t * (double)f) / (double)NSC;
+            __complex__ double e = cexp(arg);
+            F[t * NSC + f].re = __real__ e;
+            F[t * NSC + f].im = __imag__ e;
+        }
+}
+
+// determinant_impl_rec: det = m00 * det(S), S_ij = m_ij - m_i0*m_0j/m_00.
+static cld det_schur(const cld *m, int order, cld *scratch)
+{
+    if (order == 1) return m[0];
+    if (order == 2) return m[0] * m[3] - m[1] * m[2];
+    const int s = order - 1;
+    cld *sub = scratch;
+    const cld pivot = m[0];
+    for (int i = 1; i < order; i++) {
+        const cld mi0 = m[i * order];
+        for (int j = 1; j < order; j++)
+            sub[(i - 1) * s + (j - 1)] = m[i * order + j] - (mi0 * m[j] / pivot);
+    }
+    return pivot * det_schur(sub, s, scratch + (size_t)s * s);
+}
+
+static size_t schur_scratch(int order)
+{
+    size_t t = 1;
+    for (int s = order - 1; s >= 1; s--) t += (size_t)s * s;
+    return t;
+}
+
+void host_inverse_cofactor(const ldc *Ain, int n, ldc *Y, int nthreads)
+{
+    std::vector<cld> A(n * n);
+    for (int i = 0; i < n * n; i++) A[i] = from(Ain[i]);
+    std::vector<cld> scratch(schur_scratch(n));
+    const cld one = mk(1.0L, 0.0L);
+    const cld det = one / det_schur(A.data(), n, scratch.data());
+    const int m = n - 1;
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> pool;
+    for (int w = 0; w < nthreads; w++) {
+        pool.emplace_back([&, w]() {
+            std::vector<cld> minor((size_t)m * m), scr(schur_scratch(m));
+            for (int c = w; c < n * n; c += nthreads) {
+                const int j = c / n, i = c % n;  // cofactor of A(j, i) -> Y[i][j]
+                int rc = 0;
+                for (int r = 0; r < n; r++) {
+                    if (r == j) continue;
+                    int cc = 0;
+                    for (int col = 0; col < n; col++) {
+                        if (col == i) continue;
+                        minor[rc * m + cc++] = A[r * n + col];
+                    }
+                    rc++;
+                }
+                cld v = det * det_schur(minor.data(), m, scr.data());
+                if ((i + j) % 2 == 1) v = -1.0L * v;
+                Y[i * n + j] = to(v);
+            }
+        });
+    }
+    for (auto &t : pool) t.join();
+}
+
+static std::once_flag g_invF_once;
+static ldc g_F[NSC * NSC], g_invF[NSC * NSC];
+
+static void compute_reference_invF()
+{
+    host_fmatrix(g_F);
+    unsigned hw = std::thread::hardware_concurrency();
+    int nt = hw ? (int)std::min(hw, 16u) : 4;
+    host_inverse_cofactor(g_F, NSC, g_invF, nt);
+}
+
+const ldc *host_reference_invF()
+{
+    std::call_once(g_invF_once, compute_reference_invF);
+    return g_invF;
+}
+
+const ldc *host_reference_F()
+{
+    std::call_once(g_invF_once, compute_reference_invF);
+    return g_F;
+}
+
+void host_lt_ls(const ldc *tx_pre, const ldc *rx_pre, ldc *H)
+{
+    for (int k = 0; k < NSC; k++) {
+        if (k == 26) { H[k].re = 0; H[k].im = 0; continue; }
+        const cld tx = from(tx_pre[k]), rx = from(rx_pre[k]);
+        const cld c = mk((long double)(creal_d(tx) - cimag_d(tx)), 0.0L);  // real "conj" (main.c:69)
+        H[k] = to((c * rx) / (c * tx));
+    }
+}
+
+// multiply() of utils.c:16-31 for an (r x k) * (k x c) product.
+static void mat_mul(const cld *M1, int r1, int c1, const cld *M2, int c2, cld *res)
+{
+    for (int c = 0; c < r1; c++)
+        for (int d = 0; d < c2; d++) {
+            cld sum = mk(0, 0);
+            for (int k = 0; k < c1; k++) sum = sum + M1[c * c1 + k] * M2[k * c2 + d];
+            res[c * c2 + d] = sum;
+        }
+}
+
+int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS, const ldc *tx_pre,
+                     double ow2, int mode)
+{
+    if (mode != WCE_MMSE_REF && mode != WCE_MMSE_TEXTBOOK) return WCE_EINVAL;
+    std::memset(st, 0, sizeof(State));
+    const int n = NSC;
+    std::vector<cld> F(n * n), C(n * n);
+    for (int i = 0; i < n * n; i++) F[i] = from(Fl[i]);
+    if (mode == WCE_MMSE_REF) {
+        std::vector<cld> invF(n * n), FH(n * n), Rhh(n * n), t1(n * n), g(n), h(n);
+        for (int i = 0; i < n * n; i++) invF[i] = from(invFl[i]);
+        for (int i = 0; i < n; i++) h[i] = from(H_LS[i]);
+        for (int r = 0; r < n; r++)   // hermitian(): transpose of the real value re - im (utils.c:3-7)
+            for (int c = 0; c < n; c++)
+                FH[c * n + r] = mk((long double)(creal_d(F[r * n + c]) - cimag_d(F[r * n + c])), 0.0L);
+        mat_mul(invF.data(), n, n, h.data(), 1, g.data());            // main.c:187
+        for (int r = 0; r < n; r++)                                      // main.c:188-189
+            for (int c = 0; c < n; c++)
+                Rhh[r * n + c] = g[r] * mk((long double)(creal_d(g[c]) - cimag_d(g[c])), 0.0L);
+        mat_mul(Rhh.data(), n, n, FH.data(), n, t1.data());            // main.c:191
+        mat_mul(F.data(), n, n, t1.data(), n, C.data());               // main.c:203 (F*Rhy, X4 applied per frame)
+        st->acoef = 0.0;                 // addition() returns Id+Id (utils.c:117): Ryy = 2 ow2 I
+        st->bcoef = 2.0 * ow2;
+        st->xmask = (1ull << WCE_P0) | (1ull << WCE_P1) | (1ull << WCE_P2) | (1ull << WCE_P3);
+    } else {
+        std::vector<cld> hh(n), Fh(n);
+        for (int t = 0; t < n; t++) {    // ifft(H_LS, 53) = conj(F) H / 53
+            cld s = mk(0, 0);
+            for (int k = 0; k < n; k++) {
+                cld fc = F[t * n + k];
+                __imag__ fc = -__imag__ fc;
+                s = s + fc * from(H_LS[k]);
+            }
+            hh[t] = s / mk((long double)n, 0.0L);
+        }
+        mat_mul(F.data(), n, n, hh.data(), 1, Fh.data());
+        for (int i = 0; i < n; i++)      // F (h h') F' = (F h)(F h)'
+            for (int j = 0; j < n; j++) {
+                cld cj = Fh[j];
+                __imag__ cj = -__imag__ cj;
+                C[i * n + j] = Fh[i] * cj;
+            }
+        st->acoef = 1.0;
+        st->bcoef = ow2;
+        st->xmask = (1ull << NSC) - 1;
+    }
+    for (int i = 0; i < n * n; i++) {
+        st->C[2 * i] = (double)__real__ C[i];
+        st->C[2 * i + 1] = (double)__imag__ C[i];
+    }
+    for (int k = 0; k < n; k++) {
+        st->h_lt[2 * k] = (double)H_LS[k].re;
+        st->h_lt[2 * k + 1] = (double)H_LS[k].im;
+        st->tx_pre[2 * k] = (double)tx_pre[k].re;
+        st->tx_pre[2 * k + 1] = (double)tx_pre[k].im;
+    }
+    const long double delta = PILOT[1] - PILOT[0];
+    for (int p = 0; p < 4; p++)
+        for (int k = 0; k < n; k++) {
+            double a = (k - PILOT[p]) / delta;   // main.c:136-139 (long double -> double)
+            st->sinc[p][k] = a != 0 ? std::sin(M_PI * a) / (M_PI * a) : 1.0;
+        }
+    st->ow2 = ow2;
+    st->mode = mode;
+    st->magic = STATE_MAGIC;
+    return WCE_OK;
+}
+
+}  // namespace wce
+
+// Debug hooks for the parity tests (not in wce.h): the 80-bit invF / F as
+// {re, im} long double pairs, n = 53.
+extern "C" int wce_debug_reference_invF(long double *out)
+{
+    const wce::ldc *v = wce::host_reference_invF();
+    for (int i = 0; i < wce::NSC * wce::NSC; i++) { out[2 * i] = v[i].re; out[2 * i + 1] = v[i].im; }
+    return 0;
+}
+
+extern "C" int wce_debug_reference_F(long double *out)
+{
+    const wce::ldc *v = wce::host_reference_F();
+    for (int i = 0; i < wce::NSC * wce::NSC; i++) { out[2 * i] = v[i].re; out[2 * i + 1] = v[i].im; }
+    return 0;
+}
+
+// Host-only state build (no device): the shared state wce_ctx_create would
+// upload, for CPU parity tests.  C: 53*53 {re,im}, h_lt: 53, sinc: 4*53.
+extern "C" int wce_debug_build_state(const double *tx_pre, const double *rx_pre, double ow2, int mode, double *C,
+                                     double *h_lt, double *sinc, double *ab, unsigned long long *xmask)
+{
+    using namespace wce;
+    ldc txl[NSC], rxl[NSC], hlt[NSC];
+    for (int k = 0; k < NSC; k++) {
+        txl[k].re = tx_pre[2 * k]; txl[k].im = tx_pre[2 * k + 1];
+        rxl[k].re = rx_pre[2 * k]; rxl[k].im = rx_pre[2 * k + 1];
+    }
+    host_lt_ls(txl, rxl, hlt);
+    State *st = new State;
+    int rc = host_build_state(st, host_reference_F(), host_reference_invF(), hlt, txl, ow2, mode);
+    if (rc == WCE_OK) {
+        if (C) std::memcpy(C, st->C, sizeof(st->C));
+        if (h_lt) std::memcpy(h_lt, st->h_lt, sizeof(double) * 2 * NSC);
+        if (sinc)
+            for (int p = 0; p < 4; p++) std::memcpy(sinc + p * NSC, st->sinc[p], sizeof(double) * NSC);
+        if (ab) { ab[0] = st->acoef; ab[1] = st->bcoef; }
+        if (xmask) *xmask = st->xmask;
+    }
+    delete st;
+    return rc;
+}

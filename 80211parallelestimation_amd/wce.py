@@ -1,0 +1,388 @@
+"""Python host binding of libwce.so (the C ABI in include/wce.h).
+
+Two layers, mirroring the C side:
+
+* the reference's five entry points (main.c:4-8) with the same names and
+  argument meaning -- one frame, host arrays, results written into H_EST --
+  implemented by the compat shims in libwce.so (include/wce_compat.h);
+* the batched engine: :class:`Context` (shared state on one device),
+  :class:`DeviceArray` (HBM buffers), :meth:`Context.estimate` over B frames.
+
+There is no CPU fallback: every compute call goes through the gfx950
+kernels and raises :class:`WceError` if the library or the device is absent.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_double, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+NSC = 53          # SAMPUTIL   (utils.h:13)
+NBLK = 15         # OFDMBLK    (utils.h:15)
+DC = 26           # main.c:74
+PILOTS = (5, 19, 33, 47)   # utils.h:16-19
+
+LT_LS = 1 << 0
+PS_LINEAR = 1 << 1
+PS_CUBIC = 1 << 2
+PS_SINC = 1 << 3
+PS_MMSE = 1 << 4
+EQUALIZE = 1 << 5
+LS_ALL = 0xF
+ALL = 0x3F
+
+MMSE_REF = 0
+MMSE_TEXTBOOK = 1
+
+STATUS = {0: "ok", -1: "invalid argument", -2: "HIP error", -3: "out of memory",
+          -4: "context state not ready", -5: "no gfx950 device"}
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwce.so")
+
+
+class WceError(RuntimeError):
+    def __init__(self, code, where=""):
+        msg = STATUS.get(code, f"error {code}")
+        detail = ""
+        if _lib is not None:
+            try:
+                detail = _lib.wce_last_error().decode()
+            except Exception:  # pragma: no cover
+                detail = ""
+        super().__init__(f"{where}: {msg}" + (f" ({detail})" if detail else ""))
+        self.code = code
+
+
+class Complex(ctypes.Structure):
+    _fields_ = [("re", c_double), ("im", c_double)]
+
+
+class Frames(ctypes.Structure):
+    """struct wce_frames (include/wce.h)."""
+    _fields_ = [("tx", c_void_p), ("rx", c_void_p), ("rx_pre", c_void_p), ("tx_pre", c_void_p),
+                ("frame_stride", c_int64), ("block_stride", c_int64), ("pre_stride", c_int64),
+                ("n_frames", c_int64), ("block", c_int32), ("reserved", c_int32)]
+
+
+class Outputs(ctypes.Structure):
+    """struct wce_outputs (include/wce.h)."""
+    _fields_ = [("lt_ls", c_void_p), ("ps_linear", c_void_p), ("ps_cubic", c_void_p), ("ps_sinc", c_void_p),
+                ("ps_mmse", c_void_p), ("eq", c_void_p), ("out_stride", c_int64),
+                ("eq_frame_stride", c_int64), ("eq_block_stride", c_int64), ("eq_source", c_uint32),
+                ("reserved", c_uint32)]
+
+
+_lib = None
+
+# (name, argtypes) for every symbol include/wce.h and include/wce_compat.h declare
+ABI = {
+    "wce_ctx_create": [POINTER(c_void_p), c_int, c_void_p, c_void_p, c_double, c_int],
+    "wce_ctx_create_empty": [POINTER(c_void_p), c_int],
+    "wce_ctx_destroy": [c_void_p],
+    "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
+    "wce_ctx_mark_ready": [c_void_p],
+    "wce_ctx_get_shared": [c_void_p, c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)],
+    "wce_estimate": [c_void_p, POINTER(Frames), POINTER(Outputs), c_uint32, c_void_p],
+    "wce_mmse_solve": [c_void_p, POINTER(Frames), c_void_p, c_int64, c_void_p],
+    "wce_mmse_apply": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p],
+    "wce_synth_frames": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                         c_uint64, c_void_p, c_double, c_double, c_void_p],
+    "wce_device_count": [POINTER(c_int)],
+    "wce_set_device": [c_int],
+    "wce_malloc": [POINTER(c_void_p), c_size_t],
+    "wce_free": [c_void_p],
+    "wce_memcpy_htod": [c_void_p, c_void_p, c_size_t],
+    "wce_memcpy_dtoh": [c_void_p, c_void_p, c_size_t],
+    "wce_memset": [c_void_p, c_int, c_size_t],
+    "wce_stream_create": [POINTER(c_void_p)],
+    "wce_stream_destroy": [c_void_p],
+    "wce_stream_synchronize": [c_void_p],
+    "wce_event_create": [POINTER(c_void_p)],
+    "wce_event_destroy": [c_void_p],
+    "wce_event_record": [c_void_p, c_void_p],
+    "wce_event_elapsed_ms": [POINTER(ctypes.c_float), c_void_p, c_void_p],
+    "wce_last_error": [],
+    "wce_version": [],
+    "wce_compat_last_status": [],
+    "WiFi_channel_estimation_LT_LS": [c_void_p, c_void_p, c_void_p],
+    "WiFi_channel_estimation_PS_Linear": [c_void_p, c_void_p, c_void_p],
+    "WiFi_channel_estimation_PS_Cubic": [c_void_p, c_void_p, c_void_p],
+    "WiFi_channel_estimation_PS_Sinc": [c_void_p, c_void_p, c_void_p],
+    "WiFi_channel_estimation_PS_MMSE": [c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p],
+}
+_VOID = {"WiFi_channel_estimation_LT_LS", "WiFi_channel_estimation_PS_Linear", "WiFi_channel_estimation_PS_Cubic",
+         "WiFi_channel_estimation_PS_Sinc", "WiFi_channel_estimation_PS_MMSE"}
+_STR = {"wce_last_error", "wce_version"}
+
+
+def load(path: str = LIB_PATH):
+    """Load libwce.so (in-tree build).  Raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise WceError(-5, f"libwce.so not built at {path}; run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    for name, args in ABI.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = None if name in _VOID else (ctypes.c_char_p if name in _STR else c_int)
+    _lib = lib
+    return lib
+
+
+def _check(rc, where):
+    if rc != 0:
+        raise WceError(rc, where)
+
+
+def device_count() -> int:
+    n = c_int(0)
+    _check(load().wce_device_count(byref(n)), "wce_device_count")
+    return n.value
+
+
+def _as_c128(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.complex128))
+
+
+class DeviceArray:
+    """A complex128 buffer in HBM (owned)."""
+
+    def __init__(self, shape, dtype=np.complex128, zero=False):
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        self.ptr = c_void_p()
+        _check(load().wce_malloc(byref(self.ptr), max(self.nbytes, 16)), "wce_malloc")
+        if zero:
+            _check(_lib.wce_memset(self.ptr, 0, max(self.nbytes, 16)), "wce_memset")
+
+    @classmethod
+    def from_numpy(cls, a):
+        a = np.ascontiguousarray(a)
+        d = cls(a.shape, a.dtype)
+        if d.nbytes:
+            _check(_lib.wce_memcpy_htod(d.ptr, a.ctypes.data_as(c_void_p), d.nbytes), "wce_memcpy_htod")
+        return d
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        if self.nbytes:
+            _check(_lib.wce_memcpy_dtoh(out.ctypes.data_as(c_void_p), self.ptr, self.nbytes), "wce_memcpy_dtoh")
+        return out
+
+    def free(self):
+        if self.ptr is not None and self.ptr.value:
+            _lib.wce_free(self.ptr)
+            self.ptr = c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # pragma: no cover
+            pass
+
+    @property
+    def addr(self) -> int:
+        return self.ptr.value or 0
+
+
+def _addr(x):
+    if x is None:
+        return None
+    if isinstance(x, DeviceArray):
+        return x.addr
+    return int(x)
+
+
+class Context:
+    """wce_ctx: shared (frame-independent) state resident on one device."""
+
+    def __init__(self, tx_pre=None, rx_pre=None, ow2=None, mode=MMSE_REF, device=0, empty=False):
+        lib = load()
+        self.handle = c_void_p()
+        self.device = device
+        self.mode = mode
+        if empty:
+            _check(lib.wce_ctx_create_empty(byref(self.handle), device), "wce_ctx_create_empty")
+            return
+        tp, rp = _as_c128(tx_pre), _as_c128(rx_pre)
+        if tp.shape != (NSC,) or rp.shape != (NSC,):
+            raise ValueError("tx_pre / rx_pre must hold 53 subcarriers")
+        _check(lib.wce_ctx_create(byref(self.handle), device, tp.ctypes.data_as(c_void_p),
+                                  rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_ctx_create")
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            _lib.wce_ctx_destroy(self.handle)
+            self.handle = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    def state(self):
+        ptr, nb = c_void_p(), c_size_t()
+        _check(_lib.wce_ctx_state(self.handle, byref(ptr), byref(nb)), "wce_ctx_state")
+        return ptr.value, nb.value
+
+    def mark_ready(self):
+        _check(_lib.wce_ctx_mark_ready(self.handle), "wce_ctx_mark_ready")
+
+    def shared(self):
+        h = np.zeros(NSC, np.complex128)
+        C = np.zeros((NSC, NSC), np.complex128)
+        a, b = c_double(), c_double()
+        _check(_lib.wce_ctx_get_shared(self.handle, h.ctypes.data_as(c_void_p), C.ctypes.data_as(c_void_p),
+                                       byref(a), byref(b)), "wce_ctx_get_shared")
+        return h, C, a.value, b.value
+
+    # ---------------------------------------------------------------- batched
+    @staticmethod
+    def frames(tx, rx, n_frames, frame_stride=NBLK * NSC, block_stride=NSC, rx_pre=None, pre_stride=NSC,
+               tx_pre=None, block=0) -> Frames:
+        return Frames(_addr(tx), _addr(rx), _addr(rx_pre), _addr(tx_pre), frame_stride, block_stride, pre_stride,
+                      n_frames, block, 0)
+
+    def estimate(self, frames: Frames, outputs: Outputs, mask: int, stream=None):
+        _check(_lib.wce_estimate(self.handle, byref(frames), byref(outputs), mask, stream), "wce_estimate")
+
+    def mmse_solve(self, frames: Frames, W, w_stride=NSC, stream=None):
+        _check(_lib.wce_mmse_solve(self.handle, byref(frames), _addr(W), w_stride, stream), "wce_mmse_solve")
+
+    def mmse_apply(self, W, H, n_frames, stride=NSC, stream=None):
+        _check(_lib.wce_mmse_apply(self.handle, _addr(W), _addr(H), stride, n_frames, stream), "wce_mmse_apply")
+
+    def synth(self, tx, rx, rx_pre, n_frames, first_frame=0, seed=0x80211, h_shared=None, amplitude=8.8753,
+              ow2=9.6172e-08, frame_stride=NBLK * NSC, block_stride=NSC, pre_stride=NSC, stream=None):
+        _check(_lib.wce_synth_frames(self.handle, _addr(tx), _addr(rx), _addr(rx_pre), frame_stride, block_stride,
+                                     pre_stride, first_frame, n_frames, seed, _addr(h_shared), amplitude, ow2,
+                                     stream), "wce_synth_frames")
+
+    def estimate_host(self, tx, rx, rx_pre=None, mask=ALL, block=0, eq_source=PS_LINEAR):
+        """Convenience: host numpy frames [B][15][53] -> dict of host outputs."""
+        tx, rx = _as_c128(tx), _as_c128(rx)
+        B = tx.shape[0]
+        if tx.shape != (B, NBLK, NSC) or rx.shape != tx.shape:
+            raise ValueError("tx/rx must be [B][15][53] complex")
+        dtx, drx = DeviceArray.from_numpy(tx), DeviceArray.from_numpy(rx)
+        dpre = DeviceArray.from_numpy(_as_c128(rx_pre)) if rx_pre is not None else None
+        names = [("lt_ls", LT_LS), ("ps_linear", PS_LINEAR), ("ps_cubic", PS_CUBIC), ("ps_sinc", PS_SINC),
+                 ("ps_mmse", PS_MMSE)]
+        outs = {n: DeviceArray((B, NSC), zero=True) for n, bit in names if mask & bit}
+        deq = DeviceArray((B, NBLK, NSC), zero=True) if mask & EQUALIZE else None
+        o = Outputs(*[(outs[n].addr if n in outs else None) for n, _ in names],
+                    deq.addr if deq is not None else None, NSC, NBLK * NSC, NSC, eq_source, 0)
+        fr = self.frames(dtx, drx, B, rx_pre=dpre, block=block)
+        self.estimate(fr, o, mask)
+        synchronize()
+        res = {n: outs[n].numpy() for n in outs}
+        if deq is not None:
+            res["eq"] = deq.numpy()
+        return res
+
+
+def synchronize(stream=None):
+    _check(load().wce_stream_synchronize(stream), "wce_stream_synchronize")
+
+
+class Stream:
+    def __init__(self):
+        self.handle = c_void_p()
+        _check(load().wce_stream_create(byref(self.handle)), "wce_stream_create")
+
+    def synchronize(self):
+        _check(_lib.wce_stream_synchronize(self.handle), "wce_stream_synchronize")
+
+    def __del__(self):
+        try:
+            if self.handle.value:
+                _lib.wce_stream_destroy(self.handle)
+        except Exception:  # pragma: no cover
+            pass
+
+
+class Event:
+    def __init__(self):
+        self.handle = c_void_p()
+        _check(load().wce_event_create(byref(self.handle)), "wce_event_create")
+
+    def record(self, stream=None):
+        s = stream.handle if isinstance(stream, Stream) else stream
+        _check(_lib.wce_event_record(self.handle, s), "wce_event_record")
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = ctypes.c_float()
+        _check(_lib.wce_event_elapsed_ms(byref(ms), self.handle, end.handle), "wce_event_elapsed_ms")
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.handle.value:
+                _lib.wce_event_destroy(self.handle)
+        except Exception:  # pragma: no cover
+            pass
+
+
+# ------------------------------------------------------------------------
+# The reference's entry points (main.c:4-8): same names, same argument
+# meaning, results written into H_EST (53 complex).  Arrays are numpy
+# clongdouble (= long double _Complex) or anything convertible.
+# ------------------------------------------------------------------------
+def _ld(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.clongdouble))
+
+
+def _call_compat(name, *arrays, out):
+    lib = load()
+    ins = [_ld(a) for a in arrays]
+    if any(a.shape[0] < NSC for a in ins):
+        raise ValueError("estimator inputs need 53 subcarriers")
+    res = np.zeros(NSC, np.clongdouble)
+    getattr(lib, name)(*[a.ctypes.data_as(c_void_p) for a in ins], res.ctypes.data_as(c_void_p))
+    _check(lib.wce_compat_last_status(), name)
+    if out is not None:
+        out[:NSC] = res
+    return res
+
+
+def WiFi_channel_estimation_LT_LS(tx_pre, rx_pre, H_EST=None):
+    """main.c:66-75 on the GPU."""
+    return _call_compat("WiFi_channel_estimation_LT_LS", tx_pre, rx_pre, out=H_EST)
+
+
+def WiFi_channel_estimation_PS_Linear(tx_symbols, rx_symbols, H_EST=None):
+    """main.c:77-101 on the GPU."""
+    return _call_compat("WiFi_channel_estimation_PS_Linear", tx_symbols, rx_symbols, out=H_EST)
+
+
+def WiFi_channel_estimation_PS_Cubic(tx_symbols, rx_symbols, H_EST=None):
+    """main.c:103-122 on the GPU."""
+    return _call_compat("WiFi_channel_estimation_PS_Cubic", tx_symbols, rx_symbols, out=H_EST)
+
+
+def WiFi_channel_estimation_PS_Sinc(tx_symbols, rx_symbols, H_EST=None):
+    """main.c:124-146 on the GPU."""
+    return _call_compat("WiFi_channel_estimation_PS_Sinc", tx_symbols, rx_symbols, out=H_EST)
+
+
+def WiFi_channel_estimation_PS_MMSE(tx_symbols, rx_symbols, F, ow2, H_EST_LS, H_EST=None):
+    """main.c:148-212 (REF-repaired) on the GPU.  F: 53x53."""
+    lib = load()
+    tx, rx, hls = _ld(tx_symbols), _ld(rx_symbols), _ld(H_EST_LS)
+    Fm = np.ascontiguousarray(np.asarray(F, dtype=np.clongdouble).reshape(NSC, NSC))
+    rows = (c_void_p * NSC)(*[Fm[i].ctypes.data for i in range(NSC)])
+    res = np.zeros(NSC, np.clongdouble)
+    lib.WiFi_channel_estimation_PS_MMSE(tx.ctypes.data_as(c_void_p), rx.ctypes.data_as(c_void_p),
+                                        ctypes.cast(rows, c_void_p), float(ow2), hls.ctypes.data_as(c_void_p),
+                                        res.ctypes.data_as(c_void_p))
+    _check(lib.wce_compat_last_status(), "WiFi_channel_estimation_PS_MMSE")
+    if H_EST is not None:
+        H_EST[:NSC] = res
+    return res

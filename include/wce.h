@@ -1,0 +1,168 @@
+/*
+ * wce.h -- C ABI of the MI355X 802.11 channel-estimation engine (libwce.so).
+ *
+ * Drop-in boundary for the estimator path of usmandroid/80211ParallelEstimation
+ * (main.c / utils.c).  Plain pointers and sizes only: no HIP or torch types in
+ * the signatures (streams are passed as `void *` hipStream_t, NULL = default
+ * stream).  Every call returns an int status (0 ok, < 0 error); the reference
+ * functions return void and print on dimension mismatch (utils.c:18-19).
+ *
+ * Two layers:
+ *   1. the batched API below (wce_ctx_*, wce_estimate, wce_mmse_*) that runs
+ *      B frames resident in HBM through hand-written gfx950 kernels;
+ *   2. include/wce_compat.h: the five reference signatures of main.c:4-8,
+ *      one frame in host memory, implemented on top of layer 1.
+ *
+ * Data layout: complex fp64 is {re, im} (16 B, binary-compatible with C99
+ * double _Complex and hipDoubleComplex).  Frame f, OFDM block b, subcarrier k
+ * lives at base[f*frame_stride + b*block_stride + k] (strides in elements);
+ * the reference's block-major inputs.h layout (tx_symb[53*15]) is
+ * frame_stride = 795, block_stride = 53.
+ */
+#ifndef WCE_H
+#define WCE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WCE_NSC 53   /* SAMPUTIL, utils.h:13 */
+#define WCE_NBLK 15  /* OFDMBLK,  utils.h:15 */
+#define WCE_DC 26    /* main.c:74 H_EST[26] = 0 */
+#define WCE_P0 5     /* utils.h:16-19 pilot subcarriers */
+#define WCE_P1 19
+#define WCE_P2 33
+#define WCE_P3 47
+
+typedef struct { double re, im; } wce_complex;
+
+enum {
+    WCE_OK = 0,
+    WCE_EINVAL = -1,   /* bad argument / shape */
+    WCE_EHIP = -2,     /* HIP runtime error */
+    WCE_ENOMEM = -3,
+    WCE_ESTATE = -4,   /* context has no valid shared state */
+    WCE_ENODEV = -5    /* no usable gfx950 device */
+};
+
+/* estimator mask bits (one per reference entry point, main.c:4-8) */
+#define WCE_EST_LT_LS     (1u << 0)  /* WiFi_channel_estimation_LT_LS     main.c:66  */
+#define WCE_EST_PS_LINEAR (1u << 1)  /* WiFi_channel_estimation_PS_Linear main.c:77  */
+#define WCE_EST_PS_CUBIC  (1u << 2)  /* WiFi_channel_estimation_PS_Cubic  main.c:103 */
+#define WCE_EST_PS_SINC   (1u << 3)  /* WiFi_channel_estimation_PS_Sinc   main.c:124 */
+#define WCE_EST_PS_MMSE   (1u << 4)  /* WiFi_channel_estimation_PS_MMSE   main.c:148 */
+#define WCE_EQUALIZE      (1u << 5)  /* WiFi_Equalization.m (no C original) */
+#define WCE_EST_LS_ALL    (0xFu)
+
+/* MMSE semantics (DESIGN.md "MMSE contract"):
+ *  REF      : main.c:148-212 with the NaN inverse(Ryy) repaired:
+ *             H = C_ref X4 (2 ow2 I)^-1 rx, C_ref = F Rhh FH, X4 = pilots of tx.
+ *  TEXTBOOK : WiFi_channel_estimation_PS_MMSE.m per block:
+ *             H = C X (X C X' + ow2 I)^-1 rx, C = F Rhh F', X = diag(tx).
+ * Both run the same kernel: H = C X (a X C X' + b I)^-1 rx. */
+enum { WCE_MMSE_REF = 0, WCE_MMSE_TEXTBOOK = 1 };
+
+typedef struct wce_ctx wce_ctx;
+
+/* Build the shared state on the host (F, the reference's cofactor invF in
+ * 80-bit long double, H_LT from the shared preamble, the MMSE covariance C,
+ * the sinc table) and upload it to `device`.  tx_pre/rx_pre: the shared
+ * preamble FFTs (53 each, host).  The first call in a process spends
+ * ~0.5 s (8 threads) on invF; later calls reuse it. */
+int wce_ctx_create(wce_ctx **ctx, int device, const wce_complex *tx_pre,
+                   const wce_complex *rx_pre, double ow2, int mmse_mode);
+
+/* A context whose device state is filled later (e.g. by an RCCL broadcast
+ * into the buffer returned by wce_ctx_state). */
+int wce_ctx_create_empty(wce_ctx **ctx, int device);
+int wce_ctx_destroy(wce_ctx *ctx);
+
+/* Device pointer and size of the packed shared state (C, H_LT, tx_pre, sinc
+ * table, MMSE coefficients): the single buffer a multi-GPU run broadcasts
+ * from rank 0.  After writing it externally call wce_ctx_mark_ready. */
+int wce_ctx_state(wce_ctx *ctx, void **device_ptr, size_t *bytes);
+int wce_ctx_mark_ready(wce_ctx *ctx);
+
+/* Copy back the shared vectors (host outputs, may be NULL): H_LT (53),
+ * C (53*53 row-major), and the MMSE coefficients a, b. */
+int wce_ctx_get_shared(wce_ctx *ctx, wce_complex *h_lt, wce_complex *C, double *a, double *b);
+
+typedef struct {
+    const wce_complex *tx;      /* device; tx[f*frame_stride + b*block_stride + k] */
+    const wce_complex *rx;      /* device; same layout as tx */
+    const wce_complex *rx_pre;  /* device; per-frame preamble FFT rx_pre[f*pre_stride + k],
+                                   NULL = use the context's shared H_LT */
+    const wce_complex *tx_pre;  /* device; shared preamble (53), NULL = context's */
+    int64_t frame_stride;
+    int64_t block_stride;
+    int64_t pre_stride;
+    int64_t n_frames;
+    int32_t block;              /* OFDM block read by PS_* / MMSE (main.c:16 uses 0) */
+    int32_t reserved;
+} wce_frames;
+
+typedef struct {
+    wce_complex *lt_ls;         /* device [n_frames][out_stride], NULL = not requested */
+    wce_complex *ps_linear;
+    wce_complex *ps_cubic;
+    wce_complex *ps_sinc;
+    wce_complex *ps_mmse;
+    wce_complex *eq;            /* equalized symbols, eq[f*eq_frame_stride + b*eq_block_stride + k] */
+    int64_t out_stride;         /* >= 53 */
+    int64_t eq_frame_stride;
+    int64_t eq_block_stride;
+    uint32_t eq_source;         /* PS estimate blended with H_LT (WiFi_RX.m:60 uses PS_Linear);
+                                   0 = WCE_EST_PS_LINEAR */
+    uint32_t reserved;
+} wce_outputs;
+
+/* Run the estimators selected in `mask` over all frames, asynchronously on
+ * `stream`.  LS family + equalization: one HBM-streaming kernel; MMSE: the
+ * LDS/register-resident Cholesky solve kernel followed by the MFMA GEMM
+ * (the ps_mmse buffer doubles as the solve->GEMM workspace). */
+int wce_estimate(wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
+                 uint32_t mask, void *stream);
+
+/* The two MMSE stages, exposed for profiling:
+ *   solve: W[f] = X_f (a X_f C X_f' + b I)^-1 rx_f        (FP64 VALU, per frame)
+ *   apply: H[f] = C W[f]                                  (FP64 MFMA batched GEMM)
+ * W and H may alias (in place). */
+int wce_mmse_solve(wce_ctx *ctx, const wce_frames *in, wce_complex *W, int64_t w_stride, void *stream);
+int wce_mmse_apply(wce_ctx *ctx, const wce_complex *W, wce_complex *H, int64_t stride,
+                   int64_t n_frames, void *stream);
+
+/* Synthetic 802.11 frames generated on the device from a counter-based RNG
+ * keyed by (seed, global frame index), so any shard regenerates identical
+ * frames: BPSK data +-A, pilots A*(1,1,1,-1)*p_b (802.11 polarity), DC = 0,
+ * a 6-tap exponential-PDP channel (or h_shared for every frame, if non-NULL),
+ * CN(0, ow2) noise.  rx_pre (may be NULL) = per-frame preamble H*tx_pre + noise/sqrt2. */
+int wce_synth_frames(wce_ctx *ctx, wce_complex *tx, wce_complex *rx, wce_complex *rx_pre,
+                     int64_t frame_stride, int64_t block_stride, int64_t pre_stride,
+                     int64_t first_frame, int64_t n_frames, uint64_t seed,
+                     const wce_complex *h_shared, double amplitude, double ow2, void *stream);
+
+/* ---- thin runtime helpers (so C hosts and tests need no other HIP binding) ---- */
+int wce_device_count(int *count);
+int wce_set_device(int device);
+int wce_malloc(void **ptr, size_t bytes);
+int wce_free(void *ptr);
+int wce_memcpy_htod(void *dst, const void *src, size_t bytes);
+int wce_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+int wce_memset(void *dst, int value, size_t bytes);
+int wce_stream_create(void **stream);
+int wce_stream_destroy(void *stream);
+int wce_stream_synchronize(void *stream);
+int wce_event_create(void **event);
+int wce_event_destroy(void *event);
+int wce_event_record(void *event, void *stream);
+int wce_event_elapsed_ms(float *ms, void *start, void *stop);
+const char *wce_last_error(void);
+const char *wce_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WCE_H */

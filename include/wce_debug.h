@@ -1,0 +1,17 @@
+/* wce_debug.h -- host-only hooks of libwce.so used by the parity tests to
+ * check the 80-bit shared-state precompute without a GPU. */
+#ifndef WCE_DEBUG_H
+#define WCE_DEBUG_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* F and the reference's cofactor invF (utils.c:141-170), 53*53 {re, im} long double pairs */
+int wce_debug_reference_F(long double *out);
+int wce_debug_reference_invF(long double *out);
+/* the State wce_ctx_create builds: C (53*53 {re,im}), H_LT (53), sinc table (4*53), {a, b}, X mask */
+int wce_debug_build_state(const double *tx_pre, const double *rx_pre, double ow2, int mode, double *C,
+                          double *h_lt, double *sinc, double *ab, unsigned long long *xmask);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,111 @@
+// ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (builds oracle/_ref/libref.so).
+//
+// Compiles the reference's own main.c / utils.c from where they lie under
+// /root/reference (never copied) and exposes their estimator functions and
+// matrix helpers through extern "C" entry points, so tests/golden/make_golden.py
+// can produce golden vectors from the real reference code.  Built with
+// g++ -std=gnu++98 against the MPICH headers the image ships in /opt/conda
+// (utils.h includes <mpi.h>); recipe in oracle/Makefile.
+#define main ref_main
+#include "main.c"
+#undef main
+
+#include <stdlib.h>
+
+typedef long double complex ldc;
+
+static ldc **rows(ldc *flat, int n, int m)
+{
+    ldc **r = (ldc **)malloc(sizeof(ldc *) * n);
+    for (int i = 0; i < n; i++) r[i] = flat + (size_t)i * m;
+    return r;
+}
+
+extern "C" {
+
+// inputs.h globals (inputs.h:18,20,75,130,928)
+double refh_ow2(void) { return OW2; }
+void refh_inputs(ldc *tx_pre, ldc *rx_pre, ldc *tx_sym, ldc *rx_sym)
+{
+    for (int i = 0; i < SAMPUTIL; i++) { tx_pre[i] = tx_preamble_fft[i]; rx_pre[i] = rx_preamble_fft[i]; }
+    for (int i = 0; i < SIZESYMBOL; i++) { tx_sym[i] = tx_symb[i]; rx_sym[i] = rx_symb[i]; }
+}
+
+// main.c:18-26 (same expression, evaluated by the reference's compiler settings)
+void refh_fmatrix(ldc *F)
+{
+    for (int f = 0; f < SAMPUTIL; f++)
+        for (int t = 0; t < SAMPUTIL; t++)
+            F[t * SAMPUTIL + f] = cexp(-2 * I * PI * t * f / SAMPUTIL);
+}
+
+void refh_lt_ls(ldc *tx, ldc *rx, ldc *H) { WiFi_channel_estimation_LT_LS(tx, rx, H); }
+void refh_ps_linear(ldc *tx, ldc *rx, ldc *H) { WiFi_channel_estimation_PS_Linear(tx, rx, H); }
+void refh_ps_cubic(ldc *tx, ldc *rx, ldc *H) { WiFi_channel_estimation_PS_Cubic(tx, rx, H); }
+void refh_ps_sinc(ldc *tx, ldc *rx, ldc *H) { WiFi_channel_estimation_PS_Sinc(tx, rx, H); }
+
+// utils.c:141 inverse (cofactor / unpivoted Schur determinant)
+void refh_inverse(ldc *A, int n, ldc *Y)
+{
+    ldc **a = rows(A, n, n), **y = rows(Y, n, n);
+    inverse(a, n, y);
+    free(a); free(y);
+}
+
+// utils.c:543 determinant_impl_rec
+void refh_det(ldc *A, int n, ldc *out)
+{
+    ldc **a = rows(A, n, n);
+    *out = determinant_impl_rec(a, n);
+    free(a);
+}
+
+// The reference's PS_MMSE (main.c:148-212) rebuilt from the reference's own
+// helpers in the same order, with the single repair: invRyy = exact inverse
+// of the diagonal Ryy (the cofactor inverse returns NaN off the diagonal).
+// invF_in != NULL skips the 4 s inverse(F) (pass the reference's own invF).
+void refh_mmse_repaired(ldc *tx_symbols, ldc *rx_symbols, ldc *Fflat, double ow2,
+                        ldc *H_EST_LS, ldc *invF_in, ldc *H_EST_MMSE, ldc *invF_out)
+{
+    const int n = SAMPUTIL;
+    ldc *buf = (ldc *)calloc((size_t)n * n * 12 + 4 * n, sizeof(ldc));
+    ldc **F = rows(Fflat, n, n);
+    ldc **FHermitian = rows(buf + 0 * n * n, n, n), **X4Hermitian = rows(buf + 1 * n * n, n, n);
+    ldc **X4 = rows(buf + 2 * n * n, n, n), **Rhh = rows(buf + 3 * n * n, n, n);
+    ldc **Rhy = rows(buf + 4 * n * n, n, n), **Ryy = rows(buf + 5 * n * n, n, n);
+    ldc **invRyy = rows(buf + 6 * n * n, n, n), **invF = rows(buf + 7 * n * n, n, n);
+    ldc **temp1 = rows(buf + 8 * n * n, n, n), **temp2 = rows(buf + 9 * n * n, n, n);
+    ldc **temp3 = rows(buf + 10 * n * n, n, n), **Id = rows(buf + 11 * n * n, n, n);
+    ldc **rx1 = rows(buf + 12 * n * n, n, 1), **H1 = rows(buf + 12 * n * n + n, n, 1);
+    for (int r = 0; r < n; r++) {
+        for (int c = 0; c < n; c++) {
+            if (r == c && (r == P0 || r == P1 || r == P2 || r == P3)) X4[r][c] = tx_symbols[r];
+            else X4[r][c] = 0.0;
+        }
+        rx1[r][0] = rx_symbols[r];
+        H1[r][0] = H_EST_LS[r];
+    }
+    hermitian(F, n, n, FHermitian);
+    hermitian(X4, n, n, X4Hermitian);
+    if (invF_in) { for (int i = 0; i < n * n; i++) invF[i / n][i % n] = invF_in[i]; }
+    else inverse(F, n, invF);
+    if (invF_out) for (int i = 0; i < n * n; i++) invF_out[i] = invF[i / n][i % n];
+    multiply(invF, n, n, H1, n, 1, temp1);
+    hermitian(temp1, n, n, temp2);      // only row 0 of temp2 is consumed below
+    multiplyVxVeqM(temp1, n, n, temp2, n, n, Rhh);
+    multiply(Rhh, n, n, FHermitian, n, n, temp1);
+    multiply(temp1, n, n, X4, n, n, Rhy);
+    identity(Id, n, ow2);
+    addition(Id, n, n, temp2, n, n, Ryy);
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < n; c++) invRyy[r][c] = (r == c) ? 1.0L / Ryy[r][c] : 0.0L;  // repair
+    multiply(F, n, n, Rhy, n, n, temp1);
+    multiply(invRyy, n, n, rx1, n, 1, temp3);
+    multiply(temp1, n, n, temp3, n, 1, temp2);
+    for (int r = 0; r < n; r++) H_EST_MMSE[r] = temp2[r][0];
+    free(F); free(FHermitian); free(X4Hermitian); free(X4); free(Rhh); free(Rhy); free(Ryy);
+    free(invRyy); free(invF); free(temp1); free(temp2); free(temp3); free(Id); free(rx1); free(H1);
+    free(buf);
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+"""C-ABI boundary checks that need no GPU: libwce.so loads, exports every
+symbol include/*.h declares, its 80-bit host precompute (F, the reference's
+cofactor invF, the MMSE covariance) matches the reference bit for bit, and
+device entry points fail loudly without a gfx950 device."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle_py import N, from_split
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for h in ("wce.h", "wce_compat.h", "wce_debug.h"):
+        src = open(os.path.join(REPO, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", src, flags=re.M):
+            if m.group(1) not in ("if", "defined"):
+                names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol(wce):
+    lib = wce.load()
+    syms = declared_symbols()
+    assert {"wce_estimate", "wce_ctx_create", "WiFi_channel_estimation_PS_MMSE"} <= syms
+    missing = [s for s in sorted(syms) if not hasattr(lib, s)]
+    assert not missing, missing
+    # the Python mirror binds the whole public ABI
+    public = declared_symbols() - {s for s in syms if s.startswith("wce_debug")}
+    assert public <= set(wce.wce.ABI), sorted(public - set(wce.wce.ABI))
+
+
+def test_version_string(wce):
+    assert b"gfx950" in wce.load().wce_version()
+
+
+def _ld_pairs(fn):
+    out = np.zeros(N * N * 2, np.longdouble)
+    assert fn(out.ctypes.data_as(ctypes.c_void_p)) == 0
+    return out[0::2] + 1j * out[1::2].astype(np.clongdouble)
+
+
+def test_host_F_and_invF_bit_exact(wce, golden):
+    lib = wce.load()
+    F = _ld_pairs(lib.wce_debug_reference_F).reshape(N, N)
+    invF = _ld_pairs(lib.wce_debug_reference_invF).reshape(N, N)
+    gF, ginv = from_split(golden["ref"]["F"]), from_split(golden["ref"]["invF"])
+    assert np.array_equal(F.real, gF.real) and np.array_equal(F.imag, gF.imag)
+    assert np.array_equal(invF.real, ginv.real) and np.array_equal(invF.imag, ginv.imag)
+
+
+def build_state(wce, tx_pre, rx_pre, ow2, mode):
+    lib = wce.load()
+    tp = np.ascontiguousarray(tx_pre, np.complex128)
+    rp = np.ascontiguousarray(rx_pre, np.complex128)
+    C = np.zeros((N, N), np.complex128)
+    h = np.zeros(N, np.complex128)
+    s = np.zeros((4, N))
+    ab = np.zeros(2)
+    xm = ctypes.c_ulonglong()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    lib.wce_debug_build_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_int] + \
+        [ctypes.c_void_p] * 4 + [ctypes.POINTER(ctypes.c_ulonglong)]
+    rc = lib.wce_debug_build_state(p(tp), p(rp), float(ow2), mode, p(C), p(h), p(s), p(ab), ctypes.byref(xm))
+    assert rc == 0
+    return C, h, s, ab, xm.value
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_ref_state_bit_exact(wce, oracle, golden, case):
+    """C_ref = F (Rhh FH) from the reference's invF, H_LT from LT_LS: bit-exact
+    against the oracle's long double pipeline rounded to fp64."""
+    r = golden["ref"]
+    C, h, s, ab, xm = build_state(wce, r["pre_tx"][case], r["pre_rx"][case], r["ow2"], wce.MMSE_REF)
+    hls = from_split(r["pre_lt_ls"][case])
+    assert np.array_equal(h, hls.astype(np.complex128))
+    Co = oracle.mmse_ref_cmatrix(from_split(r["F"]), from_split(r["invF"]), hls).astype(np.complex128)
+    assert np.array_equal(C, Co)
+    assert ab[0] == 0.0 and ab[1] == 2 * r["ow2"]
+    assert xm == sum(1 << k for k in (5, 19, 33, 47))
+
+
+def test_textbook_state(wce, oracle, golden):
+    r = golden["ref"]
+    C, h, s, ab, xm = build_state(wce, r["pre_tx"][0], r["pre_rx"][0], r["ow2"], wce.MMSE_TEXTBOOK)
+    Co = oracle.mmse_textbook_cmatrix(from_split(r["F"]), from_split(r["pre_lt_ls"][0])).astype(np.complex128)
+    assert np.abs(C - Co).max() / np.abs(Co).max() < 1e-15
+    assert np.allclose(C, C.conj().T, rtol=0, atol=1e-20)      # Hermitian
+    assert ab[0] == 1.0 and ab[1] == r["ow2"] and xm == (1 << N) - 1
+
+
+def test_sinc_table(wce, golden):
+    r = golden["ref"]
+    _, _, s, _, _ = build_state(wce, r["pre_tx"][0], r["pre_rx"][0], r["ow2"], wce.MMSE_REF)
+    for p, P in enumerate((5, 19, 33, 47)):
+        a = (np.arange(N) - P) / 14.0
+        ref = np.where(a == 0, 1.0, np.sin(np.pi * a) / np.where(a == 0, 1, np.pi * a))
+        assert np.allclose(s[p], ref, rtol=1e-15, atol=1e-17)
+        assert s[p][P] == 1.0
+
+
+def test_no_device_fails_loudly(wce):
+    if wce.device_count() > 0:
+        pytest.skip("a device is present")
+    with pytest.raises(wce.WceError) as e:
+        wce.Context(np.ones(N), np.ones(N), 1e-7)
+    assert e.value.code in (-5, -2)
+    with pytest.raises(wce.WceError):
+        wce.WiFi_channel_estimation_PS_Linear(np.ones(N), np.ones(N))

@@ -1,0 +1,167 @@
+"""The CPU oracle pinned against the reference's own outputs (golden vectors
+produced by the compiled reference, tests/golden/make_golden.py) and against
+the MATLAB workspace matlab.mat.  No GPU needed."""
+import numpy as np
+import pytest
+
+from oracle_py import N, NBLK, PILOTS, from_split, normrel
+
+
+def bits_equal(a, b):
+    a = np.asarray(a, np.clongdouble)
+    b = np.asarray(b, np.clongdouble)
+    return np.array_equal(a.real, b.real) and np.array_equal(a.imag, b.imag)
+
+
+def test_fmatrix_bit_exact(oracle, golden):
+    assert bits_equal(oracle.fmatrix(), from_split(golden["ref"]["F"]))
+
+
+@pytest.mark.parametrize("name", ["ps_linear", "ps_cubic", "ps_sinc"])
+def test_ps_estimators_bit_exact(oracle, golden, name):
+    r = golden["ref"]
+    for f in range(r["frames_tx"].shape[0]):
+        H = getattr(oracle, name)(r["frames_tx"][f], r["frames_rx"][f])
+        assert bits_equal(H, from_split(r[name][f])), (name, f)
+
+
+def test_lt_ls_bit_exact(oracle, golden):
+    r = golden["ref"]
+    for f in range(r["frames_tx"].shape[0]):
+        H = oracle.lt_ls(r["pre_tx"][f % 2], r["pre_rx"][f % 2])
+        assert bits_equal(H, from_split(r["lt_ls"][f]))
+        assert H[26] == 0
+
+
+def test_inverse_cofactor_bit_exact(oracle, golden):
+    invF = oracle.inverse_cofactor(oracle.fmatrix())
+    assert bits_equal(invF, from_split(golden["ref"]["invF"]))
+    # and it is only ~1.5e-7 accurate: exact F^-1 = F^H / 53
+    exact = oracle.fmatrix().conj().T / 53
+    err = np.abs((invF - exact).astype(np.complex128)).max() * 53
+    assert 1e-8 < err < 1e-6
+
+
+def test_mmse_ref_repaired_bit_exact(oracle, golden):
+    r = golden["ref"]
+    F = from_split(r["F"])
+    invF = from_split(r["invF"])
+    for c in range(2):
+        hls = from_split(r["pre_lt_ls"][c])
+        for f in range(r["frames_tx"].shape[0]):
+            H = oracle.mmse_ref_repaired(r["frames_tx"][f], r["frames_rx"][f], F, r["ow2"], hls, invF)
+            assert bits_equal(H, from_split(r["ps_mmse_ref"][c, f])), (c, f)
+
+
+def test_mmse_golden_values(golden):
+    # values quoted in SURVEY 8(c)(i): inputs.h frame
+    r = golden["ref"]
+    m = from_split(r["ps_mmse_ref"][0, 0]).astype(np.complex128)
+    assert abs(m[0] - (1.115539799734874443549e03 - 1.364070362604641952875e03j)) < 1e-9
+    lin = from_split(r["ps_linear"][0]).astype(np.complex128)
+    assert abs(lin[0] - (9.253895176911212610829e-03 - 1.592455267909223567380e-04j)) < 1e-17
+
+
+def test_literal_inverse_is_nan(oracle, golden):
+    """Known answer: the reference's cofactor inverse of a diagonal Ryy divides
+    0/0 in its unpivoted Schur determinant (utils.c:557) -> NaN."""
+    R = np.diag(np.full(6, 2 * golden["ref"]["ow2"]))
+    Ri = oracle.inverse_cofactor(R)
+    nan = np.isnan(Ri.real.astype(float)) | np.isnan(Ri.imag.astype(float))
+    assert np.array_equal(nan, golden["ref"]["literal_inv_diag6_nan"])
+    assert nan.sum() > 0
+
+
+def test_mmse_unified_matches_ref_formula(oracle, golden):
+    """The unified kernel formula in REF mode (C_ref, pilots, a=0, b=2 ow2)
+    reproduces the repaired reference pipeline."""
+    r = golden["ref"]
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    for c in range(2):
+        hls = from_split(r["pre_lt_ls"][c])
+        C = oracle.mmse_ref_cmatrix(F, invF, hls)
+        for f in range(r["frames_tx"].shape[0]):
+            H = oracle.mmse_unified(C, oracle.pilot_mask(), 0, 2 * np.longdouble(r["ow2"]), r["frames_tx"][f],
+                                    r["frames_rx"][f])
+            assert normrel(H, from_split(r["ps_mmse_ref"][c, f])) < 1e-15
+
+
+def test_mmse_textbook_closed_form(oracle, golden):
+    """TEXTBOOK (MATLAB per-block) MMSE: long double Cholesky vs closed form.
+    Parity unpinned against the reference (no MMSE output in matlab.mat)."""
+    r = golden["ref"]
+    F = from_split(r["F"])
+    for c in range(2):
+        hls = from_split(r["pre_lt_ls"][c])
+        C = oracle.mmse_textbook_cmatrix(F, hls)
+        # C = c c^H with c = F ifft(H_LT) (= H_LT up to the rounding of the double-precision F)
+        cvec = F @ (F.conj() @ hls / 53)
+        assert normrel(C.reshape(-1), np.outer(cvec, cvec.conj()).reshape(-1)) < 1e-17
+        assert normrel(cvec, hls) < 1e-13
+        for f in range(r["frames_tx"].shape[0]):
+            tx, rx = r["frames_tx"][f], r["frames_rx"][f]
+            H = oracle.mmse_unified(C, np.ones(N, np.uint8), 1, r["ow2"], tx, rx)
+            Hc = oracle.mmse_textbook_closed(cvec, tx, rx, r["ow2"])
+            assert normrel(H, Hc) < 1e-11   # Ryy has cond ~4e6; frames 1-7 carry channels unrelated to H_LT
+
+
+@pytest.mark.parametrize("name,key", [("ps_linear", "H_EST_PS_Linear"), ("ps_sinc", "H_EST_PS_Sinc"),
+                                      ("ps_cubic", "H_EST_PS_Cubic")])
+def test_matlab_pins(oracle, golden, name, key):
+    """Per-block interpolators, averaged over blocks 1-4 as WiFi_channel_estimation_PS_*.m do,
+    reproduce matlab.mat (pins the per-block formula the C code shares; cubic with MATLAB divisors)."""
+    m = golden["matlab"]
+    tx, rx = m["tx_symb"].T, m["rx_symb"].T   # MATLAB [53][15] -> [15][53]
+    H = oracle.matlab(name, tx, rx)
+    assert normrel(H, m[key]) < 1e-13
+
+
+def test_matlab_lt_ls_and_c_quirk(oracle, golden):
+    m = golden["matlab"]
+    H = oracle.matlab_lt_ls(m["tx_preamble_fft"], m["rx_preamble_fft"])
+    assert normrel(H, m["H_EST_LT_LS"]) < 1e-14
+    # the C "conj" quirk (a real scale factor) cancels: same estimate to rounding
+    Hc = oracle.lt_ls(m["tx_preamble_fft"], m["rx_preamble_fft"])
+    assert normrel(Hc, m["H_EST_LT_LS"]) < 1e-14
+
+
+def test_equalization_matlab_pin(oracle, golden):
+    m = golden["matlab"]
+    eq = oracle.equalize(m["rx_symb"].T, m["H_EST_LT_LS"], m["H_EST_PS_Linear"])
+    ref = m["eq_symbols"].T
+    assert np.max(np.abs((eq - ref).astype(np.complex128))) / np.max(np.abs(ref)) < 1e-13
+    assert np.all(eq[:, 26] == 0)
+
+
+def test_cubic_c_vs_matlab_divisors_differ(oracle, golden):
+    """Documented quirk: main.c divides every difference by 14 (main.c:116-118)."""
+    m = golden["matlab"]
+    tx, rx = m["tx_symb"].T, m["rx_symb"].T
+    c_quirk = np.mean([oracle.ps_cubic(tx[b], rx[b]) for b in range(4)], axis=0)
+    assert normrel(c_quirk, m["H_EST_PS_Cubic"]) > 0.1
+
+
+def test_pilots_through_interpolants(oracle, golden):
+    r = golden["ref"]
+    for f in range(r["frames_tx"].shape[0]):
+        tx, rx = r["frames_tx"][f], r["frames_rx"][f]
+        hp = rx[list(PILOTS)] / tx[list(PILOTS)]
+        for name in ("ps_linear", "ps_sinc"):
+            H = getattr(oracle, name)(tx, rx).astype(np.complex128)
+            assert np.allclose(H[list(PILOTS)], hp, rtol=1e-14, atol=0), name
+        # the divisor quirk keeps the C cubic on the first two pilots only
+        H = oracle.ps_cubic(tx, rx).astype(np.complex128)
+        assert np.allclose(H[list(PILOTS[:2])], hp[:2], rtol=1e-14, atol=0)
+
+
+def test_cpu_port_matches_oracle(oracle, golden):
+    """The fp64 OpenMP port (bench cpu_baseline) agrees with the long double oracle."""
+    r = golden["ref"]
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    hls = from_split(r["pre_lt_ls"][0])
+    C = oracle.mmse_ref_cmatrix(F, invF, hls).astype(np.complex128)
+    tx = np.ascontiguousarray(r["frames_tx"].reshape(-1))
+    rx = np.ascontiguousarray(r["frames_rx"].reshape(-1))
+    H, _ = oracle.bench_mmse_f64(C, oracle.pilot_mask(), 0.0, 2 * r["ow2"], tx, rx, N, 2)
+    for f in range(r["frames_tx"].shape[0]):
+        assert normrel(H[f], from_split(r["ps_mmse_ref"][0, f])) < 1e-13

@@ -1,0 +1,254 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the reference's
+golden vectors and the CPU oracle.  Tolerance (north star): 1e-10
+norm-relative per frame, max_k|dH_k| / max_k|H_ref,k|."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle_py import N, NBLK, PILOTS, from_split, normrel
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10          # north_star: within 1e-10 relative, complex double
+TOL_LS = 1e-13       # LS family: fp64 vs the reference's x87 long double
+
+
+def frames_from_block0(tx0, rx0):
+    """[B][53] block-0 data -> [B][15][53] frames (other blocks zero)."""
+    B = tx0.shape[0]
+    tx = np.zeros((B, NBLK, N), np.complex128)
+    rx = np.zeros((B, NBLK, N), np.complex128)
+    tx[:, 0], rx[:, 0] = tx0, rx0
+    return tx, rx
+
+
+@pytest.fixture(scope="module")
+def ref_ctx(gpu_wce, golden):
+    r = golden["ref"]
+    return [gpu_wce.Context(r["pre_tx"][c], r["pre_rx"][c], r["ow2"], gpu_wce.MMSE_REF) for c in range(2)]
+
+
+def test_ls_family_golden(gpu_wce, golden, ref_ctx):
+    r = golden["ref"]
+    tx, rx = frames_from_block0(r["frames_tx"], r["frames_rx"])
+    rx_pre = np.stack([r["pre_rx"][f % 2] for f in range(tx.shape[0])])
+    out = ref_ctx[0].estimate_host(tx, rx, rx_pre=rx_pre, mask=gpu_wce.LS_ALL)
+    for name in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc"):
+        err = normrel(out[name], from_split(r[name]))
+        assert err.max() < TOL_LS, (name, err)
+    assert np.all(out["lt_ls"][:, 26] == 0)
+
+
+def test_lt_ls_shared_preamble(gpu_wce, golden, ref_ctx):
+    r = golden["ref"]
+    tx, rx = frames_from_block0(r["frames_tx"][:2], r["frames_rx"][:2])
+    out = ref_ctx[1].estimate_host(tx, rx, mask=gpu_wce.LT_LS)
+    ref = from_split(r["pre_lt_ls"][1])
+    assert normrel(out["lt_ls"], np.stack([ref, ref])).max() < 1e-15
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_mmse_ref_golden(gpu_wce, golden, ref_ctx, case):
+    """PS_MMSE (REF-repaired main.c) on the reference's golden frames."""
+    r = golden["ref"]
+    tx, rx = frames_from_block0(r["frames_tx"], r["frames_rx"])
+    out = ref_ctx[case].estimate_host(tx, rx, mask=gpu_wce.PS_MMSE)
+    err = normrel(out["ps_mmse"], from_split(r["ps_mmse_ref"][case]))
+    assert err.max() < TOL, err
+
+
+def test_compat_entry_points(gpu_wce, golden):
+    """The five reference signatures (main.c:4-8) on the inputs.h frame."""
+    r, inp = golden["ref"], golden["inputs"]
+    tx0, rx0 = inp["tx_symb"][0], inp["rx_symb"][0]
+    H = np.zeros(N, np.clongdouble)
+    gpu_wce.WiFi_channel_estimation_LT_LS(inp["tx_pre"], inp["rx_pre"], H)
+    assert normrel(H, from_split(r["lt_ls"][0])) < TOL_LS
+    for fn, key in ((gpu_wce.WiFi_channel_estimation_PS_Linear, "ps_linear"),
+                    (gpu_wce.WiFi_channel_estimation_PS_Cubic, "ps_cubic"),
+                    (gpu_wce.WiFi_channel_estimation_PS_Sinc, "ps_sinc")):
+        assert normrel(fn(tx0, rx0), from_split(r[key][0])) < TOL_LS, key
+    F = from_split(r["F"])
+    Hm = gpu_wce.WiFi_channel_estimation_PS_MMSE(tx0, rx0, F, r["ow2"], from_split(r["lt_ls"][0]))
+    assert normrel(Hm, from_split(r["ps_mmse_ref"][0, 0])) < TOL
+
+
+def _synth(ctx, wce, B, seed=0x80211, h_shared=None, rx_pre=False):
+    tx = wce.DeviceArray((B, NBLK, N))
+    rx = wce.DeviceArray((B, NBLK, N))
+    pre = wce.DeviceArray((B, N)) if rx_pre else None
+    hs = wce.DeviceArray.from_numpy(np.ascontiguousarray(h_shared, np.complex128)) if h_shared is not None else None
+    ctx.synth(tx, rx, pre, B, seed=seed, h_shared=hs)
+    wce.synchronize()
+    return tx, rx, pre
+
+
+def test_mmse_textbook_closed_form(gpu_wce, golden, oracle):
+    """TEXTBOOK mode (WiFi_channel_estimation_PS_MMSE.m per block): the full
+    53x53 solve against the long double closed form.  Parity unpinned against
+    the reference (no MMSE in matlab.mat); frames share the preamble's channel."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_TEXTBOOK)
+    hlt, C, a, b = ctx.shared()
+    B = 96
+    tx, rx, _ = _synth(ctx, gpu_wce, B, h_shared=hlt)
+    txh, rxh = tx.numpy(), rx.numpy()
+    txh[0], rxh[0] = inp["tx_symb"], inp["rx_symb"]     # frame 0 = inputs.h
+    out = ctx.estimate_host(txh, rxh, mask=gpu_wce.PS_MMSE)["ps_mmse"]
+    F = oracle.fmatrix()
+    hls = oracle.lt_ls(inp["tx_pre"], inp["rx_pre"])
+    cvec = F @ (F.conj() @ hls / 53)
+    errs = [normrel(out[f], oracle.mmse_textbook_closed(cvec, txh[f, 0], rxh[f, 0], inp["ow2"])) for f in range(B)]
+    assert max(errs) < TOL, max(errs)
+
+
+def test_batch_sampled_vs_oracle(gpu_wce, golden, oracle):
+    """20k device-generated frames, per-frame preamble, every estimator +
+    equalization; 48 sampled frames re-checked on the CPU oracle."""
+    r = golden["ref"]
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    B = 20000
+    tx, rx, pre = _synth(ctx, gpu_wce, B, seed=7, rx_pre=True)
+    outs = {n: gpu_wce.DeviceArray((B, N), zero=True) for n in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc",
+                                                                 "ps_mmse")}
+    eq = gpu_wce.DeviceArray((B, NBLK, N), zero=True)
+    o = gpu_wce.Outputs(*(outs[n].addr for n in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc", "ps_mmse")),
+                        eq.addr, N, NBLK * N, N, 0, 0)
+    ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre), o, gpu_wce.ALL)
+    gpu_wce.synchronize()
+    host = {n: outs[n].numpy() for n in outs}
+    eqh = eq.numpy()
+    txh, rxh, preh = tx.numpy(), rx.numpy(), pre.numpy()
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    hls_shared = oracle.lt_ls(inp["tx_pre"], inp["rx_pre"])
+    rng = np.random.default_rng(3)
+    for f in np.concatenate([[0, B - 1], rng.choice(B, 46, replace=False)]):
+        t0, r0 = txh[f, 0], rxh[f, 0]
+        hlt = oracle.lt_ls(inp["tx_pre"], preh[f])
+        assert normrel(host["lt_ls"][f], hlt) < TOL_LS
+        lin = oracle.ps_linear(t0, r0)
+        assert normrel(host["ps_linear"][f], lin) < TOL_LS
+        assert normrel(host["ps_cubic"][f], oracle.ps_cubic(t0, r0)) < TOL_LS
+        assert normrel(host["ps_sinc"][f], oracle.ps_sinc(t0, r0)) < TOL_LS
+        mm = oracle.mmse_ref_repaired(t0, r0, F, inp["ow2"], hls_shared, invF)
+        assert normrel(host["ps_mmse"][f], mm) < TOL
+        e = oracle.equalize(rxh[f], hlt, lin)
+        assert normrel(eqh[f].reshape(-1), e.reshape(-1)) < 1e-12
+        assert np.all(eqh[f][:, 26] == 0)
+
+
+def test_mfma_apply_exact_integers(gpu_wce, golden):
+    """v_mfma_f64_16x16x4 fragment maps: an asymmetric integer C and integer W
+    give an exact product (catches transposed or misplaced C/D layouts)."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    rng = np.random.default_rng(11)
+    C = (rng.integers(-8, 9, (N, N)) + 1j * rng.integers(-8, 9, (N, N))).astype(np.complex128)
+    C[3, 7] += 100  # asymmetric
+    ptr, nbytes = ctx.state()
+    lib = gpu_wce.load()
+    assert lib.wce_memcpy_htod(ptr, C.ctypes.data_as(ctypes.c_void_p), C.nbytes) == 0
+    for B in (1, 16, 37):
+        W = (rng.integers(-5, 6, (B, N)) + 1j * rng.integers(-5, 6, (B, N))).astype(np.complex128)
+        dW = gpu_wce.DeviceArray.from_numpy(W)
+        dH = gpu_wce.DeviceArray((B, N), zero=True)
+        ctx.mmse_apply(dW, dH, B)
+        gpu_wce.synchronize()
+        assert np.array_equal(dH.numpy(), W @ C.T), B
+        ctx.mmse_apply(dW, dW, B)           # in place
+        gpu_wce.synchronize()
+        assert np.array_equal(dW.numpy(), W @ C.T), B
+
+
+def test_strided_layout_and_block(gpu_wce, golden, oracle):
+    """Non-default strides and OFDM block != 0 read the right subcarriers."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    B, fs, bs, blk = 5, 2000, 60, 3
+    rng = np.random.default_rng(5)
+    buf_tx = np.zeros(B * fs, np.complex128)
+    buf_rx = np.zeros(B * fs, np.complex128)
+    for f in range(B):
+        for b in range(NBLK):
+            buf_tx[f * fs + b * bs: f * fs + b * bs + N] = inp["tx_symb"][b]
+            buf_rx[f * fs + b * bs: f * fs + b * bs + N] = inp["rx_symb"][b] * (1 + 0.1 * f) + 1e-4 * rng.standard_normal(N)
+    dtx, drx = gpu_wce.DeviceArray.from_numpy(buf_tx), gpu_wce.DeviceArray.from_numpy(buf_rx)
+    os_ = 64
+    dlin, dmm = gpu_wce.DeviceArray((B, os_), zero=True), gpu_wce.DeviceArray((B, os_), zero=True)
+    o = gpu_wce.Outputs(None, dlin.addr, None, None, dmm.addr, None, os_, 0, 0, 0, 0)
+    ctx.estimate(ctx.frames(dtx, drx, B, frame_stride=fs, block_stride=bs, block=blk),
+                 o, gpu_wce.PS_LINEAR | gpu_wce.PS_MMSE)
+    gpu_wce.synchronize()
+    lin, mm = dlin.numpy(), dmm.numpy()
+    r = golden["ref"]
+    hls = oracle.lt_ls(inp["tx_pre"], inp["rx_pre"])
+    for f in range(B):
+        t = buf_tx[f * fs + blk * bs: f * fs + blk * bs + N]
+        x = buf_rx[f * fs + blk * bs: f * fs + blk * bs + N]
+        assert normrel(lin[f, :N], oracle.ps_linear(t, x)) < TOL_LS
+        ref = oracle.mmse_ref_repaired(t, x, from_split(r["F"]), inp["ow2"], hls, from_split(r["invF"]))
+        assert normrel(mm[f, :N], ref) < TOL
+        assert np.all(lin[f, N:] == 0)     # padding untouched
+
+
+def test_argument_errors(gpu_wce, golden):
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    d = gpu_wce.DeviceArray((4, NBLK, N), zero=True)
+    h = gpu_wce.DeviceArray((4, N), zero=True)
+    good = gpu_wce.Outputs(h.addr, None, None, None, None, None, N, 0, 0, 0, 0)
+    ctx.estimate(ctx.frames(d, d, 0), good, gpu_wce.LT_LS)          # empty batch is fine
+    with pytest.raises(gpu_wce.WceError) as e:                       # requested output missing
+        ctx.estimate(ctx.frames(d, d, 4), good, gpu_wce.PS_LINEAR)
+    assert e.value.code == -1
+    with pytest.raises(gpu_wce.WceError):                            # frame stride too small
+        ctx.estimate(ctx.frames(d, d, 4, frame_stride=10), good, gpu_wce.LT_LS)
+    with pytest.raises(gpu_wce.WceError):                            # block out of range
+        ctx.estimate(ctx.frames(d, d, 4, block=15), good, gpu_wce.LT_LS)
+    with pytest.raises(gpu_wce.WceError):                            # unknown estimator bit
+        ctx.estimate(ctx.frames(d, d, 4), good, 1 << 9)
+    with pytest.raises(gpu_wce.WceError):
+        gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], -1.0)
+    empty = gpu_wce.Context(empty=True)
+    with pytest.raises(gpu_wce.WceError) as e:
+        empty.estimate(empty.frames(d, d, 4), good, gpu_wce.LT_LS)
+    assert e.value.code == -4
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_full_size_properties(gpu_wce, golden, mode):
+    """BASELINE config 3 size (65,536 frames): size-independent properties.
+    Ryy does not depend on rx, so H(2 rx) = 2 H(rx) bit for bit; reruns and
+    sharded generation/estimation are bit-identical."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], mode)
+    hlt, _, _, _ = ctx.shared()
+    B = 65536
+    tx, rx, _ = _synth(ctx, gpu_wce, B, seed=99, h_shared=hlt if mode == 1 else None)
+    H1 = gpu_wce.DeviceArray((B, N), zero=True)
+    o = gpu_wce.Outputs(None, None, None, None, H1.addr, None, N, 0, 0, 0, 0)
+    ctx.estimate(ctx.frames(tx, rx, B), o, gpu_wce.PS_MMSE)
+    gpu_wce.synchronize()
+    a = H1.numpy()
+    assert np.all(np.isfinite(a))
+    ctx.estimate(ctx.frames(tx, rx, B), o, gpu_wce.PS_MMSE)
+    gpu_wce.synchronize()
+    assert np.array_equal(H1.numpy(), a)                              # deterministic
+    rx2 = gpu_wce.DeviceArray.from_numpy(rx.numpy() * 2)
+    ctx.estimate(ctx.frames(tx, rx2, B), o, gpu_wce.PS_MMSE)
+    gpu_wce.synchronize()
+    assert np.array_equal(H1.numpy(), 2 * a)                          # linear in rx, exactly
+    # shard: frames [B/2, B) generated as their own batch with first_frame offset
+    half = B // 2
+    tx2 = gpu_wce.DeviceArray((half, NBLK, N))
+    rxh = gpu_wce.DeviceArray((half, NBLK, N))
+    hs = gpu_wce.DeviceArray.from_numpy(hlt) if mode == 1 else None
+    ctx.synth(tx2, rxh, None, half, first_frame=half, seed=99, h_shared=hs)
+    H2 = gpu_wce.DeviceArray((half, N), zero=True)
+    ctx.estimate(ctx.frames(tx2, rxh, half), gpu_wce.Outputs(None, None, None, None, H2.addr, None, N, 0, 0, 0, 0),
+                 gpu_wce.PS_MMSE)
+    gpu_wce.synchronize()
+    assert np.array_equal(rxh.numpy(), rx.numpy()[half:])
+    assert np.array_equal(H2.numpy(), a[half:])
