@@ -302,6 +302,11 @@ int wce_malloc(void **p, size_t bytes) { HIPCHECK(hipMalloc(p, bytes), "hipMallo
 int wce_free(void *p) { HIPCHECK(hipFree(p), "hipFree"); return WCE_OK; }
 int wce_memcpy_htod(void *d, const void *s, size_t b) { HIPCHECK(hipMemcpy(d, s, b, hipMemcpyHostToDevice), "htod"); return WCE_OK; }
 int wce_memcpy_dtoh(void *d, const void *s, size_t b) { HIPCHECK(hipMemcpy(d, s, b, hipMemcpyDeviceToHost), "dtoh"); return WCE_OK; }
+int wce_memcpy_dtod(void *d, const void *s, size_t b, void *st)
+{
+    HIPCHECK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToDevice, (hipStream_t)st), "dtod");
+    return WCE_OK;
+}
 int wce_memset(void *d, int v, size_t b) { HIPCHECK(hipMemset(d, v, b), "hipMemset"); return WCE_OK; }
 int wce_stream_create(void **s)
 {

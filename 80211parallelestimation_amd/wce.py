@@ -96,6 +96,7 @@ ABI = {
     "wce_free": [c_void_p],
     "wce_memcpy_htod": [c_void_p, c_void_p, c_size_t],
     "wce_memcpy_dtoh": [c_void_p, c_void_p, c_size_t],
+    "wce_memcpy_dtod": [c_void_p, c_void_p, c_size_t, c_void_p],
     "wce_memset": [c_void_p, c_int, c_size_t],
     "wce_stream_create": [POINTER(c_void_p)],
     "wce_stream_destroy": [c_void_p],

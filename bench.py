@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""Benchmark: MMSE-estimated 802.11 frames/s on MI355X (BASELINE.json metric).
+
+Workload (N=1 = BASELINE configs[2]): PS_MMSE over 65,536 synthetic frames
+per GPU (53 subcarriers x 15 OFDM blocks, complex fp64, resident in HBM
+before timing), 53x53 solve per frame + batched f64-MFMA product.  The timed
+step is one wce_estimate(PS_MMSE) over the whole batch.  Headline mode is
+TEXTBOOK (dense Ryy = X C X' + ow2 I, WiFi_channel_estimation_PS_MMSE.m); the
+REF-repaired main.c mode (same kernels, Ryy = 2 ow2 I) is reported beside it.
+
+Multi-GPU: one process per GPU (torch.distributed.run); frames are sharded
+(weak scaling, frames_per_gpu each), the shared state (C, H_LT, tx_pre, ...)
+is built on rank 0 and sent with ONE RCCL broadcast; no other collective on
+the data path.  Timing: barrier + device sync on both sides, max over ranks.
+
+Extra JSON fields: roofline of the dominant kernel (mmse_solve) measured with
+HIP events on the launch stream, the MFMA apply kernel, the LS/HBM path
+(config 2), and a CPU baseline (the oracle's fp64 OpenMP port, rank 0 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+N, NBLK = 53, 15
+# algorithmic work per frame (DESIGN.md "Rooflines")
+FLOP_CHOL = 4.0 / 3.0 * N ** 3           # n^3/6 complex MACs x 8
+FLOP_RYY = 12.0 * N * N                  # a x_i C_ij conj(x_j) + b
+FLOP_TRSV = 8.0 * N * N                  # forward (bordered row) + back substitution
+FLOP_APPLY = 8.0 * N * N                 # H = C w
+FLOP_SOLVE_TXT = FLOP_CHOL + FLOP_RYY + FLOP_TRSV
+FLOP_SOLVE_REF = FLOP_CHOL + FLOP_TRSV   # REF: a = 0, Ryy is the diagonal 2 ow2 I (no build term)
+BYTES_LS_CFG2 = 2672                     # LT_LS + PS_Linear: rx_pre 848 + pilots 128 + 2 x 848 out
+PEAK_FP64_TFLOPS = 78.6                  # MI355X FP64 vector = FP64 matrix (spec)
+PEAK_HBM_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "MMSE-estimated 802.11 frames/sec (53 subcarriers) at 1/2/4/8 MI355X; % roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-gpu", type=int, default=65536)
+    ap.add_argument("--mode", choices=["textbook", "ref"], default="textbook")
+    ap.add_argument("--ls-frames", type=int, default=1 << 20, help="config-2 LS batch (past the 256 MiB MALL)")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (for profiling runs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
+    return ap.parse_args()
+
+
+class Dist:
+    """torch.distributed only when launched with WORLD_SIZE > 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.torch, self.dist = torch, dist
+
+    def barrier(self):
+        if self.torch is not None:
+            self.dist.barrier(device_ids=[self.local])
+
+    def max(self, x: float) -> float:
+        if self.torch is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def broadcast_state(self, wce, ctx, stream):
+        """One RCCL broadcast of the packed shared state from rank 0."""
+        if self.torch is None:
+            return
+        ptr, nbytes = ctx.state()
+        buf = self.torch.empty(nbytes, dtype=self.torch.uint8, device="cuda")
+        lib = wce.load()
+        if self.rank == 0:
+            assert lib.wce_memcpy_dtod(buf.data_ptr(), ptr, nbytes, None) == 0
+        self.torch.cuda.synchronize()
+        self.dist.broadcast(buf, src=0)
+        self.torch.cuda.synchronize()
+        if self.rank != 0:
+            assert lib.wce_memcpy_dtod(ptr, buf.data_ptr(), nbytes, None) == 0
+            ctx.mark_ready()
+
+    def close(self):
+        if self.torch is not None:
+            self.dist.destroy_process_group()
+
+
+def time_events(wce, stream, fn, reps):
+    e0, e1 = wce.Event(), wce.Event()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    return e0.elapsed_ms(e1) / reps
+
+
+def main():
+    args = parse()
+    dist = Dist()
+    import importlib
+    wce = importlib.import_module("80211parallelestimation_amd")
+    dev = dist.local if dist.world > 1 else 0
+    assert wce.device_count() > 0, "bench needs an MI355X"
+    wce.load().wce_set_device(dev)
+    inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
+    mode = wce.MMSE_TEXTBOOK if args.mode == "textbook" else wce.MMSE_REF
+    stream = wce.Stream()
+
+    def make_ctx(m):
+        if dist.world > 1 and dist.rank != 0:
+            c = wce.Context(empty=True, device=dev)
+        else:
+            c = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m, device=dev)
+        dist.broadcast_state(wce, c, stream)
+        return c
+
+    ctx = make_ctx(mode)
+    hlt, _, _, _ = ctx.shared()
+    B = args.frames_per_gpu
+    first = dist.rank * B
+    tx = wce.DeviceArray((B, NBLK, N))
+    rx = wce.DeviceArray((B, NBLK, N))
+    hs = wce.DeviceArray.from_numpy(hlt)     # frames share the preamble's channel (physically consistent)
+    ctx.synth(tx, rx, None, B, first_frame=first, seed=0x80211, h_shared=hs, stream=stream.handle)
+    H = wce.DeviceArray((B, N), zero=True)
+    frames = ctx.frames(tx, rx, B)
+    outs = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+    s = stream.handle
+
+    def step(c=ctx):
+        c.estimate(frames, outs, wce.PS_MMSE, s)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    dist.barrier()
+    stream.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    stream.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = dist.max(t1 - t0)
+    total_frames = B * dist.world * args.steps
+    value = total_frames / elapsed
+    res = {"metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": dist.world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": f"PS_MMSE {args.mode} (53x53 per-frame solve + MFMA C*W), BASELINE configs[2]",
+                      "frames_per_gpu": B, "global_frames": B * dist.world, "subcarriers": N, "ofdm_blocks": NBLK,
+                      "parallelism": f"dp{dist.world} (frames sharded, 1 RCCL state broadcast)"}}
+
+    if not args.no_extras:
+        # dominant kernel: mmse_solve, HIP events on the launch stream
+        W = H
+        reps = max(5, args.steps)
+        t_solve = time_events(wce, stream, lambda: ctx.mmse_solve(frames, W, N, s), reps)
+        t_apply = time_events(wce, stream, lambda: ctx.mmse_apply(W, H, B, N, s), reps)
+        fl_solve = FLOP_SOLVE_TXT if mode == wce.MMSE_TEXTBOOK else FLOP_SOLVE_REF
+        ach = fl_solve * B / (t_solve * 1e-3) / 1e12
+        res["roofline"] = {"bound": "mfma", "kernel": "mmse_solve_kernel (fp64 VALU Cholesky)",
+                           "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": None,
+                           "flop_per_frame": fl_solve, "frames_per_launch": B, "avg_launch_ms": t_solve,
+                           "note": "peak = MI355X FP64 (vector = matrix, spec); traffic: see profiles/"}
+        ach_apply = FLOP_APPLY * B / (t_apply * 1e-3) / 1e12
+        res["apply_kernel"] = {"kernel": "mmse_apply_kernel (v_mfma_f64_16x16x4)", "avg_launch_ms": t_apply,
+                               "achieved_tflops": ach_apply, "frac_fp64_peak": ach_apply / PEAK_FP64_TFLOPS}
+        res["mmse_total_flop_per_frame"] = fl_solve + FLOP_APPLY
+        res["mmse_frac_of_roofline"] = value / dist.world * (fl_solve + FLOP_APPLY) / (PEAK_FP64_TFLOPS * 1e12)
+
+        # the other MMSE mode, same kernels
+        other = wce.MMSE_REF if mode == wce.MMSE_TEXTBOOK else wce.MMSE_TEXTBOOK
+        ctx2 = make_ctx(other)
+        for _ in range(2):
+            step(ctx2)
+        t_other = time_events(wce, stream, lambda: step(ctx2), reps)
+        t_os = time_events(wce, stream, lambda: ctx2.mmse_solve(frames, W, N, s), reps)
+        res["ref_mode" if other == wce.MMSE_REF else "textbook_mode"] = {
+            "frames_per_s_per_gpu": B / (t_other * 1e-3), "ms_per_step": t_other,
+            "solve_ms": t_os, "solve_tflops": (FLOP_SOLVE_REF if other == wce.MMSE_REF else FLOP_SOLVE_TXT) * B
+            / (t_os * 1e-3) / 1e12}
+        del ctx2
+
+        # LS path (config 2: LT_LS + PS_Linear), HBM-bound
+        if dist.rank == 0:
+            res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
+
+    if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
+        res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
+
+    if dist.rank == 0:
+        print(json.dumps(res), flush=True)
+    dist.close()
+
+
+def bench_ls(wce, ctx, stream, n, reps):
+    """LT_LS (per-frame preamble) + PS_Linear over n frames; algorithmic bytes
+    2,672 B/frame.  Frames hold block 0 only (frame_stride = 53): the PS path
+    reads 4 pilots of block 0, LT_LS the frame's own preamble."""
+    s = stream.handle
+    lib = wce.load()
+    tx, rx, pre = wce.DeviceArray((n, N)), wce.DeviceArray((n, N)), wce.DeviceArray((n, N))
+    rng = np.random.default_rng(1)
+    chunk = min(n, 65536)
+    txh = np.where(rng.random((chunk, N)) < 0.5, -8.8753, 8.8753).astype(np.complex128)
+    rxh = txh * (0.01 + 0.001j) + 1e-4 * rng.standard_normal((chunk, N))
+    tp = np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz"))["tx_pre"]
+    preh = np.repeat(((0.01 + 0.001j) * tp)[None], chunk, axis=0) + 1e-4 * rng.standard_normal((chunk, N))
+    for off in range(0, n, chunk):
+        m = min(chunk, n - off)
+        for d, h in ((tx, txh), (rx, rxh), (pre, preh)):
+            assert lib.wce_memcpy_htod(d.addr + off * N * 16, h[:m].ctypes.data, m * N * 16) == 0
+    hlt, hlin = wce.DeviceArray((n, N)), wce.DeviceArray((n, N))
+    o = wce.Outputs(hlt.addr, hlin.addr, None, None, None, None, N, 0, 0, 0, 0)
+    out = {"workload": "LT_LS + PS_Linear (config 2), per-frame preamble, algorithmic 2672 B/frame"}
+    for label, nb in (("b%d" % n, n), ("b65536", min(n, 65536))):
+        fr = ctx.frames(tx, rx, nb, frame_stride=N, block_stride=N, rx_pre=pre, pre_stride=N)
+        f = lambda: ctx.estimate(fr, o, wce.LT_LS | wce.PS_LINEAR, s)
+        for _ in range(3):
+            f()
+        t = time_events(wce, stream, f, reps)
+        gbs = BYTES_LS_CFG2 * nb / (t * 1e-3) / 1e9
+        out[label] = {"frames": nb, "avg_launch_ms": t, "frames_per_s": nb / (t * 1e-3), "achieved_GBs": gbs,
+                      "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
+    return out
+
+
+def cpu_baseline(ctx, tx, rx, B, mode, budget_s):
+    """The oracle's fp64 OpenMP port of the same unified MMSE (kind "port"),
+    on a bounded sample of the benchmark's own frames."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    hlt, C, a, b = ctx.shared()
+    mask = oracle_py.pilot_mask() if mode == 0 else np.ones(N, np.uint8)
+    m = min(B, 4096)
+    txh = tx.numpy()[:m, 0].copy()
+    rxh = rx.numpy()[:m, 0].copy()
+    _, t = oracle_py.bench_mmse_f64(C, mask, a, b, txh.reshape(-1), rxh.reshape(-1), N, cores)
+    rate = m / t
+    target = int(min(max(rate * budget_s / cores, m), 2_000_000))
+    reps = max(1, target // m)
+    t_tot = 0.0
+    for _ in range(reps):
+        _, t = oracle_py.bench_mmse_f64(C, mask, a, b, txh.reshape(-1), rxh.reshape(-1), N, cores)
+        t_tot += t
+    frames = reps * m
+    return {"value": frames / t_tot, "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{frames} frames ({m} distinct bench frames x {reps}), same unified MMSE algorithm in fp64, "
+                      f"OpenMP over frames, {t_tot:.2f} s wall",
+            "reference_main_c_seconds_per_frame": 232.6,
+            "reference_note": "main.c PS_MMSE itself: ~200-233 s/frame on 1 core, output NaN (SURVEY 0-1); "
+                              "its OpenMP path segfaults"}
+
+
+if __name__ == "__main__":
+    main()

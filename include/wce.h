@@ -151,6 +151,7 @@ int wce_malloc(void **ptr, size_t bytes);
 int wce_free(void *ptr);
 int wce_memcpy_htod(void *dst, const void *src, size_t bytes);
 int wce_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+int wce_memcpy_dtod(void *dst, const void *src, size_t bytes, void *stream);
 int wce_memset(void *dst, int value, size_t bytes);
 int wce_stream_create(void **stream);
 int wce_stream_destroy(void *stream);
