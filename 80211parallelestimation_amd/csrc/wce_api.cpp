@@ -157,7 +157,9 @@ int wce_ctx_get_shared(wce_ctx *c, wce_complex *h_lt, wce_complex *C, double *a,
     hipError_t e = hipMemcpy(h, c->d_state, sizeof(State), hipMemcpyDeviceToHost);
     if (e != hipSuccess) { delete h; return hipfail(e, "download state"); }
     if (h_lt) std::memcpy(h_lt, h->h_lt, sizeof(wce_complex) * wce::NSC);
-    if (C) std::memcpy(C, h->C, sizeof(h->C));
+    if (C)
+        for (int i = 0; i < wce::NSC; i++)
+            std::memcpy(C + i * wce::NSC, h->C + 2 * i * wce::CLD, sizeof(wce_complex) * wce::NSC);
     if (a) *a = h->acoef;
     if (b) *b = h->bcoef;
     delete h;

@@ -10,13 +10,15 @@ namespace wce {
 constexpr int NSC = WCE_NSC;      // 53 useful subcarriers (utils.h:13)
 constexpr int NBLK = WCE_NBLK;    // 15 OFDM blocks (utils.h:15)
 constexpr int NPAD = 64;          // one wave64 lane per subcarrier
+constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
 
 // The frame-independent shared state: everything one rank broadcasts to the
-// others (one RCCL broadcast, 47 KB).  Complex values are {re, im} fp64.
+// others (one RCCL broadcast, 68 KB).  Complex values are {re, im} fp64.
 struct State {
-    double C[NSC * NSC * 2];   // MMSE covariance operator, row-major (44,944 B)
+    double C[CLD * CLD * 2];   // MMSE covariance operator, row-major, zero-padded to 64 x 64
+                               // (65,536 B): kernels index it without bounds checks
     double h_lt[NPAD * 2];     // LT_LS of the shared preamble (main.c:66-75)
     double tx_pre[NPAD * 2];   // shared tx preamble FFT
     double sinc[4][NPAD];      // sinc((k - P_p)/14) in double (utils.c:727-733)

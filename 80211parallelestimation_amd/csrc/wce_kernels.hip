@@ -149,79 +149,130 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 // MMSE solve.  One wave per frame, lane = 8p + q holds A[p+8a][q+8b] for the
 // 28 register blocks a >= b (a, b < 7): the block-cyclic 8x8 grid spreads the
 // shrinking trailing matrix evenly over lanes.  Row 53 holds conj(rx), so the
-// factorisation of [[Ryy, rx], [rx', *]] leaves conj(L^-1 rx) in that row.
+// factorisation of [[Ryy, rx], [rx', *]] also runs the forward solve.
+//
+// Square-root-free LDL' (Ryy = L D L', L unit lower): step k needs only
+// r_k = 1/d_k (v_rcp_f64 + 2 Newton steps), no sqrt and no IEEE divide, and
+// the back-substitution with L' has a unit diagonal.  One-step lookahead: the
+// block column holding k+1 is updated first, the next pivot is formed and its
+// column is published to the other half of a ping-pong LDS buffer, and only
+// then is the bulk of step k issued, so the pivot chain and the LDS round trip
+// hide behind the rank-1 update.
 // =====================================================================
 constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
 
 struct SolveLds {
-    double2 col[64];      // pivot-column broadcast L[:, k]
-    double2 x[64];        // masked tx of the frame (X diagonal), 0 past 53
+    double2 u[2][64];     // pivot column k (unscaled A[:, k]) ping-pong
+    double2 x[64];        // masked tx of the frame (diagonal of X), 0 past 53
     double2 rx[64];
-    double2 blk[64];      // diagonal 8x8 block during back-substitution
+    double2 blk[64];      // diagonal 8x8 block of L during back-substitution
     double2 z[64];        // solution
-    double rd[64];        // 1 / L[k][k]
 };
 
-template <int KB>
-__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane)
+__device__ __forceinline__ double rcp_nr(double d)
 {
-    constexpr int NK = (KB == 6) ? (NSC - 48) : 8;
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A[aa][BB] -= Ur[aa] * conj(V[BB]) for aa = BB..6
+template <int BB>
+__device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 (&V)[RB])
+{
+#pragma unroll
+    for (int aa = BB; aa < RB; ++aa) cmsub_conj(A[aa][BB], Ur[aa], V[BB]);
+}
+
+template <int BB>
+__device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 (&V)[RB])
+{
+    if constexpr (BB < RB) {
+        upd_col<BB>(A, Ur, V);
+        upd_cols_from<BB + 1>(A, Ur, V);
+    }
+}
+
+// Publish column k (unscaled) from the lanes that own it (q == kq).
+template <int KB>
+__device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 *buf, int p, int q, int kq)
+{
+    if (q == kq) {
+#pragma unroll
+        for (int aa = KB; aa < RB; ++aa) buf[p + 8 * aa] = A[aa][KB];
+    }
+}
+
+template <int KB>
+__device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, double &r)
+{
+    constexpr int NK = (KB == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
 #pragma unroll 1
     for (int kq = 0; kq < NK; ++kq) {
-        const double d = readlane_f64(A[KB][KB].x, 9 * kq);   // pivot lives in lane (kq, kq)
-        const double sq = sqrt(d);
-        const double rs = 1.0 / sq;
+        const int k = 8 * KB + kq;
+        const double2 *col = s.u[k & 1];
+        double2 Ur[RB], V[RB];
+#pragma unroll
+        for (int aa = KB; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
+#pragma unroll
+        for (int bb = KB; bb < RB; ++bb) V[bb] = cscale(col[q + 8 * bb], r);
+        // column k becomes L[:, k] = A[:, k] / d_k in the owning lanes
         if (q == kq) {
 #pragma unroll
-            for (int aa = KB; aa < RB; ++aa) {
-                A[aa][KB] = cscale(A[aa][KB], rs);
-                s.col[p + 8 * aa] = A[aa][KB];
-            }
+            for (int aa = KB; aa < RB; ++aa) A[aa][KB] = cscale(Ur[aa], r);
         }
-        if (lane == 0) s.rd[8 * KB + kq] = rs;
-        __syncthreads();
-        double2 Lr[RB], Lc[RB];
-#pragma unroll
-        for (int aa = KB; aa < RB; ++aa) Lr[aa] = s.col[p + 8 * aa];
-#pragma unroll
-        for (int bb = KB; bb < RB; ++bb) Lc[bb] = s.col[q + 8 * bb];
-        if (q > kq) {
-#pragma unroll
-            for (int aa = KB; aa < RB; ++aa) cmsub_conj(A[aa][KB], Lr[aa], Lc[KB]);
+        double2 *next = s.u[(k + 1) & 1];
+        if (kq + 1 < NK) {
+            // lookahead: block column KB (columns > k) first
+            if (q > kq) upd_col<KB>(A, Ur, V);
+            r = rcp_nr(readlane_f64(A[KB][KB].x, 9 * (kq + 1)));
+            publish_col<KB>(A, next, p, q, kq + 1);
+            upd_cols_from<KB + 1>(A, Ur, V);
+        } else if constexpr (KB + 1 < RB) {
+            // last column of the block: the next pivot opens block KB + 1
+            upd_col<KB + 1>(A, Ur, V);
+            r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
+            publish_col<KB + 1>(A, next, p, q, 0);
+            upd_cols_from<KB + 2>(A, Ur, V);
         }
-#pragma unroll
-        for (int aa = KB + 1; aa < RB; ++aa)
-#pragma unroll
-            for (int bb = KB + 1; bb <= aa; ++bb) cmsub_conj(A[aa][bb], Lr[aa], Lc[bb]);
-        __syncthreads();
+        wave_lds_sync();
     }
 }
 
 template <int BLK>
-__device__ __forceinline__ void back_block(double2 (&A)[RB][RB], double2 (&P)[RB], SolveLds &s, int p, int q,
+__device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (&P)[RB], SolveLds &s, int p, int q,
                                            int lane)
 {
-    constexpr int NROW = (BLK == 6) ? (NSC - 48) : 8;
-    // w[8*BLK + q] = y - sum of the contributions of the rows already solved
+    constexpr int NROW = (BLK == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
+    // w[8*BLK + q] = (D^-1 L^-1 rx) minus the contributions of the solved rows
     double2 w = P[BLK];
     w = cadd(w, shfl_xor_c(w, 8));
     w = cadd(w, shfl_xor_c(w, 16));
     w = cadd(w, shfl_xor_c(w, 32));
     s.blk[lane] = A[BLK][BLK];
-    __syncthreads();
-#pragma unroll 1
+    wave_lds_sync();
+    double2 lb[NROW];
+#pragma unroll
+    for (int t = 0; t < NROW; ++t) lb[t] = s.blk[8 * t + q];   // L[8*BLK + t][8*BLK + q]
+#pragma unroll
     for (int t = NROW - 1; t >= 0; --t) {
-        const int i = 8 * BLK + t;
-        const double2 z = cscale(readlane_c(w, t), s.rd[i]);    // lane t = (0, t) holds w_t
-        if (lane == 0) s.z[i] = z;
-        const double2 l = s.blk[8 * t + q];                      // L[i][8*BLK + q]
-        cmsub_conj(w, z, l);                                     // w_q -= conj(L[i][q]) z_i
+        const double2 z = readlane_c(w, t);                   // lane t = (0, t) holds w_t
+        if (lane == 0) s.z[8 * BLK + t] = z;
+        cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i (unit diagonal)
     }
-    __syncthreads();
-    const double2 zp = s.z[8 * BLK + p];                         // rows >= 53 read 0
+    wave_lds_sync();
+    const double2 zp = s.z[8 * BLK + p];                       // rows >= 53 read 0
 #pragma unroll
     for (int bb = 0; bb < BLK; ++bb) cmsub_conj(P[bb], zp, A[BLK][bb]);
-    __syncthreads();
 }
 
 __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
@@ -241,34 +292,46 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restri
         s.rx[lane] = r;
         s.z[lane] = make_double2(0, 0);
     }
-    __syncthreads();
+    wave_lds_sync();
     const double ac = st->acoef, bc = st->bcoef;
     double2 A[RB][RB];
-    double2 xr[RB], xc[RB];
+    {
+        double2 xr[RB], xc[RB];
 #pragma unroll
-    for (int aa = 0; aa < RB; ++aa) { xr[aa] = s.x[p + 8 * aa]; xc[aa] = s.x[q + 8 * aa]; }
+        for (int aa = 0; aa < RB; ++aa) { xr[aa] = s.x[p + 8 * aa]; xc[aa] = cconj(s.x[q + 8 * aa]); }
+        if (ac != 0.0) {   // a X C X'  (C zero-padded: no bounds checks)
 #pragma unroll
-    for (int aa = 0; aa < RB; ++aa)
+            for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
-        for (int bb = 0; bb <= aa; ++bb) {
-            const int i = p + 8 * aa, j = q + 8 * bb;
-            double2 v = make_double2(0, 0);
-            if (ac != 0.0 && i < NSC && j < NSC) {
-                const double2 c = ld2(st->C, i * NSC + j);
-                v = cscale(cmul(cmul(xr[aa], c), cconj(xc[bb])), ac);
-            }
-            if (i == j && i < NSC) v.x += bc;
-            if (aa == RB - 1 && i == NSC && j < NSC) v = cconj(s.rx[j]);   // bordered rx row
-            A[aa][bb] = v;
+                for (int bb = 0; bb <= aa; ++bb)
+                    A[aa][bb] = cscale(cmul(cmul(xr[aa], ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb)), xc[bb]), ac);
+        } else {
+#pragma unroll
+            for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+                for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0, 0);
         }
-    chol_panel<0>(A, s, p, q, lane);
-    chol_panel<1>(A, s, p, q, lane);
-    chol_panel<2>(A, s, p, q, lane);
-    chol_panel<3>(A, s, p, q, lane);
-    chol_panel<4>(A, s, p, q, lane);
-    chol_panel<5>(A, s, p, q, lane);
-    chol_panel<6>(A, s, p, q, lane);
-    // row 53 now holds conj(y), y = L^-1 rx
+#pragma unroll
+        for (int aa = 0; aa < RB; ++aa)
+            if (p == q && p + 8 * aa < NSC) A[aa][aa].x += bc;
+        // bordered row 53 = conj(rx)  (lanes p == 5, register row 6)
+        if (p == NSC - 8 * (RB - 1)) {
+#pragma unroll
+            for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
+        }
+    }
+    // pivot 0 and its column
+    double r = rcp_nr(readlane_f64(A[0][0].x, 0));
+    publish_col<0>(A, s.u[0], p, q, 0);
+    wave_lds_sync();
+    ldl_panel<0>(A, s, p, q, r);
+    ldl_panel<1>(A, s, p, q, r);
+    ldl_panel<2>(A, s, p, q, r);
+    ldl_panel<3>(A, s, p, q, r);
+    ldl_panel<4>(A, s, p, q, r);
+    ldl_panel<5>(A, s, p, q, r);
+    ldl_panel<6>(A, s, p, q, r);
+    // row 53 now holds conj(w), w = D^-1 L^-1 rx
     double2 P[RB];
 #pragma unroll
     for (int bb = 0; bb < RB; ++bb) P[bb] = (p == 5) ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
@@ -279,6 +342,7 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restri
     back_block<2>(A, P, s, p, q, lane);
     back_block<1>(A, P, s, p, q, lane);
     back_block<0>(A, P, s, p, q, lane);
+    wave_lds_sync();
     if (lane < NSC) st2(a.w, f * a.ws + lane, cmul(s.x[lane], s.z[lane]));
 }
 
@@ -315,7 +379,7 @@ __global__ __launch_bounds__(256) void mmse_apply_kernel(const State *__restrict
 #pragma unroll
         for (int s = 0; s < KSTEPS; ++s) {
             const int j = 4 * s + kl;
-            const double2 c = (i < NSC && j < NSC) ? ld2(st->C, i * NSC + j) : make_double2(0, 0);
+            const double2 c = ld2(st->C, i * CLD + j);   // zero-padded 64 x 64
             accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
             accr = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[s], c.y, accr, 0, 0, 0);
             acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);

@@ -197,10 +197,11 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
         st->bcoef = ow2;
         st->xmask = (1ull << NSC) - 1;
     }
-    for (int i = 0; i < n * n; i++) {
-        st->C[2 * i] = (double)__real__ C[i];
-        st->C[2 * i + 1] = (double)__imag__ C[i];
-    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            st->C[2 * (i * CLD + j)] = (double)__real__ C[i * n + j];
+            st->C[2 * (i * CLD + j) + 1] = (double)__imag__ C[i * n + j];
+        }
     for (int k = 0; k < n; k++) {
         st->h_lt[2 * k] = (double)H_LS[k].re;
         st->h_lt[2 * k + 1] = (double)H_LS[k].im;
@@ -252,7 +253,8 @@ extern "C" int wce_debug_build_state(const double *tx_pre, const double *rx_pre,
     State *st = new State;
     int rc = host_build_state(st, host_reference_F(), host_reference_invF(), hlt, txl, ow2, mode);
     if (rc == WCE_OK) {
-        if (C) std::memcpy(C, st->C, sizeof(st->C));
+        if (C)
+            for (int i = 0; i < NSC; i++) std::memcpy(C + 2 * i * NSC, st->C + 2 * i * CLD, sizeof(double) * 2 * NSC);
         if (h_lt) std::memcpy(h_lt, st->h_lt, sizeof(double) * 2 * NSC);
         if (sinc)
             for (int p = 0; p < 4; p++) std::memcpy(sinc + p * NSC, st->sinc[p], sizeof(double) * NSC);

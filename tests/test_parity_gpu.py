@@ -149,7 +149,9 @@ def test_mfma_apply_exact_integers(gpu_wce, golden):
     C[3, 7] += 100  # asymmetric
     ptr, nbytes = ctx.state()
     lib = gpu_wce.load()
-    assert lib.wce_memcpy_htod(ptr, C.ctypes.data_as(ctypes.c_void_p), C.nbytes) == 0
+    Cpad = np.zeros((64, 64), np.complex128)     # State.C is zero-padded to 64 x 64
+    Cpad[:N, :N] = C
+    assert lib.wce_memcpy_htod(ptr, Cpad.ctypes.data_as(ctypes.c_void_p), Cpad.nbytes) == 0
     for B in (1, 16, 37):
         W = (rng.integers(-5, 6, (B, N)) + 1j * rng.integers(-5, 6, (B, N))).astype(np.complex128)
         dW = gpu_wce.DeviceArray.from_numpy(W)
