@@ -152,12 +152,14 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 // factorisation of [[Ryy, rx], [rx', *]] also runs the forward solve.
 //
 // Square-root-free LDL' (Ryy = L D L', L unit lower): step k needs only
-// r_k = 1/d_k (v_rcp_f64 + 2 Newton steps), no sqrt and no IEEE divide, and
-// the back-substitution with L' has a unit diagonal.  One-step lookahead: the
-// block column holding k+1 is updated first, the next pivot is formed and its
-// column is published to the other half of a ping-pong LDS buffer, and only
-// then is the bulk of step k issued, so the pivot chain and the LDS round trip
-// hide behind the rank-1 update.
+// r_k = 1/d_k (v_rcp_f64 + 2 Newton steps), no sqrt and no IEEE divide.
+// Columns stay UNSCALED in registers (u = L d): r_k is applied once to the
+// broadcast column operand, and folded into the back-substitution sums, so
+// the factorisation never rewrites a column under a divergent branch (which
+// costs phi copies on every step).  One-step lookahead: the block column
+// holding k+1 is updated first, the next pivot is formed and its column is
+// published to the other half of a ping-pong LDS buffer, then the bulk of
+// step k is issued, hiding the pivot chain and the LDS round trip.
 // =====================================================================
 constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
 
@@ -165,8 +167,9 @@ struct SolveLds {
     double2 u[2][64];     // pivot column k (unscaled A[:, k]) ping-pong
     double2 x[64];        // masked tx of the frame (diagonal of X), 0 past 53
     double2 rx[64];
-    double2 blk[64];      // diagonal 8x8 block of L during back-substitution
+    double2 blk[64];      // diagonal 8x8 block of u during back-substitution
     double2 z[64];        // solution
+    double rd[64];        // r_k = 1 / d_k, 0 past 52
 };
 
 __device__ __forceinline__ double rcp_nr(double d)
@@ -185,24 +188,25 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// A[aa][BB] -= Ur[aa] * conj(V[BB]) for aa = BB..6
+// A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
 template <int BB>
-__device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 (&V)[RB])
+__device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v)
 {
 #pragma unroll
-    for (int aa = BB; aa < RB; ++aa) cmsub_conj(A[aa][BB], Ur[aa], V[BB]);
+    for (int aa = BB; aa < RB; ++aa) cmsub_conj(A[aa][BB], Ur[aa], v);
 }
 
 template <int BB>
 __device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 (&V)[RB])
 {
     if constexpr (BB < RB) {
-        upd_col<BB>(A, Ur, V);
+        upd_col<BB>(A, Ur, V[BB]);
         upd_cols_from<BB + 1>(A, Ur, V);
     }
 }
 
-// Publish column k (unscaled) from the lanes that own it (q == kq).
+// Publish column k (unscaled) from the lanes that own it (q == kq).  Only
+// stores sit under the branch: no register is redefined in it.
 template <int KB>
 __device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 *buf, int p, int q, int kq)
 {
@@ -212,62 +216,69 @@ __device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 
     }
 }
 
+// Step k of the factorisation.  NEXT_IN_BLOCK: column k+1 lies in block KB
+// (runtime kq); otherwise k is the last column of block KB and the next pivot
+// opens block KB + 1 (compile-time), or k = 52 is the last pivot.
+template <int KB, bool NEXT_IN_BLOCK>
+__device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane, double &r, int kq)
+{
+    const int k = 8 * KB + kq;
+    const double2 *col = s.u[k & 1];
+    double2 Ur[RB], V[RB];
+#pragma unroll
+    for (int aa = KB; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
+#pragma unroll
+    for (int bb = KB; bb < RB; ++bb) V[bb] = cscale(col[q + 8 * bb], r);
+    if (lane == 0) s.rd[k] = r;
+    double2 *next = s.u[(k + 1) & 1];
+    if constexpr (NEXT_IN_BLOCK) {
+        // lookahead: columns > k of block KB first (operand select, not a branch)
+        const double2 vk = (q > kq) ? V[KB] : make_double2(0.0, 0.0);
+        upd_col<KB>(A, Ur, vk);
+        r = rcp_nr(readlane_f64(A[KB][KB].x, 9 * (kq + 1)));
+        publish_col<KB>(A, next, p, q, kq + 1);
+        upd_cols_from<KB + 1>(A, Ur, V);
+    } else if constexpr (KB + 1 < RB) {
+        upd_col<KB + 1>(A, Ur, V[KB + 1]);
+        r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
+        publish_col<KB + 1>(A, next, p, q, 0);
+        upd_cols_from<KB + 2>(A, Ur, V);
+    }
+    wave_lds_sync();
+}
+
 template <int KB>
-__device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, double &r)
+__device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane, double &r)
 {
     constexpr int NK = (KB == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
 #pragma unroll 1
-    for (int kq = 0; kq < NK; ++kq) {
-        const int k = 8 * KB + kq;
-        const double2 *col = s.u[k & 1];
-        double2 Ur[RB], V[RB];
-#pragma unroll
-        for (int aa = KB; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
-#pragma unroll
-        for (int bb = KB; bb < RB; ++bb) V[bb] = cscale(col[q + 8 * bb], r);
-        // column k becomes L[:, k] = A[:, k] / d_k in the owning lanes
-        if (q == kq) {
-#pragma unroll
-            for (int aa = KB; aa < RB; ++aa) A[aa][KB] = cscale(Ur[aa], r);
-        }
-        double2 *next = s.u[(k + 1) & 1];
-        if (kq + 1 < NK) {
-            // lookahead: block column KB (columns > k) first
-            if (q > kq) upd_col<KB>(A, Ur, V);
-            r = rcp_nr(readlane_f64(A[KB][KB].x, 9 * (kq + 1)));
-            publish_col<KB>(A, next, p, q, kq + 1);
-            upd_cols_from<KB + 1>(A, Ur, V);
-        } else if constexpr (KB + 1 < RB) {
-            // last column of the block: the next pivot opens block KB + 1
-            upd_col<KB + 1>(A, Ur, V);
-            r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
-            publish_col<KB + 1>(A, next, p, q, 0);
-            upd_cols_from<KB + 2>(A, Ur, V);
-        }
-        wave_lds_sync();
-    }
+    for (int kq = 0; kq < NK - 1; ++kq) ldl_step<KB, true>(A, s, p, q, lane, r, kq);
+    ldl_step<KB, false>(A, s, p, q, lane, r, NK - 1);
 }
 
+// Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
+// registers hold u = L D; r_j = 1/d_j rescales sums once per column.
 template <int BLK>
-__device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (&P)[RB], SolveLds &s, int p, int q,
-                                           int lane)
+__device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
+                                           SolveLds &s, int p, int q, int lane)
 {
     constexpr int NROW = (BLK == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
-    // w[8*BLK + q] = (D^-1 L^-1 rx) minus the contributions of the solved rows
+    // w_j = r_j * (conj(u_53,j) - sum_{i solved} conj(u_ij) z_i),  j = 8*BLK + q
     double2 w = P[BLK];
     w = cadd(w, shfl_xor_c(w, 8));
     w = cadd(w, shfl_xor_c(w, 16));
     w = cadd(w, shfl_xor_c(w, 32));
+    w = cscale(w, rq[BLK]);
     s.blk[lane] = A[BLK][BLK];
     wave_lds_sync();
     double2 lb[NROW];
 #pragma unroll
-    for (int t = 0; t < NROW; ++t) lb[t] = s.blk[8 * t + q];   // L[8*BLK + t][8*BLK + q]
+    for (int t = 0; t < NROW; ++t) lb[t] = cscale(s.blk[8 * t + q], rq[BLK]);   // L[8*BLK + t][8*BLK + q]
 #pragma unroll
     for (int t = NROW - 1; t >= 0; --t) {
         const double2 z = readlane_c(w, t);                   // lane t = (0, t) holds w_t
         if (lane == 0) s.z[8 * BLK + t] = z;
-        cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i (unit diagonal)
+        cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i
     }
     wave_lds_sync();
     const double2 zp = s.z[8 * BLK + p];                       // rows >= 53 read 0
@@ -291,30 +302,36 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restri
         s.x[lane] = inx ? t : make_double2(0, 0);
         s.rx[lane] = r;
         s.z[lane] = make_double2(0, 0);
+        s.rd[lane] = 0.0;
     }
     wave_lds_sync();
     const double ac = st->acoef, bc = st->bcoef;
     double2 A[RB][RB];
     {
-        double2 xr[RB], xc[RB];
-#pragma unroll
-        for (int aa = 0; aa < RB; ++aa) { xr[aa] = s.x[p + 8 * aa]; xc[aa] = cconj(s.x[q + 8 * aa]); }
         if (ac != 0.0) {   // a X C X'  (C zero-padded: no bounds checks)
+            double2 yr[RB], xc[RB];
+#pragma unroll
+            for (int aa = 0; aa < RB; ++aa) {
+                yr[aa] = cscale(s.x[p + 8 * aa], ac);
+                xc[aa] = cconj(s.x[q + 8 * aa]);
+            }
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb)
-                    A[aa][bb] = cscale(cmul(cmul(xr[aa], ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb)), xc[bb]), ac);
+                    A[aa][bb] = cmul(cmul(yr[aa], ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb)), xc[bb]);
         } else {
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0, 0);
         }
+        const double bdiag = (p == q) ? bc : 0.0;
 #pragma unroll
-        for (int aa = 0; aa < RB; ++aa)
-            if (p == q && p + 8 * aa < NSC) A[aa][aa].x += bc;
-        // bordered row 53 = conj(rx)  (lanes p == 5, register row 6)
+        for (int aa = 0; aa < RB - 1; ++aa) A[aa][aa].x += bdiag;
+        A[RB - 1][RB - 1].x += (p == q && p < NSC - 8 * (RB - 1)) ? bc : 0.0;
+        // bordered row 53 = conj(rx)  (lanes p == 5, register row 6).  A branch, not
+        // a select: a select on an A element defeats SROA (A would live in scratch).
         if (p == NSC - 8 * (RB - 1)) {
 #pragma unroll
             for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
@@ -324,24 +341,29 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restri
     double r = rcp_nr(readlane_f64(A[0][0].x, 0));
     publish_col<0>(A, s.u[0], p, q, 0);
     wave_lds_sync();
-    ldl_panel<0>(A, s, p, q, r);
-    ldl_panel<1>(A, s, p, q, r);
-    ldl_panel<2>(A, s, p, q, r);
-    ldl_panel<3>(A, s, p, q, r);
-    ldl_panel<4>(A, s, p, q, r);
-    ldl_panel<5>(A, s, p, q, r);
-    ldl_panel<6>(A, s, p, q, r);
-    // row 53 now holds conj(w), w = D^-1 L^-1 rx
-    double2 P[RB];
+    ldl_panel<0>(A, s, p, q, lane, r);
+    ldl_panel<1>(A, s, p, q, lane, r);
+    ldl_panel<2>(A, s, p, q, lane, r);
+    ldl_panel<3>(A, s, p, q, lane, r);
+    ldl_panel<4>(A, s, p, q, lane, r);
+    ldl_panel<5>(A, s, p, q, lane, r);
+    ldl_panel<6>(A, s, p, q, lane, r);
+    wave_lds_sync();
+    // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
+    double rq[RB];
 #pragma unroll
-    for (int bb = 0; bb < RB; ++bb) P[bb] = (p == 5) ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
-    back_block<6>(A, P, s, p, q, lane);
-    back_block<5>(A, P, s, p, q, lane);
-    back_block<4>(A, P, s, p, q, lane);
-    back_block<3>(A, P, s, p, q, lane);
-    back_block<2>(A, P, s, p, q, lane);
-    back_block<1>(A, P, s, p, q, lane);
-    back_block<0>(A, P, s, p, q, lane);
+    for (int bb = 0; bb < RB; ++bb) rq[bb] = s.rd[q + 8 * bb];
+    double2 P[RB];
+    const bool brow = (p == NSC - 8 * (RB - 1));
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) P[bb] = brow ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
+    back_block<6>(A, P, rq, s, p, q, lane);
+    back_block<5>(A, P, rq, s, p, q, lane);
+    back_block<4>(A, P, rq, s, p, q, lane);
+    back_block<3>(A, P, rq, s, p, q, lane);
+    back_block<2>(A, P, rq, s, p, q, lane);
+    back_block<1>(A, P, rq, s, p, q, lane);
+    back_block<0>(A, P, rq, s, p, q, lane);
     wave_lds_sync();
     if (lane < NSC) st2(a.w, f * a.ws + lane, cmul(s.x[lane], s.z[lane]));
 }
