@@ -147,6 +147,17 @@ int wce_ctx_mark_ready(wce_ctx *c)
     return WCE_OK;
 }
 
+int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
+{
+    if (!c || !host_state || bytes < sizeof(State)) return fail(WCE_EINVAL, "bad state blob");
+    if (static_cast<const State *>(host_state)->magic != wce::STATE_MAGIC)
+        return fail(WCE_ESTATE, "state blob has no valid magic");
+    DeviceGuard g(c->device);
+    HIPCHECK(hipMemcpy(c->d_state, host_state, sizeof(State), hipMemcpyHostToDevice), "upload state");
+    c->ready = true;
+    return WCE_OK;
+}
+
 int wce_ctx_get_shared(wce_ctx *c, wce_complex *h_lt, wce_complex *C, double *a, double *b)
 {
     if (!c) return fail(WCE_EINVAL, "null ctx");

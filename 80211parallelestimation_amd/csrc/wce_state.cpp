@@ -264,3 +264,21 @@ extern "C" int wce_debug_build_state(const double *tx_pre, const double *rx_pre,
     delete st;
     return rc;
 }
+
+extern "C" size_t wce_state_size(void) { return sizeof(wce::State); }
+
+extern "C" int wce_state_build(void *out, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
+                               double ow2, int mode)
+{
+    using namespace wce;
+    if (!out || !tx_pre || !rx_pre || bytes < sizeof(State)) return WCE_EINVAL;
+    if (!(ow2 > 0)) return WCE_EINVAL;
+    ldc txl[NSC], rxl[NSC], hlt[NSC];
+    for (int k = 0; k < NSC; k++) {
+        txl[k].re = tx_pre[k].re; txl[k].im = tx_pre[k].im;
+        rxl[k].re = rx_pre[k].re; rxl[k].im = rx_pre[k].im;
+    }
+    host_lt_ls(txl, rxl, hlt);
+    return host_build_state(static_cast<State *>(out), host_reference_F(), host_reference_invF(), hlt, txl, ow2,
+                            mode);
+}

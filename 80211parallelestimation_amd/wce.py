@@ -84,6 +84,9 @@ ABI = {
     "wce_ctx_destroy": [c_void_p],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
+    "wce_state_size": [],
+    "wce_state_build": [c_void_p, c_size_t, c_void_p, c_void_p, c_double, c_int],
+    "wce_ctx_load_state": [c_void_p, c_void_p, c_size_t],
     "wce_ctx_get_shared": [c_void_p, c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)],
     "wce_estimate": [c_void_p, POINTER(Frames), POINTER(Outputs), c_uint32, c_void_p],
     "wce_mmse_solve": [c_void_p, POINTER(Frames), c_void_p, c_int64, c_void_p],
@@ -131,6 +134,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = None if name in _VOID else (ctypes.c_char_p if name in _STR else c_int)
+    lib.wce_state_size.restype = c_size_t
     _lib = lib
     return lib
 
@@ -233,6 +237,11 @@ class Context:
         _check(_lib.wce_ctx_state(self.handle, byref(ptr), byref(nb)), "wce_ctx_state")
         return ptr.value, nb.value
 
+    def load_state(self, blob: np.ndarray):
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        _check(_lib.wce_ctx_load_state(self.handle, blob.ctypes.data_as(c_void_p), blob.nbytes),
+               "wce_ctx_load_state")
+
     def mark_ready(self):
         _check(_lib.wce_ctx_mark_ready(self.handle), "wce_ctx_mark_ready")
 
@@ -287,6 +296,17 @@ class Context:
         if deq is not None:
             res["eq"] = deq.numpy()
         return res
+
+
+def state_blob(tx_pre, rx_pre, ow2, mode=MMSE_REF) -> np.ndarray:
+    """The shared state built on the host (no device): bytes to broadcast."""
+    lib = load()
+    n = lib.wce_state_size()
+    blob = np.zeros(n, np.uint8)
+    tp, rp = _as_c128(tx_pre), _as_c128(rx_pre)
+    _check(lib.wce_state_build(blob.ctypes.data_as(c_void_p), n, tp.ctypes.data_as(c_void_p),
+                               rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_state_build")
+    return blob
 
 
 def synchronize(stream=None):

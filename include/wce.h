@@ -86,6 +86,14 @@ int wce_ctx_destroy(wce_ctx *ctx);
 int wce_ctx_state(wce_ctx *ctx, void **device_ptr, size_t *bytes);
 int wce_ctx_mark_ready(wce_ctx *ctx);
 
+/* Host-only shared state: build it once (no device needed), ship the bytes
+ * to other processes / devices (RCCL broadcast, file, ...), and load them
+ * into a context.  wce_state_size() is the byte size of that blob. */
+size_t wce_state_size(void);
+int wce_state_build(void *host_state, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
+                    double ow2, int mmse_mode);
+int wce_ctx_load_state(wce_ctx *ctx, const void *host_state, size_t bytes);
+
 /* Copy back the shared vectors (host outputs, may be NULL): H_LT (53),
  * C (53*53 row-major), and the MMSE coefficients a, b. */
 int wce_ctx_get_shared(wce_ctx *ctx, wce_complex *h_lt, wce_complex *C, double *a, double *b);

@@ -254,3 +254,19 @@ def test_full_size_properties(gpu_wce, golden, mode):
     gpu_wce.synchronize()
     assert np.array_equal(rxh.numpy(), rx.numpy()[half:])
     assert np.array_equal(H2.numpy(), a[half:])
+
+
+def test_state_blob_roundtrip(gpu_wce, golden):
+    """A host-built state loaded into an empty context (the multi-rank path)
+    gives bit-identical estimates to a context built on its own device."""
+    inp = golden["inputs"]
+    blob = gpu_wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_TEXTBOOK)
+    c1 = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_TEXTBOOK)
+    c2 = gpu_wce.Context(empty=True)
+    c2.load_state(blob)
+    tx = np.repeat(inp["tx_symb"][None], 3, axis=0)
+    rx = np.repeat(inp["rx_symb"][None], 3, axis=0) * np.array([1.0, -0.5, 2.0])[:, None, None]
+    a = c1.estimate_host(tx, rx, mask=gpu_wce.ALL)
+    b = c2.estimate_host(tx, rx, mask=gpu_wce.ALL)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
