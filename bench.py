@@ -57,42 +57,82 @@ def parse():
 
 
 class Dist:
-    """torch.distributed only when launched with WORLD_SIZE > 1."""
+    """torch.distributed only when launched with WORLD_SIZE > 1.  Backend
+    "nccl" (= RCCL over xGMI, the default) or, for rehearsing the control path
+    on a one-GPU box, WCE_DIST_BACKEND=gloo (ranks then share devices)."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = os.environ.get("WCE_DIST_BACKEND", "nccl")
         self.torch = None
+        self.device = self.local
         if self.world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
             self.torch, self.dist = torch, dist
+            if self.backend == "nccl":
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                self.device = self.local % max(1, torch.cuda.device_count())
+                dist.init_process_group("gloo")
 
     def barrier(self):
-        if self.torch is not None:
+        if self.torch is None:
+            return
+        if self.backend == "nccl":
             self.dist.barrier(device_ids=[self.local])
+        else:
+            self.dist.barrier()
 
     def max(self, x: float) -> float:
         if self.torch is None:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def broadcast_state(self, wce, ctx):
-        """One RCCL broadcast of the packed shared state from rank 0."""
+        """One broadcast of the packed shared state from rank 0 (RCCL, device
+        to device; host-staged under gloo)."""
         if self.torch is None:
             return
         import importlib
         multi = importlib.import_module("80211parallelestimation_amd.multi")
-        multi.broadcast_state_device(self.dist, wce, ctx, src=0)
+        if self.backend == "nccl":
+            multi.broadcast_state_device(self.dist, wce, ctx, src=0)
+        else:
+            ptr, n = ctx.state()
+            blob = np.zeros(n, np.uint8)
+            if self.rank == 0:
+                assert wce.load().wce_memcpy_dtoh(blob.ctypes.data, ptr, n) == 0
+            blob = multi.broadcast_state_host(self.dist, blob, n, src=0)
+            if self.rank != 0:
+                ctx.load_state(blob)
 
     def close(self):
         if self.torch is not None:
             self.dist.destroy_process_group()
+
+
+def pmc_traffic(kernel: str, launches_frames: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_summary.json, tools/pmc_passes.sh): FETCH_SIZE (KiB, x2 for
+    gfx950's half-counted 16-B/lane streaming reads, MI355X_MICROARCH.md HBM) +
+    WRITE_SIZE (KiB).  The summary was taken at 65,536 frames per launch."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("wce::" + kernel)
+    if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+        return None, None
+    b = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0
+    return b * launches_frames / 65536.0, os.path.basename(files[-1])
 
 
 def time_events(wce, stream, fn, reps):
@@ -109,7 +149,7 @@ def main():
     dist = Dist()
     import importlib
     wce = importlib.import_module("80211parallelestimation_amd")
-    dev = dist.local if dist.world > 1 else 0
+    dev = dist.device if dist.world > 1 else 0
     assert wce.device_count() > 0, "bench needs an MI355X"
     wce.load().wce_set_device(dev)
     inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
@@ -171,7 +211,10 @@ def main():
         ach = fl_solve * B / (t_solve * 1e-3) / 1e12
         res["roofline"] = {"bound": "mfma", "kernel": "mmse_solve_kernel (fp64 VALU Cholesky)",
                            "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": None,
+                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("mmse_solve_kernel", B)[0],
+                           "traffic_unit": "bytes/launch (FETCH_SIZEx2 + WRITE_SIZE)",
+                           "traffic_source": pmc_traffic("mmse_solve_kernel", B)[1],
+                           "algorithmic_bytes": 3 * 848 * B,
                            "flop_per_frame": fl_solve, "frames_per_launch": B, "avg_launch_ms": t_solve,
                            "note": "peak = MI355X FP64 (vector = matrix, spec); traffic: see profiles/"}
         ach_apply = FLOP_APPLY * B / (t_apply * 1e-3) / 1e12
