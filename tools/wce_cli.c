@@ -1,0 +1,107 @@
+/*
+ * wce_cli.c -- a C host that uses only the C ABI (include/wce.h): the
+ * reference's driver loop (main.c:10-64) turned into a batched run.
+ *
+ *   wce_cli [frames] [mode: ref|textbook] [reps]
+ *
+ * Builds the shared state from a synthetic 802.11 preamble, generates the
+ * frames on the device, runs LT_LS + PS_Linear/Cubic/Sinc + PS_MMSE +
+ * equalization, and prints frames/s per configuration.  Exit code != 0 on
+ * any wce error.
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "wce.h"
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        int rc_ = (x);                                                                    \
+        if (rc_) {                                                                        \
+            fprintf(stderr, "%s failed: %d (%s)\n", #x, rc_, wce_last_error());           \
+            exit(2);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+static float time_it(void *stream, wce_ctx *ctx, const wce_frames *in, const wce_outputs *out, unsigned mask,
+                     int reps)
+{
+    void *e0, *e1;
+    float ms = 0;
+    CHECK(wce_estimate(ctx, in, out, mask, stream)); /* warm-up */
+    CHECK(wce_event_create(&e0));
+    CHECK(wce_event_create(&e1));
+    CHECK(wce_event_record(e0, stream));
+    for (int i = 0; i < reps; i++) CHECK(wce_estimate(ctx, in, out, mask, stream));
+    CHECK(wce_event_record(e1, stream));
+    CHECK(wce_event_elapsed_ms(&ms, e0, e1));
+    wce_event_destroy(e0);
+    wce_event_destroy(e1);
+    return ms / reps;
+}
+
+int main(int argc, char **argv)
+{
+    const long B = argc > 1 ? atol(argv[1]) : 65536;
+    const int mode = (argc > 2 && strcmp(argv[2], "textbook") == 0) ? WCE_MMSE_TEXTBOOK : WCE_MMSE_REF;
+    const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const double ow2 = 9.6172e-08, A = 8.8753;
+    int ndev = 0;
+    CHECK(wce_device_count(&ndev));
+    if (ndev == 0) {
+        fprintf(stderr, "no device\n");
+        return 1;
+    }
+    /* synthetic shared preamble: BPSK long training symbol through a 3-tap channel */
+    wce_complex tx_pre[WCE_NSC], rx_pre[WCE_NSC];
+    for (int k = 0; k < WCE_NSC; k++) {
+        double s = ((k * 7 + 3) % 5 < 2) ? -A : A;
+        double th = -2 * M_PI * (k - 26) / 64.0;
+        double hr = 0.009 + 0.003 * cos(th) + 0.001 * cos(2 * th), hi = 0.003 * sin(th) + 0.001 * sin(2 * th);
+        tx_pre[k].re = k == WCE_DC ? 0 : s;
+        tx_pre[k].im = 0;
+        rx_pre[k].re = tx_pre[k].re * hr;
+        rx_pre[k].im = tx_pre[k].re * hi;
+    }
+    wce_ctx *ctx;
+    CHECK(wce_ctx_create(&ctx, 0, tx_pre, rx_pre, ow2, mode));
+    void *stream;
+    CHECK(wce_stream_create(&stream));
+    const size_t fr = (size_t)WCE_NBLK * WCE_NSC;
+    wce_complex *tx, *rx, *h[5], *eq;
+    CHECK(wce_malloc((void **)&tx, B * fr * sizeof(wce_complex)));
+    CHECK(wce_malloc((void **)&rx, B * fr * sizeof(wce_complex)));
+    CHECK(wce_malloc((void **)&eq, B * fr * sizeof(wce_complex)));
+    for (int i = 0; i < 5; i++) CHECK(wce_malloc((void **)&h[i], B * WCE_NSC * sizeof(wce_complex)));
+    CHECK(wce_synth_frames(ctx, tx, rx, NULL, fr, WCE_NSC, WCE_NSC, 0, B, 0x80211ull, NULL, A, ow2, stream));
+    wce_frames in = {tx, rx, NULL, NULL, (int64_t)fr, WCE_NSC, WCE_NSC, B, 0, 0};
+    wce_outputs out = {h[0], h[1], h[2], h[3], h[4], eq, WCE_NSC, (int64_t)fr, WCE_NSC, 0, 0};
+    struct { const char *name; unsigned mask; } cfg[] = {
+        {"LT_LS+PS_Linear", WCE_EST_LT_LS | WCE_EST_PS_LINEAR},
+        {"LS family (4 estimators)", WCE_EST_LS_ALL},
+        {"PS_MMSE", WCE_EST_PS_MMSE},
+        {"all 5 + equalization", WCE_EST_LS_ALL | WCE_EST_PS_MMSE | WCE_EQUALIZE},
+    };
+    printf("wce_cli: %ld frames, MMSE mode %s, %s\n", B, mode ? "textbook" : "ref", wce_version());
+    for (unsigned c = 0; c < sizeof(cfg) / sizeof(cfg[0]); c++) {
+        float ms = time_it(stream, ctx, &in, &out, cfg[c].mask, reps);
+        printf("  %-26s %9.3f ms  %.3e frames/s\n", cfg[c].name, ms, B / (ms * 1e-3));
+    }
+    /* spot check: LT_LS of frame 0 at DC must be 0 (main.c:74) */
+    wce_complex h0[WCE_NSC];
+    CHECK(wce_stream_synchronize(stream));
+    CHECK(wce_memcpy_dtoh(h0, h[0], sizeof(h0)));
+    if (h0[WCE_DC].re != 0 || h0[WCE_DC].im != 0) {
+        fprintf(stderr, "DC not zero\n");
+        return 3;
+    }
+    for (int i = 0; i < 5; i++) wce_free(h[i]);
+    wce_free(tx);
+    wce_free(rx);
+    wce_free(eq);
+    wce_stream_destroy(stream);
+    wce_ctx_destroy(ctx);
+    return 0;
+}
