@@ -196,12 +196,16 @@ __device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur
     for (int aa = BB; aa < RB; ++aa) cmsub_conj(A[aa][BB], Ur[aa], v);
 }
 
+// Bulk of the rank-1 update, block columns BB..6.  The column operand
+// v = r * u[q + 8 bb] is read from LDS per block column (streamed), so only
+// the 7 row operands stay resident: fewer live registers, more waves.
 template <int BB>
-__device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 (&V)[RB])
+__device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col,
+                                              int q, double r)
 {
     if constexpr (BB < RB) {
-        upd_col<BB>(A, Ur, V[BB]);
-        upd_cols_from<BB + 1>(A, Ur, V);
+        upd_col<BB>(A, Ur, cscale(col[q + 8 * BB], r));
+        upd_cols_from<BB + 1>(A, Ur, col, q, r);
     }
 }
 
@@ -224,25 +228,24 @@ __device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int 
 {
     const int k = 8 * KB + kq;
     const double2 *col = s.u[k & 1];
-    double2 Ur[RB], V[RB];
+    const double rk = r;
+    double2 Ur[RB];
 #pragma unroll
     for (int aa = KB; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
-#pragma unroll
-    for (int bb = KB; bb < RB; ++bb) V[bb] = cscale(col[q + 8 * bb], r);
-    if (lane == 0) s.rd[k] = r;
+    if (lane == 0) s.rd[k] = rk;
     double2 *next = s.u[(k + 1) & 1];
     if constexpr (NEXT_IN_BLOCK) {
-        // lookahead: columns > k of block KB first (operand select, not a branch)
-        const double2 vk = (q > kq) ? V[KB] : make_double2(0.0, 0.0);
-        upd_col<KB>(A, Ur, vk);
+        // lookahead: columns > k of block KB first; the lane mask is folded into r
+        const double rm = (q > kq) ? rk : 0.0;
+        upd_col<KB>(A, Ur, cscale(col[q + 8 * KB], rm));
         r = rcp_nr(readlane_f64(A[KB][KB].x, 9 * (kq + 1)));
         publish_col<KB>(A, next, p, q, kq + 1);
-        upd_cols_from<KB + 1>(A, Ur, V);
+        upd_cols_from<KB + 1>(A, Ur, col, q, rk);
     } else if constexpr (KB + 1 < RB) {
-        upd_col<KB + 1>(A, Ur, V[KB + 1]);
+        upd_col<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
         r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
         publish_col<KB + 1>(A, next, p, q, 0);
-        upd_cols_from<KB + 2>(A, Ur, V);
+        upd_cols_from<KB + 2>(A, Ur, col, q, rk);
     }
     wave_lds_sync();
 }
@@ -286,7 +289,10 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     for (int bb = 0; bb < BLK; ++bb) cmsub_conj(P[bb], zp, A[BLK][bb]);
 }
 
-__global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
+#ifndef WCE_SOLVE_WAVES_PER_SIMD
+#define WCE_SOLVE_WAVES_PER_SIMD 3
+#endif
+__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
     const int lane = threadIdx.x;
@@ -357,6 +363,13 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restri
     const bool brow = (p == NSC - 8 * (RB - 1));
 #pragma unroll
     for (int bb = 0; bb < RB; ++bb) P[bb] = brow ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
+#ifdef WCE_ABLATE_BACKSOLVE   // timing-only build: skip the back-substitution
+#pragma unroll
+    for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+        for (int bb = 0; bb <= aa; ++bb) asm volatile("" ::"v"(A[aa][bb].x), "v"(A[aa][bb].y));
+    if (lane < NSC) s.z[lane] = P[lane & 7];
+#else
     back_block<6>(A, P, rq, s, p, q, lane);
     back_block<5>(A, P, rq, s, p, q, lane);
     back_block<4>(A, P, rq, s, p, q, lane);
@@ -364,6 +377,7 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_kernel(const State *__restri
     back_block<2>(A, P, rq, s, p, q, lane);
     back_block<1>(A, P, rq, s, p, q, lane);
     back_block<0>(A, P, rq, s, p, q, lane);
+#endif
     wave_lds_sync();
     if (lane < NSC) st2(a.w, f * a.ws + lane, cmul(s.x[lane], s.z[lane]));
 }
