@@ -224,7 +224,8 @@ __device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 
 // (runtime kq); otherwise k is the last column of block KB and the next pivot
 // opens block KB + 1 (compile-time), or k = 52 is the last pivot.
 template <int KB, bool NEXT_IN_BLOCK>
-__device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane, double &r, int kq)
+__device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int p, int q, double &r, double &rsel,
+                                         int kq)
 {
     const int k = 8 * KB + kq;
     const double2 *col = s.u[k & 1];
@@ -232,7 +233,7 @@ __device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int 
     double2 Ur[RB];
 #pragma unroll
     for (int aa = KB; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
-    if (lane == 0) s.rd[k] = rk;
+    rsel = (q == kq) ? rk : rsel;      // lanes of column k keep r_k (select: no LDS store per step)
     double2 *next = s.u[(k + 1) & 1];
     if constexpr (NEXT_IN_BLOCK) {
         // lookahead: columns > k of block KB first; the lane mask is folded into r
@@ -251,12 +252,14 @@ __device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int 
 }
 
 template <int KB>
-__device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane, double &r)
+__device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, double &r)
 {
     constexpr int NK = (KB == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
+    double rsel = 0.0;
 #pragma unroll 1
-    for (int kq = 0; kq < NK - 1; ++kq) ldl_step<KB, true>(A, s, p, q, lane, r, kq);
-    ldl_step<KB, false>(A, s, p, q, lane, r, NK - 1);
+    for (int kq = 0; kq < NK - 1; ++kq) ldl_step<KB, true>(A, s, p, q, r, rsel, kq);
+    ldl_step<KB, false>(A, s, p, q, r, rsel, NK - 1);
+    if (p == 0 && q < NK) s.rd[8 * KB + q] = rsel;   // one store per panel
 }
 
 // Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
@@ -274,15 +277,20 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     w = cscale(w, rq[BLK]);
     s.blk[lane] = A[BLK][BLK];
     wave_lds_sync();
+    // lb[t] = L[8*BLK + t][8*BLK + q] for q < t, else 0: a lane's w_q is left
+    // untouched once row q is solved, so it ends holding z_q
     double2 lb[NROW];
 #pragma unroll
-    for (int t = 0; t < NROW; ++t) lb[t] = cscale(s.blk[8 * t + q], rq[BLK]);   // L[8*BLK + t][8*BLK + q]
+    for (int t = 0; t < NROW; ++t) {
+        const double2 v = cscale(s.blk[8 * t + q], rq[BLK]);
+        lb[t] = (q < t) ? v : make_double2(0.0, 0.0);
+    }
 #pragma unroll
     for (int t = NROW - 1; t >= 0; --t) {
-        const double2 z = readlane_c(w, t);                   // lane t = (0, t) holds w_t
-        if (lane == 0) s.z[8 * BLK + t] = z;
-        cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i
+        const double2 z = readlane_c(w, t);                   // lane t = (0, t) holds w_t = z_t
+        cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i, q < t
     }
+    if (p == 0 && q < NROW) s.z[8 * BLK + q] = w;              // one store per block
     wave_lds_sync();
     const double2 zp = s.z[8 * BLK + p];                       // rows >= 53 read 0
 #pragma unroll
@@ -347,13 +355,13 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kerne
     double r = rcp_nr(readlane_f64(A[0][0].x, 0));
     publish_col<0>(A, s.u[0], p, q, 0);
     wave_lds_sync();
-    ldl_panel<0>(A, s, p, q, lane, r);
-    ldl_panel<1>(A, s, p, q, lane, r);
-    ldl_panel<2>(A, s, p, q, lane, r);
-    ldl_panel<3>(A, s, p, q, lane, r);
-    ldl_panel<4>(A, s, p, q, lane, r);
-    ldl_panel<5>(A, s, p, q, lane, r);
-    ldl_panel<6>(A, s, p, q, lane, r);
+    ldl_panel<0>(A, s, p, q, r);
+    ldl_panel<1>(A, s, p, q, r);
+    ldl_panel<2>(A, s, p, q, r);
+    ldl_panel<3>(A, s, p, q, r);
+    ldl_panel<4>(A, s, p, q, r);
+    ldl_panel<5>(A, s, p, q, r);
+    ldl_panel<6>(A, s, p, q, r);
     wave_lds_sync();
     // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
     double rq[RB];
