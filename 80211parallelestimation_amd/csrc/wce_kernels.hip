@@ -66,12 +66,21 @@ __device__ __forceinline__ void st2(double *p, int64_t idx, double2 v)
 {
     reinterpret_cast<double2 *>(p)[idx] = v;
 }
+typedef double v2d __attribute__((ext_vector_type(2)));
+// streaming (non-temporal) 16-B store of outputs nobody re-reads in this kernel
+__device__ __forceinline__ void st2_nt(double *p, int64_t idx, double2 v)
+{
+    v2d t = {v.x, v.y};
+    __builtin_nontemporal_store(t, reinterpret_cast<v2d *>(p) + idx);
+}
 
 // =====================================================================
 // LS family + equalization: one wave per frame, lane k = subcarrier k.
 // =====================================================================
 constexpr int LS_WAVES = 4;   // waves per 256-thread workgroup
+constexpr int LS_FRAMES = 4;  // frames per wave iteration: all loads issued up front
 
+template <bool EQ>
 __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -81,6 +90,7 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
     const double *txp = a.tx_pre ? a.tx_pre : st->tx_pre;
     const double2 tpk = ld2(txp, k);
     const double cq = tpk.x - tpk.y;           // real "conj" of main.c:69-70
+    const double2 tden = make_double2(cq * tpk.x, cq * tpk.y);
     const double2 hlt_shared = ld2(st->h_lt, k);
     const double s0 = st->sinc[0][k], s1 = st->sinc[1][k], s2 = st->sinc[2][k], s3 = st->sinc[3][k];
     const uint32_t mask = a.mask;
@@ -91,55 +101,74 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
     const double alpha = (double)(k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) * (1.0 / 14.0);
     const double dk0 = (double)(k - WCE_P0), dk1 = (double)(k - WCE_P1), dk2 = (double)(k - WCE_P2);
     const int pil = lane < 4 ? (lane == 0 ? WCE_P0 : lane == 1 ? WCE_P1 : lane == 2 ? WCE_P2 : WCE_P3) : 0;
+    const bool rx_pre = need_lt && a.rx_pre;
 
-    for (int64_t f = (int64_t)blockIdx.x * LS_WAVES + (threadIdx.x >> 6); f < a.n; f += nw) {
-        const int64_t base = f * a.fs + (int64_t)a.blk * a.bs;
-        double2 h0 = make_double2(0, 0), h1 = h0, h2 = h0, h3 = h0;
-        if (need_ps) {
-            double2 hp = make_double2(0, 0);
-            if (lane < 4) hp = cdiv(ld2(a.rx, base + pil), ld2(a.tx, base + pil));  // main.c:82-84
-            h0 = shfl_c(hp, 0); h1 = shfl_c(hp, 1); h2 = shfl_c(hp, 2); h3 = shfl_c(hp, 3);
+    for (int64_t f0 = ((int64_t)blockIdx.x * LS_WAVES + (threadIdx.x >> 6)) * LS_FRAMES; f0 < a.n;
+         f0 += nw * LS_FRAMES) {
+        // ---- issue every load of LS_FRAMES frames before any use
+        double2 ptx[LS_FRAMES], prx[LS_FRAMES], rp[LS_FRAMES];
+#pragma unroll
+        for (int u = 0; u < LS_FRAMES; ++u) {
+            const int64_t f = f0 + u < a.n ? f0 + u : a.n - 1;
+            const int64_t base = f * a.fs + (int64_t)a.blk * a.bs;
+            ptx[u] = make_double2(1, 0);
+            prx[u] = make_double2(0, 0);
+            if (need_ps && lane < 4) {
+                ptx[u] = ld2(a.tx, base + pil);
+                prx[u] = ld2(a.rx, base + pil);
+            }
+            rp[u] = rx_pre ? ld2(a.rx_pre, f * a.ps + k) : make_double2(0, 0);
         }
-        double2 hlt = hlt_shared;
-        if (need_lt && a.rx_pre) {
-            const double2 rp = ld2(a.rx_pre, f * a.ps + k);
-            hlt = cdiv(make_double2(cq * rp.x, cq * rp.y), make_double2(cq * tpk.x, cq * tpk.y));
-        }
-        if (k == 26) hlt = make_double2(0, 0);   // main.c:74
-        double2 hlin = make_double2(0, 0);
-        if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {
-            const double2 lo = seg == 0 ? h0 : (seg == 1 ? h1 : h2);
-            const double2 hi = seg == 0 ? h1 : (seg == 1 ? h2 : h3);
-            hlin = cadd(lo, cscale(csub(hi, lo), alpha));
-        }
-        double2 hcub = make_double2(0, 0);
-        if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
-            const double r = 1.0 / 14.0;
-            const double2 f01 = cscale(csub(h1, h0), r), f12 = cscale(csub(h2, h1), r), f23 = cscale(csub(h3, h2), r);
-            const double2 f012 = cscale(csub(f12, f01), r), f123 = cscale(csub(f23, f12), r);
-            const double2 f0123 = cscale(csub(f123, f012), r);
-            hcub = cadd(cadd(cadd(h0, cscale(f01, dk0)), cscale(cscale(f012, dk0), dk1)),
-                        cscale(cscale(cscale(f0123, dk0), dk1), dk2));
-        }
-        double2 hsnc = make_double2(0, 0);
-        if (mask & WCE_EST_PS_SINC)            // main.c:135-145
-            hsnc = cadd(cadd(cadd(cscale(h0, s0), cscale(h1, s1)), cscale(h2, s2)), cscale(h3, s3));
-        if (act) {
-            const int64_t o = f * a.os + k;
-            if ((mask & WCE_EST_LT_LS) && a.lt) st2(a.lt, o, hlt);
-            if ((mask & WCE_EST_PS_LINEAR) && a.lin) st2(a.lin, o, hlin);
-            if ((mask & WCE_EST_PS_CUBIC) && a.cub) st2(a.cub, o, hcub);
-            if ((mask & WCE_EST_PS_SINC) && a.snc) st2(a.snc, o, hsnc);
-        }
-        if ((mask & WCE_EQUALIZE) && a.eq && act) {   // WiFi_Equalization.m:1-9
-            const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
-            const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
-#pragma unroll 5
-            for (int b = 0; b < NBLK; b++) {
-                const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
-                const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
-                const double2 rv = ld2(a.rx, rb + b * a.bs);
-                st2(a.eq, eb + b * a.eqbs, k == 26 ? make_double2(0, 0) : cdiv(rv, hu));
+#pragma unroll
+        for (int u = 0; u < LS_FRAMES; ++u) {
+            const int64_t f = f0 + u;
+            if (f >= a.n) break;
+            double2 h0 = make_double2(0, 0), h1 = h0, h2 = h0, h3 = h0;
+            if (need_ps) {
+                const double2 hp = cdiv(prx[u], ptx[u]);                 // main.c:82-84
+                h0 = shfl_c(hp, 0); h1 = shfl_c(hp, 1); h2 = shfl_c(hp, 2); h3 = shfl_c(hp, 3);
+            }
+            double2 hlt = rx_pre ? cdiv(make_double2(cq * rp[u].x, cq * rp[u].y), tden) : hlt_shared;
+            if (k == 26) hlt = make_double2(0, 0);   // main.c:74
+            double2 hlin = make_double2(0, 0);
+            if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {
+                const double2 lo = seg == 0 ? h0 : (seg == 1 ? h1 : h2);
+                const double2 hi = seg == 0 ? h1 : (seg == 1 ? h2 : h3);
+                hlin = cadd(lo, cscale(csub(hi, lo), alpha));
+            }
+            double2 hcub = make_double2(0, 0);
+            if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
+                const double r = 1.0 / 14.0;
+                const double2 f01 = cscale(csub(h1, h0), r), f12 = cscale(csub(h2, h1), r),
+                              f23 = cscale(csub(h3, h2), r);
+                const double2 f012 = cscale(csub(f12, f01), r), f123 = cscale(csub(f23, f12), r);
+                const double2 f0123 = cscale(csub(f123, f012), r);
+                hcub = cadd(cadd(cadd(h0, cscale(f01, dk0)), cscale(cscale(f012, dk0), dk1)),
+                            cscale(cscale(cscale(f0123, dk0), dk1), dk2));
+            }
+            double2 hsnc = make_double2(0, 0);
+            if (mask & WCE_EST_PS_SINC)            // main.c:135-145
+                hsnc = cadd(cadd(cadd(cscale(h0, s0), cscale(h1, s1)), cscale(h2, s2)), cscale(h3, s3));
+            if (act) {
+                const int64_t o = f * a.os + k;
+                if ((mask & WCE_EST_LT_LS) && a.lt) st2_nt(a.lt, o, hlt);
+                if ((mask & WCE_EST_PS_LINEAR) && a.lin) st2_nt(a.lin, o, hlin);
+                if ((mask & WCE_EST_PS_CUBIC) && a.cub) st2_nt(a.cub, o, hcub);
+                if ((mask & WCE_EST_PS_SINC) && a.snc) st2_nt(a.snc, o, hsnc);
+            }
+            if (EQ && act) {   // WiFi_Equalization.m:1-9
+                const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
+                const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
+                double2 rv[NBLK];
+#pragma unroll
+                for (int b = 0; b < NBLK; b++) rv[b] = ld2(a.rx, rb + b * a.bs);
+#pragma unroll
+                for (int b = 0; b < NBLK; b++) {
+                    const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
+                    const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
+                    const double2 e = k == 26 ? make_double2(0, 0) : cdiv(rv[b], hu);
+                    st2_nt(a.eq, eb + b * a.eqbs, e);
+                }
             }
         }
     }
@@ -516,10 +545,13 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 int launch_ls(const State *st, const LsArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
-    int64_t waves = a.n;
-    int64_t blocks = (waves + LS_WAVES - 1) / LS_WAVES;
-    if (blocks > 256 * 16) blocks = 256 * 16;    // grid-stride the rest
-    hipLaunchKernelGGL(ls_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a);
+    const int64_t groups = (a.n + LS_FRAMES - 1) / LS_FRAMES;     // one wave per LS_FRAMES frames
+    int64_t blocks = (groups + LS_WAVES - 1) / LS_WAVES;
+    if (blocks > 256 * 8) blocks = 256 * 8;      // grid-stride the rest
+    if ((a.mask & WCE_EQUALIZE) && a.eq)
+        hipLaunchKernelGGL(ls_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a);
+    else
+        hipLaunchKernelGGL(ls_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a);
     return hip_status(hipGetLastError());
 }
 
