@@ -184,9 +184,13 @@ static int check_frames(const wce_frames *in, bool need_blocks)
     if (in->n_frames == 0) return WCE_OK;
     if (!in->tx || !in->rx) return fail(WCE_EINVAL, "tx/rx required");
     if (in->block < 0 || in->block >= wce::NBLK) return fail(WCE_EINVAL, "block out of range");
+    if (in->semantics != WCE_SEM_C && in->semantics != WCE_SEM_MATLAB) return fail(WCE_EINVAL, "bad semantics");
+    if (in->semantics == WCE_SEM_MATLAB && in->n_frames > 0 && in->block_stride < wce::NSC)
+        return fail(WCE_EINVAL, "MATLAB semantics reads blocks 0..3: block_stride < 53");
     if (in->block_stride < wce::NSC && (need_blocks || in->block > 0))
         return fail(WCE_EINVAL, "block_stride < 53");
-    const int64_t span = (int64_t)(need_blocks ? wce::NBLK - 1 : in->block) * in->block_stride + wce::NSC;
+    const int last = need_blocks ? wce::NBLK - 1 : (in->semantics == WCE_SEM_MATLAB ? 3 : in->block);
+    const int64_t span = (int64_t)last * in->block_stride + wce::NSC;
     if (in->n_frames > 1 && in->frame_stride < span) return fail(WCE_EINVAL, "frame_stride too small");
     if (in->rx_pre && in->n_frames > 1 && in->pre_stride < wce::NSC) return fail(WCE_EINVAL, "pre_stride < 53");
     return WCE_OK;
@@ -203,7 +207,10 @@ int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_s
     wce::SolveArgs a{};
     a.tx = reinterpret_cast<const double *>(in->tx);
     a.rx = reinterpret_cast<const double *>(in->rx);
-    a.fs = in->frame_stride; a.bs = in->block_stride; a.n = in->n_frames; a.blk = in->block;
+    a.fs = in->frame_stride; a.bs = in->block_stride; a.n = in->n_frames;
+    const bool ml = in->semantics == WCE_SEM_MATLAB;
+    a.blk = ml ? 0 : in->block;
+    a.nblk = ml ? 4 : 1;
     a.w = reinterpret_cast<double *>(W);
     a.ws = w_stride;
     DeviceGuard g(c->device);
@@ -257,6 +264,7 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
         a.rx_pre = reinterpret_cast<const double *>(in->rx_pre);
         a.tx_pre = reinterpret_cast<const double *>(in->tx_pre);
         a.fs = in->frame_stride; a.bs = in->block_stride; a.ps = in->pre_stride; a.n = n; a.blk = in->block;
+        a.matlab = in->semantics == WCE_SEM_MATLAB;
         a.mask = mask & (WCE_EST_LS_ALL | WCE_EQUALIZE);
         a.lt = reinterpret_cast<double *>(out->lt_ls);
         a.lin = reinterpret_cast<double *>(out->ps_linear);

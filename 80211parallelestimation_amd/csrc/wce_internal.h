@@ -55,6 +55,8 @@ struct LsArgs {
     int64_t fs, bs, ps, n;
     int32_t blk;
     uint32_t mask;
+    int32_t matlab;
+    int32_t pad0;
     double *lt, *lin, *cub, *snc, *eq;
     int64_t os, eqfs, eqbs;
     uint32_t eq_src;
@@ -64,7 +66,7 @@ struct SolveArgs {
     const double *tx, *rx;
     int64_t fs, bs, n;
     int32_t blk;
-    int32_t pad;
+    int32_t nblk;             // blocks averaged per frame (1; 4 in MATLAB semantics)
     double *w;
     int64_t ws;
 };

@@ -80,7 +80,11 @@ __device__ __forceinline__ void st2_nt(double *p, int64_t idx, double2 v)
 constexpr int LS_WAVES = 4;   // waves per 256-thread workgroup
 constexpr int LS_FRAMES = 4;  // frames per wave iteration: all loads issued up front
 
-template <bool EQ>
+// ML: MATLAB semantics (WiFi_channel_estimation_*.m): pilot LS averaged over
+// blocks 0..3 -- Linear/Cubic/Sinc are linear in the pilot values, so the
+// 4-block average of the per-block estimates is the per-block formula applied
+// to the averaged pilots -- proper conj in LT_LS, cubic divisors 14/28/42.
+template <bool EQ, bool ML>
 __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -100,7 +104,11 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
     const int seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
     const double alpha = (double)(k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) * (1.0 / 14.0);
     const double dk0 = (double)(k - WCE_P0), dk1 = (double)(k - WCE_P1), dk2 = (double)(k - WCE_P2);
-    const int pil = lane < 4 ? (lane == 0 ? WCE_P0 : lane == 1 ? WCE_P1 : lane == 2 ? WCE_P2 : WCE_P3) : 0;
+    const int pp = lane & 3;
+    const int pil = pp == 0 ? WCE_P0 : pp == 1 ? WCE_P1 : pp == 2 ? WCE_P2 : WCE_P3;
+    // lanes loading pilots: 4 (one block) or 16 (lane = 4 b + pilot, blocks 0..3)
+    const bool pil_lane = ML ? lane < 16 : lane < 4;
+    const int64_t pil_off = ML ? (int64_t)(lane >> 2) * a.bs + pil : (int64_t)a.blk * a.bs + pil;
     const bool rx_pre = need_lt && a.rx_pre;
 
     for (int64_t f0 = ((int64_t)blockIdx.x * LS_WAVES + (threadIdx.x >> 6)) * LS_FRAMES; f0 < a.n;
@@ -110,12 +118,11 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 #pragma unroll
         for (int u = 0; u < LS_FRAMES; ++u) {
             const int64_t f = f0 + u < a.n ? f0 + u : a.n - 1;
-            const int64_t base = f * a.fs + (int64_t)a.blk * a.bs;
             ptx[u] = make_double2(1, 0);
             prx[u] = make_double2(0, 0);
-            if (need_ps && lane < 4) {
-                ptx[u] = ld2(a.tx, base + pil);
-                prx[u] = ld2(a.rx, base + pil);
+            if (need_ps && pil_lane) {
+                ptx[u] = ld2(a.tx, f * a.fs + pil_off);
+                prx[u] = ld2(a.rx, f * a.fs + pil_off);
             }
             rp[u] = rx_pre ? ld2(a.rx_pre, f * a.ps + k) : make_double2(0, 0);
         }
@@ -125,10 +132,21 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
             if (f >= a.n) break;
             double2 h0 = make_double2(0, 0), h1 = h0, h2 = h0, h3 = h0;
             if (need_ps) {
-                const double2 hp = cdiv(prx[u], ptx[u]);                 // main.c:82-84
+                double2 hp = cdiv(prx[u], ptx[u]);                       // main.c:82-84
+                if (ML) {                                                 // mean over blocks 0..3
+                    hp = cadd(hp, shfl_xor_c(hp, 4));
+                    hp = cadd(hp, shfl_xor_c(hp, 8));
+                    hp = cscale(hp, 0.25);
+                }
                 h0 = shfl_c(hp, 0); h1 = shfl_c(hp, 1); h2 = shfl_c(hp, 2); h3 = shfl_c(hp, 3);
             }
-            double2 hlt = rx_pre ? cdiv(make_double2(cq * rp[u].x, cq * rp[u].y), tden) : hlt_shared;
+            double2 hlt = hlt_shared;
+            if (rx_pre) {
+                if (ML)   // WiFi_channel_estimation_LT_LS.m: conj(tx) rx / (conj(tx) tx)
+                    hlt = cscale(cmul(cconj(tpk), rp[u]), 1.0 / (tpk.x * tpk.x + tpk.y * tpk.y));
+                else      // main.c:69-72: real "conj" c = re - im
+                    hlt = cdiv(make_double2(cq * rp[u].x, cq * rp[u].y), tden);
+            }
             if (k == 26) hlt = make_double2(0, 0);   // main.c:74
             double2 hlin = make_double2(0, 0);
             if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {
@@ -138,11 +156,12 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
             }
             double2 hcub = make_double2(0, 0);
             if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
-                const double r = 1.0 / 14.0;
+                const double r = 1.0 / 14.0;     // MATLAB (PS_Cubic.m:11-13): 14, 28, 42
+                const double r2 = ML ? 1.0 / 28.0 : r, r3 = ML ? 1.0 / 42.0 : r;
                 const double2 f01 = cscale(csub(h1, h0), r), f12 = cscale(csub(h2, h1), r),
                               f23 = cscale(csub(h3, h2), r);
-                const double2 f012 = cscale(csub(f12, f01), r), f123 = cscale(csub(f23, f12), r);
-                const double2 f0123 = cscale(csub(f123, f012), r);
+                const double2 f012 = cscale(csub(f12, f01), r2), f123 = cscale(csub(f23, f12), r2);
+                const double2 f0123 = cscale(csub(f123, f012), r3);
                 hcub = cadd(cadd(cadd(h0, cscale(f01, dk0)), cscale(cscale(f012, dk0), dk1)),
                             cscale(cscale(cscale(f0123, dk0), dk1), dk2));
             }
@@ -329,14 +348,13 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_SOLVE_WAVES_PER_SIMD
 #define WCE_SOLVE_WAVES_PER_SIMD 3
 #endif
-__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
+// One block's solve; returns w_lane = x_lane z_lane (0 for lanes >= 53 is
+// not guaranteed: callers store lanes < 53 only).
+__device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
+                                               int64_t base)
 {
-    __shared__ SolveLds s;
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
-    const int64_t f = blockIdx.x;
-    if (f >= a.n) return;
-    const int64_t base = f * a.fs + (int64_t)a.blk * a.bs;
     {
         const bool act = lane < NSC;
         const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
@@ -416,7 +434,33 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kerne
     back_block<0>(A, P, rq, s, p, q, lane);
 #endif
     wave_lds_sync();
-    if (lane < NSC) st2(a.w, f * a.ws + lane, cmul(s.x[lane], s.z[lane]));
+    return cmul(s.x[lane], s.z[lane]);
+}
+
+__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    __shared__ SolveLds s;
+    const int64_t f = blockIdx.x;
+    if (f >= a.n) return;
+    const double2 w = solve_block(st, a, s, f * a.fs + (int64_t)a.blk * a.bs);
+    if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, w);
+}
+
+// MATLAB semantics (WiFi_channel_estimation_PS_MMSE.m): the estimate is the
+// mean of the per-block MMSE estimates of blocks 0..nblk-1.  H = C W is linear
+// in W, so the mean is taken on W and the apply kernel runs once.
+__global__ __launch_bounds__(64, 2) void mmse_solve_avg_kernel(const State *__restrict__ st,
+                                                                                     SolveArgs a)
+{
+    __shared__ SolveLds s;
+    const int64_t f = blockIdx.x;
+    if (f >= a.n) return;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int b = 0; b < a.nblk; ++b) {
+        acc = cadd(acc, solve_block(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs));
+        wave_lds_sync();   // the next block overwrites s
+    }
+    if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, cscale(acc, 1.0 / a.nblk));
 }
 
 // =====================================================================
@@ -548,10 +592,15 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
     const int64_t groups = (a.n + LS_FRAMES - 1) / LS_FRAMES;     // one wave per LS_FRAMES frames
     int64_t blocks = (groups + LS_WAVES - 1) / LS_WAVES;
     if (blocks > 256 * 8) blocks = 256 * 8;      // grid-stride the rest
-    if ((a.mask & WCE_EQUALIZE) && a.eq)
-        hipLaunchKernelGGL(ls_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a);
-    else
-        hipLaunchKernelGGL(ls_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a);
+    const bool eq = (a.mask & WCE_EQUALIZE) && a.eq;
+    const dim3 g((unsigned)blocks), b(256);
+    if (a.matlab) {
+        if (eq) hipLaunchKernelGGL((ls_kernel<true, true>), g, b, 0, (hipStream_t)stream, st, a);
+        else hipLaunchKernelGGL((ls_kernel<false, true>), g, b, 0, (hipStream_t)stream, st, a);
+    } else {
+        if (eq) hipLaunchKernelGGL((ls_kernel<true, false>), g, b, 0, (hipStream_t)stream, st, a);
+        else hipLaunchKernelGGL((ls_kernel<false, false>), g, b, 0, (hipStream_t)stream, st, a);
+    }
     return hip_status(hipGetLastError());
 }
 
@@ -559,7 +608,10 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
     if (a.n > 0x7fffffffll) return WCE_EINVAL;
-    hipLaunchKernelGGL(mmse_solve_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    if (a.nblk > 1)
+        hipLaunchKernelGGL(mmse_solve_avg_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    else
+        hipLaunchKernelGGL(mmse_solve_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
     return hip_status(hipGetLastError());
 }
 

@@ -35,6 +35,8 @@ ALL = 0x3F
 
 MMSE_REF = 0
 MMSE_TEXTBOOK = 1
+SEM_C = 0          # main.c semantics
+SEM_MATLAB = 1     # WiFi_channel_estimation_*.m semantics
 
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP error", -3: "out of memory",
           -4: "context state not ready", -5: "no gfx950 device"}
@@ -64,7 +66,7 @@ class Frames(ctypes.Structure):
     """struct wce_frames (include/wce.h)."""
     _fields_ = [("tx", c_void_p), ("rx", c_void_p), ("rx_pre", c_void_p), ("tx_pre", c_void_p),
                 ("frame_stride", c_int64), ("block_stride", c_int64), ("pre_stride", c_int64),
-                ("n_frames", c_int64), ("block", c_int32), ("reserved", c_int32)]
+                ("n_frames", c_int64), ("block", c_int32), ("semantics", c_int32)]
 
 
 class Outputs(ctypes.Structure):
@@ -256,9 +258,9 @@ class Context:
     # ---------------------------------------------------------------- batched
     @staticmethod
     def frames(tx, rx, n_frames, frame_stride=NBLK * NSC, block_stride=NSC, rx_pre=None, pre_stride=NSC,
-               tx_pre=None, block=0) -> Frames:
+               tx_pre=None, block=0, semantics=SEM_C) -> Frames:
         return Frames(_addr(tx), _addr(rx), _addr(rx_pre), _addr(tx_pre), frame_stride, block_stride, pre_stride,
-                      n_frames, block, 0)
+                      n_frames, block, semantics)
 
     def estimate(self, frames: Frames, outputs: Outputs, mask: int, stream=None):
         _check(_lib.wce_estimate(self.handle, byref(frames), byref(outputs), mask, stream), "wce_estimate")
@@ -275,7 +277,8 @@ class Context:
                                      pre_stride, first_frame, n_frames, seed, _addr(h_shared), amplitude, ow2,
                                      stream), "wce_synth_frames")
 
-    def estimate_host(self, tx, rx, rx_pre=None, mask=ALL, block=0, eq_source=PS_LINEAR):
+    def estimate_host(self, tx, rx, rx_pre=None, mask=ALL, block=0, eq_source=PS_LINEAR, semantics=SEM_C,
+                      tx_pre=None):
         """Convenience: host numpy frames [B][15][53] -> dict of host outputs."""
         tx, rx = _as_c128(tx), _as_c128(rx)
         B = tx.shape[0]
@@ -289,7 +292,8 @@ class Context:
         deq = DeviceArray((B, NBLK, NSC), zero=True) if mask & EQUALIZE else None
         o = Outputs(*[(outs[n].addr if n in outs else None) for n, _ in names],
                     deq.addr if deq is not None else None, NSC, NBLK * NSC, NSC, eq_source, 0)
-        fr = self.frames(dtx, drx, B, rx_pre=dpre, block=block)
+        dtp = DeviceArray.from_numpy(_as_c128(tx_pre)) if tx_pre is not None else None
+        fr = self.frames(dtx, drx, B, rx_pre=dpre, block=block, semantics=semantics, tx_pre=dtp)
         self.estimate(fr, o, mask)
         synchronize()
         res = {n: outs[n].numpy() for n in outs}

@@ -109,8 +109,16 @@ typedef struct {
     int64_t pre_stride;
     int64_t n_frames;
     int32_t block;              /* OFDM block read by PS_* / MMSE (main.c:16 uses 0) */
-    int32_t reserved;
+    int32_t semantics;          /* WCE_SEM_C (main.c) or WCE_SEM_MATLAB (WiFi_*.m) */
 } wce_frames;
+
+/* Estimator semantics (wce_frames.semantics):
+ *  WCE_SEM_C      : main.c -- one OFDM block (`block`), LT_LS "conj" quirk
+ *                   (main.c:69), every cubic divided difference by 14 (main.c:116-118).
+ *  WCE_SEM_MATLAB : WiFi_channel_estimation_*.m -- proper conj in LT_LS, PS_* and
+ *                   PS_MMSE averaged over OFDM blocks 1..4 (0..3 here; `block`
+ *                   ignored), cubic divisors 14/28/42 (PS_Cubic.m:11-13). */
+enum { WCE_SEM_C = 0, WCE_SEM_MATLAB = 1 };
 
 typedef struct {
     wce_complex *lt_ls;         /* device [n_frames][out_stride], NULL = not requested */
