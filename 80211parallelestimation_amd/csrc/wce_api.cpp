@@ -309,6 +309,50 @@ int wce_synth_frames(wce_ctx *c, wce_complex *tx, wce_complex *rx, wce_complex *
     return rc ? fail(rc, "synth launch") : WCE_OK;
 }
 
+// ---------------------------------------------------------------- front end
+int wce_front_end_blocks(wce_ctx *c, const wce_complex *samples, int64_t packet_stride, int64_t n_frames,
+                         int32_t n_blocks, wce_complex *sym, int64_t frame_stride, int64_t block_stride,
+                         void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (n_frames < 0 || n_blocks < 1) return fail(WCE_EINVAL, "n_frames < 0 or n_blocks < 1");
+    if (n_frames == 0) return WCE_OK;
+    if (!samples || !sym) return fail(WCE_EINVAL, "null buffer");
+    if (packet_stride < (int64_t)n_blocks * WCE_SAMPLES_PER_BLOCK) return fail(WCE_EINVAL, "packet_stride < 80 n_blocks");
+    if (block_stride < wce::NSC || frame_stride < (int64_t)(n_blocks - 1) * block_stride + wce::NSC)
+        return fail(WCE_EINVAL, "output strides too small");
+    if (n_frames * n_blocks >= (int64_t)1 << 31) return fail(WCE_EINVAL, "n_frames * n_blocks >= 2^31");
+    wce::FrontArgs a{};
+    a.src = reinterpret_cast<const double *>(samples);
+    a.dst = reinterpret_cast<double *>(sym);
+    a.ps = packet_stride; a.off = WCE_SAMPLES_PER_BLOCK - WCE_FFT_SIZE; a.fs = frame_stride; a.bs = block_stride;
+    a.n_units = (uint32_t)(n_frames * n_blocks); a.nb = (uint32_t)n_blocks;
+    DeviceGuard g(c->device);
+    int rc = wce::launch_front(a, false, stream);
+    return rc ? fail(rc, "front end launch") : WCE_OK;
+}
+
+int wce_front_end_preamble(wce_ctx *c, const wce_complex *lptot, int64_t lptot_stride, int64_t lptot_len,
+                           int64_t n_frames, wce_complex *pre_fft, int64_t pre_stride, double *ow2, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (n_frames < 0) return fail(WCE_EINVAL, "n_frames < 0");
+    if (n_frames == 0) return WCE_OK;
+    if (!lptot || !pre_fft) return fail(WCE_EINVAL, "null buffer");
+    if (lptot_len < 2 * WCE_FFT_SIZE || lptot_stride < lptot_len) return fail(WCE_EINVAL, "lptot_len < 128 or stride < len");
+    if (pre_stride < wce::NSC) return fail(WCE_EINVAL, "pre_stride < 53");
+    if (n_frames >= (int64_t)1 << 31) return fail(WCE_EINVAL, "n_frames >= 2^31");
+    wce::FrontArgs a{};
+    a.src = reinterpret_cast<const double *>(lptot);
+    a.dst = reinterpret_cast<double *>(pre_fft);
+    a.ow2 = ow2;
+    a.ps = lptot_stride; a.off = lptot_len - 2 * WCE_FFT_SIZE; a.fs = pre_stride; a.bs = 0;
+    a.n_units = (uint32_t)n_frames; a.nb = 1;
+    DeviceGuard g(c->device);
+    int rc = wce::launch_front(a, true, stream);
+    return rc ? fail(rc, "front end launch") : WCE_OK;
+}
+
 // ---------------------------------------------------------------- runtime helpers
 int wce_device_count(int *count)
 {

@@ -78,7 +78,18 @@ struct SynthArgs {
     double amp, ow2;
 };
 
+// time-domain front end: unit u = (frame u / nb, unit u % nb); unit samples
+// start at src[f*ps + off + 80*b] (complex); bins at dst[f*fs + b*bs + i]
+struct FrontArgs {
+    const double *src;
+    double *dst;
+    double *ow2;          // preamble only, may be null
+    int64_t ps, off, fs, bs;
+    uint32_t n_units, nb;
+};
+
 int launch_ls(const State *st, const LsArgs &a, void *stream);
+int launch_front(const FrontArgs &a, bool preamble, void *stream);
 int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream);
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);

@@ -35,6 +35,8 @@ ALL = 0x3F
 
 MMSE_REF = 0
 MMSE_TEXTBOOK = 1
+FFT_SIZE = 64            # front end: 64-point DFT per OFDM block (WiFi_RX.m:10)
+SAMPLES_PER_BLOCK = 80   # 64 + 16-sample cyclic prefix (WiFi_RX.m:12)
 SEM_C = 0          # main.c semantics
 SEM_MATLAB = 1     # WiFi_channel_estimation_*.m semantics
 
@@ -95,6 +97,9 @@ ABI = {
     "wce_mmse_apply": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p],
     "wce_synth_frames": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                          c_uint64, c_void_p, c_double, c_double, c_void_p],
+    "wce_front_end_blocks": [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_void_p],
+    "wce_front_end_preamble": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p,
+                               c_void_p],
     "wce_device_count": [POINTER(c_int)],
     "wce_set_device": [c_int],
     "wce_malloc": [POINTER(c_void_p), c_size_t],
@@ -276,6 +281,41 @@ class Context:
         _check(_lib.wce_synth_frames(self.handle, _addr(tx), _addr(rx), _addr(rx_pre), frame_stride, block_stride,
                                      pre_stride, first_frame, n_frames, seed, _addr(h_shared), amplitude, ow2,
                                      stream), "wce_synth_frames")
+
+    def front_end_blocks(self, samples, n_frames, n_blocks=NBLK, sym=None, packet_stride=None,
+                         frame_stride=NBLK * NSC, block_stride=NSC, stream=None):
+        """Time-domain packets (device) -> 53-bin OFDM symbols (WiFi_blocks_extraction.m)."""
+        ps = packet_stride if packet_stride is not None else SAMPLES_PER_BLOCK * n_blocks
+        _check(_lib.wce_front_end_blocks(self.handle, _addr(samples), ps, n_frames, n_blocks, _addr(sym),
+                                         frame_stride, block_stride, stream), "wce_front_end_blocks")
+
+    def front_end_preamble(self, lptot, n_frames, lptot_len, pre_fft, ow2=None, lptot_stride=None,
+                           pre_stride=NSC, stream=None):
+        """Long training fields (device) -> preamble FFT [53] and sigma^2 per frame (WiFi_RX.m:18-30)."""
+        ls = lptot_stride if lptot_stride is not None else lptot_len
+        _check(_lib.wce_front_end_preamble(self.handle, _addr(lptot), ls, lptot_len, n_frames, _addr(pre_fft),
+                                           pre_stride, _addr(ow2), stream), "wce_front_end_preamble")
+
+    def front_end_host(self, packets, lptot=None, n_blocks=NBLK):
+        """Convenience: host packets [B][80 n_blocks] (+ lptot [B][L]) -> (sym [B][n_blocks][53],
+        pre_fft [B][53] or None, ow2 [B] or None)."""
+        packets = _as_c128(packets)
+        B = packets.shape[0]
+        dp = DeviceArray.from_numpy(packets)
+        dsym = DeviceArray((B, n_blocks, NSC), zero=True)
+        self.front_end_blocks(dp, B, n_blocks, dsym, packet_stride=packets.shape[1], frame_stride=n_blocks * NSC)
+        pre = ow2 = None
+        if lptot is not None:
+            lptot = _as_c128(lptot)
+            dl = DeviceArray.from_numpy(lptot)
+            dpre = DeviceArray((B, NSC), zero=True)
+            dow2 = DeviceArray((B,), np.float64, zero=True)
+            self.front_end_preamble(dl, B, lptot.shape[1], dpre, dow2)
+        synchronize()
+        sym = dsym.numpy()
+        if lptot is not None:
+            pre, ow2 = dpre.numpy(), dow2.numpy()
+        return sym, pre, ow2
 
     def estimate_host(self, tx, rx, rx_pre=None, mask=ALL, block=0, eq_source=PS_LINEAR, semantics=SEM_C,
                       tx_pre=None):

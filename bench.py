@@ -36,6 +36,8 @@ FLOP_TRSV = 8.0 * N * N                  # forward (bordered row) + back substit
 FLOP_APPLY = 8.0 * N * N                 # H = C w
 FLOP_SOLVE_TXT = FLOP_CHOL + FLOP_RYY + FLOP_TRSV
 FLOP_SOLVE_REF = FLOP_CHOL + FLOP_TRSV   # REF: a = 0, Ryy is the diagonal 2 ow2 I (no build term)
+BYTES_FE_BLOCK = 64 * 16 + N * 16        # front end: 64 useful samples in (CP skipped) + 53 bins out
+BYTES_FE_PRE = 128 * 16 + N * 16 + 8     # two LTF copies in, preamble FFT + sigma^2 out
 BYTES_LS_CFG2 = 2672                     # LT_LS + PS_Linear: rx_pre 848 + pilots 128 + 2 x 848 out
 PEAK_FP64_TFLOPS = 78.6                  # MI355X FP64 vector = FP64 matrix (spec)
 PEAK_HBM_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -239,6 +241,7 @@ def main():
         # LS path (config 2: LT_LS + PS_Linear), HBM-bound
         if dist.rank == 0:
             res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
+            res["front_end"] = bench_front(wce, ctx, stream, B, reps)
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
         res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
@@ -276,6 +279,39 @@ def bench_ls(wce, ctx, stream, n, reps):
         t = time_events(wce, stream, f, reps)
         gbs = BYTES_LS_CFG2 * nb / (t * 1e-3) / 1e9
         out[label] = {"frames": nb, "avg_launch_ms": t, "frames_per_s": nb / (t * 1e-3), "achieved_GBs": gbs,
+                      "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
+    return out
+
+
+def bench_front(wce, ctx, stream, n, reps):
+    """Time-domain front end over n frames of 15 x 80-sample
+    blocks + a 160-sample LTF each: HBM-bound, algorithmic bytes per block
+    1,872 (64 samples in, 53 bins out), per LTF 2,904."""
+    s = stream.handle
+    rng = np.random.default_rng(2)
+    chunk = min(n, 8192)
+    pk = wce.DeviceArray((n, NBLK * 80))
+    lt = wce.DeviceArray((n, 160))
+    lib = wce.load()
+    src = (rng.standard_normal((chunk, NBLK * 80)) + 1j * rng.standard_normal((chunk, NBLK * 80))) * 0.01
+    srcl = (rng.standard_normal((chunk, 160)) + 1j * rng.standard_normal((chunk, 160))) * 0.01
+    for off in range(0, n, chunk):
+        m = min(chunk, n - off)
+        assert lib.wce_memcpy_htod(pk.addr + off * NBLK * 80 * 16, src[:m].ctypes.data, m * NBLK * 80 * 16) == 0
+        assert lib.wce_memcpy_htod(lt.addr + off * 160 * 16, srcl[:m].ctypes.data, m * 160 * 16) == 0
+    sym = wce.DeviceArray((n, NBLK, N))
+    pre = wce.DeviceArray((n, N))
+    ow2 = wce.DeviceArray((n,), np.float64)
+    fb = lambda: ctx.front_end_blocks(pk, n, NBLK, sym, stream=s)
+    fp = lambda: ctx.front_end_preamble(lt, n, 160, pre, ow2, stream=s)
+    out = {"workload": f"{n} frames x 15 blocks of 80 samples + 160-sample LTF (WiFi_blocks_extraction.m, WiFi_RX.m:18-30)"}
+    for label, f, per, units in (("blocks", fb, BYTES_FE_BLOCK, n * NBLK), ("preamble", fp, BYTES_FE_PRE, n)):
+        for _ in range(3):
+            f()
+        t = time_events(wce, stream, f, reps)
+        gbs = per * units / (t * 1e-3) / 1e9
+        out[label] = {"kernel": f"front_kernel<{label == 'preamble'}>", "avg_launch_ms": t,
+                      "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_unit": per, "achieved_GBs": gbs,
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
     return out
 

@@ -160,6 +160,29 @@ int wce_synth_frames(wce_ctx *ctx, wce_complex *tx, wce_complex *rx, wce_complex
                      int64_t first_frame, int64_t n_frames, uint64_t seed,
                      const wce_complex *h_shared, double amplitude, double ow2, void *stream);
 
+/* ---- time-domain front end (MATLAB only, no C original) ----
+ * WiFi_blocks_extraction.m:1-11: OFDM block b of frame f is the 80 samples
+ * samples[f*packet_stride + 80 b + (0..79)]; the 16-sample cyclic prefix is
+ * dropped and the last 64 go through a 64-point DFT, circshift(., 26), and
+ * the first 53 bins are kept:
+ *     sym[f*frame_stride + b*block_stride + i] = DFT64[(i - 26) mod 64],  i < 53.
+ * Used for tx and rx packets alike (WiFi_RX.m:42-43).  The output is the
+ * wce_frames layout, so wce_estimate can consume it directly.  The ctx only
+ * selects the device (its state need not be loaded). */
+enum { WCE_FFT_SIZE = 64, WCE_SAMPLES_PER_BLOCK = 80 };
+int wce_front_end_blocks(wce_ctx *ctx, const wce_complex *samples, int64_t packet_stride, int64_t n_frames,
+                         int32_t n_blocks, wce_complex *sym, int64_t frame_stride, int64_t block_stride,
+                         void *stream);
+
+/* WiFi_RX.m:18-30: the long training field of frame f is
+ * lptot[f*lptot_stride + (0..lptot_len-1)]; its last 64 samples are p1 and
+ * the 64 before them p2.  pre_fft[f*pre_stride + i] = circshift(DFT64((p1+p2)/2), 26)[i],
+ * i < 53 (feed it to wce_frames.rx_pre / tx_pre), and, if ow2 != NULL,
+ * ow2[f] = sum |p2 - p1|^2 / (2*64), the noise estimate of WiFi_RX.m:30. */
+int wce_front_end_preamble(wce_ctx *ctx, const wce_complex *lptot, int64_t lptot_stride, int64_t lptot_len,
+                           int64_t n_frames, wce_complex *pre_fft, int64_t pre_stride, double *ow2,
+                           void *stream);
+
 /* ---- thin runtime helpers (so C hosts and tests need no other HIP binding) ---- */
 int wce_device_count(int *count);
 int wce_set_device(int device);

@@ -388,6 +388,49 @@ void orc_matlab_lt_ls(const ldc *tx_pre, const ldc *rx_pre, ldc *H)
 }
 
 /* ------------------------------------------------------------------------
+ * Time-domain front end (MATLAB only; no C original).  A direct 64-point DFT
+ * in long double (twiddles from cexpl), not an FFT, so the checker shares no
+ * algorithm with the GPU kernel.  Pinned by matlab.mat (rx_packet -> rx_symb,
+ * rx_lptot -> rx_preamble_fft).
+ * ------------------------------------------------------------------------ */
+#define NFFT 64         /* K            WiFi_RX.m:10 */
+#define NCP 16          /* sampXblock - K, WiFi_RX.m:12 */
+
+/* X = circshift(fft(x, 64), 26)(1:53): out[i] = DFT(x)[(i - 26) mod 64] */
+static void dft64_useful(const ldc *x, ldc *out)
+{
+    for (int i = 0; i < N; i++) {
+        const int k = (i - 26 + NFFT) % NFFT;
+        ldc acc = 0;
+        for (int n = 0; n < NFFT; n++)
+            acc += x[n] * cexpl(-2.0L * I * acosl(-1.0L) * (long double)((n * k) % NFFT) / NFFT);
+        out[i] = acc;
+    }
+}
+
+/* WiFi_blocks_extraction.m:4-9: block b = samples [80 b, 80 b + 80), CP dropped */
+void orc_front_blocks(const ldc *samples, int n_blocks, ldc *sym)
+{
+    for (int b = 0; b < n_blocks; b++) dft64_useful(samples + (NFFT + NCP) * b + NCP, sym + (long)b * N);
+}
+
+/* WiFi_RX.m:24-30: p1 = last 64 samples, p2 = the 64 before; fft of their
+ * mean; ow2 = sum |p2 - p1|^2 / (2 K) */
+void orc_front_preamble(const ldc *lptot, long len, ldc *pre_fft, long double *ow2)
+{
+    const ldc *p1 = lptot + len - NFFT, *p2 = lptot + len - 2 * NFFT;
+    ldc avg[NFFT];
+    long double s = 0;
+    for (int n = 0; n < NFFT; n++) {
+        avg[n] = (p1[n] + p2[n]) / 2;
+        const ldc d = p2[n] - p1[n];
+        s += creall(d * conjl(d));
+    }
+    dft64_useful(avg, pre_fft);
+    *ow2 = s / (2 * NFFT);
+}
+
+/* ------------------------------------------------------------------------
  * fp64 batched CPU paths, OpenMP over frames.  These are the "port" CPU
  * baselines bench.py times on the GPU host (same algorithm as the GPU
  * kernels, race-free; the reference's own OpenMP path crashes).

@@ -142,6 +142,22 @@ def matlab_lt_ls(tx_pre, rx_pre):
     return _est("orc_matlab_lt_ls", tx_pre, rx_pre)
 
 
+def front_blocks(samples, n_blocks):
+    """time-domain packet -> [n_blocks][53] useful subcarriers (WiFi_blocks_extraction.m)."""
+    out = np.zeros((n_blocks, N), LD)
+    load().orc_front_blocks(_p(_ld(samples)), ctypes.c_int(n_blocks), _p(out))
+    return out
+
+
+def front_preamble(lptot):
+    """long training field -> (preamble FFT [53], ow2) (WiFi_RX.m:24-30)."""
+    x = _ld(lptot)
+    out = np.zeros(N, LD)
+    s = np.zeros(1, np.longdouble)
+    load().orc_front_preamble(_p(x), ctypes.c_long(x.shape[0]), _p(out), _p(s))
+    return out, s[0]
+
+
 def pilot_mask():
     m = np.zeros(N, np.uint8)
     m[list(PILOTS)] = 1

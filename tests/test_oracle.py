@@ -165,3 +165,27 @@ def test_cpu_port_matches_oracle(oracle, golden):
     H, _ = oracle.bench_mmse_f64(C, oracle.pilot_mask(), 0.0, 2 * r["ow2"], tx, rx, N, 2)
     for f in range(r["frames_tx"].shape[0]):
         assert normrel(H[f], from_split(r["ps_mmse_ref"][0, f])) < 1e-13
+
+
+def test_front_end_blocks_matlab_pin(oracle, golden):
+    """WiFi_blocks_extraction.m: packet -> 80-sample blocks -> CP drop -> fft64
+    -> circshift 26 -> 53 bins; matlab.mat's tx/rx_symb reproduced."""
+    m = golden["matlab"]
+    for pk, sk in (("rx_packet", "rx_symb"), ("tx_packet", "tx_symb")):
+        sym = oracle.front_blocks(m[pk], NBLK)
+        ref = m[sk].T
+        assert np.max(np.abs((sym - ref).astype(np.complex128))) / np.max(np.abs(ref)) < 1e-14, pk
+
+
+def test_front_end_preamble_matlab_pin(oracle, golden):
+    """WiFi_RX.m:18-30: preamble copies, averaged FFT, sigma^2."""
+    m = golden["matlab"]
+    assert np.array_equal(m["rx_preamble1"], m["rx_lptot"][-64:])
+    assert np.array_equal(m["rx_preamble2"], m["rx_lptot"][-128:-64])
+    for lk, fk in (("rx_lptot", "rx_preamble_fft"), ("tx_lptot", "tx_preamble_fft")):
+        pre, ow2 = oracle.front_preamble(m[lk])
+        assert normrel(pre, m[fk]) < 1e-14, lk
+    _, ow2 = oracle.front_preamble(m["rx_lptot"])
+    d = m["rx_preamble2"] - m["rx_preamble1"]
+    assert abs(float(ow2) - np.sum(np.abs(d) ** 2) / 128) < 1e-15 * abs(float(ow2))
+    assert 0 < float(ow2) < 1e-3
