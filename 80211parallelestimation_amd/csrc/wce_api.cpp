@@ -17,7 +17,12 @@ struct wce_ctx {
     bool ready = false;
     bool has_host = false;
     State host;                 // host copy when built locally
+    int32_t mode = -1;          // State::mode, cached when the state becomes valid
+    double *ws = nullptr;       // WCE_MMSE_FRAME_COV workspace: h | g | u | w, [ws_frames][64] complex each
+    int64_t ws_frames = 0;
 };
+
+static constexpr int64_t WS_LD = 64;   // row stride (complex) of the workspace vectors
 
 static thread_local std::string g_err;
 
@@ -107,6 +112,7 @@ int wce_ctx_create(wce_ctx **out, int device, const wce_complex *tx_pre, const w
     rc = wce::host_build_state(&c->host, wce::host_reference_F(), wce::host_reference_invF(), hlt, txl, ow2, mode);
     if (rc) { wce_ctx_destroy(c); return fail(rc, "state build"); }
     c->has_host = true;
+    c->mode = mode;
     DeviceGuard g(device);
     hipError_t e = hipMemcpy(c->d_state, &c->host, sizeof(State), hipMemcpyHostToDevice);
     if (e != hipSuccess) { wce_ctx_destroy(c); return hipfail(e, "upload state"); }
@@ -118,9 +124,10 @@ int wce_ctx_create(wce_ctx **out, int device, const wce_complex *tx_pre, const w
 int wce_ctx_destroy(wce_ctx *c)
 {
     if (!c) return WCE_OK;
-    if (c->d_state) {
+    if (c->d_state || c->ws) {
         DeviceGuard g(c->device);
-        (void)hipFree(c->d_state);
+        if (c->d_state) (void)hipFree(c->d_state);
+        if (c->ws) (void)hipFree(c->ws);
     }
     delete c;
     return WCE_OK;
@@ -143,6 +150,8 @@ int wce_ctx_mark_ready(wce_ctx *c)
     HIPCHECK(hipMemcpy(&magic, reinterpret_cast<char *>(c->d_state) + offsetof(State, magic), sizeof(magic),
                        hipMemcpyDeviceToHost), "read state magic");
     if (magic != wce::STATE_MAGIC) return fail(WCE_ESTATE, "state buffer does not hold a valid state");
+    HIPCHECK(hipMemcpy(&c->mode, reinterpret_cast<char *>(c->d_state) + offsetof(State, mode), sizeof(c->mode),
+                       hipMemcpyDeviceToHost), "read state mode");
     c->ready = true;
     return WCE_OK;
 }
@@ -154,6 +163,7 @@ int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
         return fail(WCE_ESTATE, "state blob has no valid magic");
     DeviceGuard g(c->device);
     HIPCHECK(hipMemcpy(c->d_state, host_state, sizeof(State), hipMemcpyHostToDevice), "upload state");
+    c->mode = static_cast<const State *>(host_state)->mode;
     c->ready = true;
     return WCE_OK;
 }
@@ -231,11 +241,88 @@ int wce_mmse_apply(wce_ctx *c, const wce_complex *W, wce_complex *H, int64_t str
     return rc ? fail(rc, "mmse_apply launch") : WCE_OK;
 }
 
+static int ensure_ws(wce_ctx *c, int64_t n)
+{
+    if (n <= c->ws_frames) return WCE_OK;
+    DeviceGuard g(c->device);
+    if (c->ws) {
+        HIPCHECK(hipDeviceSynchronize(), "sync before workspace growth");
+        (void)hipFree(c->ws);
+        c->ws = nullptr;
+        c->ws_frames = 0;
+    }
+    HIPCHECK(hipMalloc(&c->ws, (size_t)n * 4 * WS_LD * 2 * sizeof(double)), "hipMalloc(workspace)");
+    c->ws_frames = n;
+    return WCE_OK;
+}
+
+int wce_ctx_reserve(wce_ctx *c, int64_t n)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (n < 0) return fail(WCE_EINVAL, "n_frames < 0");
+    return ensure_ws(c, n);
+}
+
+// WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvecs) -> solve
+static int mmse_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
+{
+    const int64_t n = in->n_frames;
+    if (!in->rx_pre) return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
+    int rc = ensure_ws(c, n);
+    if (rc) return rc;
+    double *hw = c->ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
+    // H_LT of every frame (reuse the caller's LT_LS output when it was requested)
+    const double *h = hw;
+    int64_t hs = WS_LD;
+    if ((mask & WCE_EST_LT_LS) && out->lt_ls) {
+        h = reinterpret_cast<const double *>(out->lt_ls);
+        hs = out->out_stride;
+    } else {
+        wce::LsArgs a{};
+        a.tx = reinterpret_cast<const double *>(in->tx);
+        a.rx = reinterpret_cast<const double *>(in->rx);
+        a.rx_pre = reinterpret_cast<const double *>(in->rx_pre);
+        a.tx_pre = reinterpret_cast<const double *>(in->tx_pre);
+        a.fs = in->frame_stride; a.bs = in->block_stride; a.ps = in->pre_stride; a.n = n; a.blk = in->block;
+        a.matlab = in->semantics == WCE_SEM_MATLAB;
+        a.mask = WCE_EST_LT_LS;
+        a.lt = hw;
+        a.os = WS_LD;
+        rc = wce::launch_ls(c->d_state, a, stream);
+        if (rc) return fail(rc, "ls launch (H_LT for frame covariance)");
+    }
+    const State *st = c->d_state;
+    const int32_t mode = c->mode;
+    if (mode == WCE_MMSE_REF) {
+        rc = wce::launch_matvec(st->Mg, st->Mu, h, hs, gw, uw, WS_LD, n, false, stream);     // g, u
+        if (!rc) rc = wce::launch_matvec(st->Mw, nullptr, gw, WS_LD, ww, nullptr, WS_LD, n, true, stream);
+    } else {
+        rc = wce::launch_matvec(st->Mu, nullptr, h, hs, uw, nullptr, WS_LD, n, false, stream);
+    }
+    if (rc) return fail(rc, "matvec launch (frame covariance)");
+    wce::SolveArgs a{};
+    a.tx = reinterpret_cast<const double *>(in->tx);
+    a.rx = reinterpret_cast<const double *>(in->rx);
+    a.fs = in->frame_stride; a.bs = in->block_stride; a.n = n;
+    const bool ml = in->semantics == WCE_SEM_MATLAB;
+    a.blk = ml ? 0 : in->block;
+    a.nblk = ml ? 4 : 1;
+    a.w = reinterpret_cast<double *>(out->ps_mmse);
+    a.ws = out->out_stride;
+    a.cu = uw;
+    a.cw = mode == WCE_MMSE_REF ? ww : nullptr;
+    a.cs = WS_LD;
+    rc = wce::launch_mmse_solve(st, a, stream);
+    return rc ? fail(rc, "mmse_solve launch (frame covariance)") : WCE_OK;
+}
+
 int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
 {
     if (!c || !out) return fail(WCE_EINVAL, "null argument");
     if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
-    if (mask & ~0x3Fu) return fail(WCE_EINVAL, "unknown estimator bits");
+    if (mask & ~0x7Fu) return fail(WCE_EINVAL, "unknown estimator bits");
+    if ((mask & WCE_MMSE_FRAME_COV) && !(mask & WCE_EST_PS_MMSE))
+        return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV modifies WCE_EST_PS_MMSE");
     const bool eq = (mask & WCE_EQUALIZE) != 0;
     int rc = check_frames(in, eq);
     if (rc) return rc;
@@ -277,6 +364,7 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
         rc = wce::launch_ls(c->d_state, a, stream);
         if (rc) return fail(rc, "ls launch");
     }
+    if (mask & WCE_MMSE_FRAME_COV) return mmse_frame_cov(c, in, out, mask, stream);
     if (mask & WCE_EST_PS_MMSE) {
         rc = wce_mmse_solve(c, in, out->ps_mmse, out->out_stride, stream);
         if (rc) return rc;

@@ -19,6 +19,15 @@ constexpr int32_t STATE_MAGIC = 0x80211;
 struct State {
     double C[CLD * CLD * 2];   // MMSE covariance operator, row-major, zero-padded to 64 x 64
                                // (65,536 B): kernels index it without bounds checks
+    // Per-frame covariance (WCE_MMSE_FRAME_COV): C_f = u_f w_f^T is rank 1 in
+    // both modes, with u_f, w_f batched matrix-vector products of the frame's
+    // own H_LT (padded 64 x 64, row-major, applied on MFMA):
+    //   REF      g = Mg h (invF_ref), u = Mu h (F invF_ref), w = Mw q(g),
+    //            q = re g - im g, Mw[j][c] = re F[j][c] - im F[j][c] (main.c:186-203)
+    //   TEXTBOOK u = Mu h (F conj(F) / 53, ifft then F), w = conj(u)
+    double Mg[CLD * CLD * 2];
+    double Mu[CLD * CLD * 2];
+    double Mw[CLD * CLD * 2];
     double h_lt[NPAD * 2];     // LT_LS of the shared preamble (main.c:66-75)
     double tx_pre[NPAD * 2];   // shared tx preamble FFT
     double sinc[4][NPAD];      // sinc((k - P_p)/14) in double (utils.c:727-733)
@@ -69,6 +78,10 @@ struct SolveArgs {
     int32_t nblk;             // blocks averaged per frame (1; 4 in MATLAB semantics)
     double *w;
     int64_t ws;
+    // per-frame covariance (null = shared C): C_f = cu_f cw_f^T, rows of stride cs;
+    // cw == null: cw_f = conj(cu_f).  Output is then H itself (no apply step).
+    const double *cu, *cw;
+    int64_t cs;
 };
 struct SynthArgs {
     double *tx, *rx, *rx_pre;
@@ -92,6 +105,10 @@ int launch_ls(const State *st, const LsArgs &a, void *stream);
 int launch_front(const FrontArgs &a, bool preamble, void *stream);
 int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream);
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream);
+// Y1[f] = M1 X[f] (and Y2[f] = M2 X[f] if M2), M = padded 64 x 64 complex;
+// qin: X replaced by (re X - im X, 0) first.
+int launch_matvec(const double *M1, const double *M2, const double *X, int64_t xs, double *Y1, double *Y2,
+                  int64_t ys, int64_t n, bool qin, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 
 }  // namespace wce

@@ -287,8 +287,11 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #endif
 // One block's solve; returns w_lane = x_lane z_lane (0 for lanes >= 53 is
 // not guaranteed: callers store lanes < 53 only).
+// FC: per-frame rank-1 covariance C_f = cu_f cw_f^T (SolveArgs::cu/cw, frame f)
+// instead of the shared State::C.
+template <bool FC>
 __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
-                                               int64_t base)
+                                               int64_t base, int64_t f)
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
@@ -306,7 +309,20 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     const double ac = st->acoef, bc = st->bcoef;
     double2 A[RB][RB];
     {
-        if (ac != 0.0) {   // a X C X'  (C zero-padded: no bounds checks)
+        if (FC && ac != 0.0) {   // a X u w^T X': both factors staged in the pivot buffers
+            const bool act = lane < NSC;
+            const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+            const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+            const double2 xl = s.x[lane];
+            s.u[0][lane] = cscale(cmul(xl, uf), ac);
+            s.u[1][lane] = cmul(wf, cconj(xl));
+            wave_lds_sync();
+#pragma unroll
+            for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+                for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = cmul(s.u[0][p + 8 * aa], s.u[1][q + 8 * bb]);
+            wave_lds_sync();   // publish_col<0> reuses s.u[0]
+        } else if (!FC && ac != 0.0) {   // a X C X'  (C zero-padded: no bounds checks)
             double2 yr[RB], xc[RB];
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa) {
@@ -379,7 +395,7 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kerne
     __shared__ SolveLds s;
     const int64_t f = blockIdx.x;
     if (f >= a.n) return;
-    const double2 w = solve_block(st, a, s, f * a.fs + (int64_t)a.blk * a.bs);
+    const double2 w = solve_block<false>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
     if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, w);
 }
 
@@ -394,10 +410,40 @@ __global__ __launch_bounds__(64, 2) void mmse_solve_avg_kernel(const State *__re
     if (f >= a.n) return;
     double2 acc = make_double2(0.0, 0.0);
     for (int b = 0; b < a.nblk; ++b) {
-        acc = cadd(acc, solve_block(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs));
+        acc = cadd(acc, solve_block<false>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f));
         wave_lds_sync();   // the next block overwrites s
     }
     if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, cscale(acc, 1.0 / a.nblk));
+}
+
+// Per-frame covariance (WCE_MMSE_FRAME_COV): C_f = u_f w_f^T, so the product
+// C_f W_f collapses to u_f (w_f . W_f): a wave reduction replaces the MFMA
+// apply, and the kernel writes H directly.  Averages nblk blocks (MATLAB).
+template <bool AVG>
+__global__ __launch_bounds__(64, AVG ? 2 : WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_kernel(
+    const State *__restrict__ st, SolveArgs a)
+{
+    __shared__ SolveLds s;
+    const int64_t f = blockIdx.x;
+    if (f >= a.n) return;
+    const int lane = threadIdx.x;
+    const bool act = lane < NSC;
+    double2 dot = make_double2(0.0, 0.0);
+    const int nb = AVG ? a.nblk : 1;
+    for (int b = 0; b < nb; ++b) {
+        const double2 wz = solve_block<true>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
+        const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+        const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+        double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
+        dot = cadd(dot, t);
+        if (AVG) wave_lds_sync();   // the next block overwrites s
+    }
+    if (act) {
+        const double2 uf = ld2(a.cu, f * a.cs + lane);
+        st2(a.w, f * a.ws + lane, cmul(uf, AVG ? cscale(dot, 1.0 / a.nblk) : dot));
+    }
 }
 
 // =====================================================================
@@ -411,8 +457,12 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 constexpr int KSTEPS = 14;   // 56 >= 53
 constexpr int APPLY_WAVES = 4;
 
-__global__ __launch_bounds__(256) void mmse_apply_kernel(const State *__restrict__ st, const double *W, double *H,
-                                                         int64_t stride, int64_t n)
+// Y1[f] = M1 X[f] (and Y2[f] = M2 X[f]) for 16-frame tiles; M padded 64 x 64.
+// QIN: the input is replaced by (re X - im X, 0) (main.c:188's real "conj").
+template <bool QIN, bool TWO>
+__global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ M1, const double *__restrict__ M2,
+                                                     const double *X, int64_t xs, double *Y1, double *Y2,
+                                                     int64_t ys, int64_t n)
 {
     const int lane = threadIdx.x & 63;
     const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
@@ -423,27 +473,33 @@ __global__ __launch_bounds__(256) void mmse_apply_kernel(const State *__restrict
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
         const int j = 4 * s + kl;
-        double2 v = (fa < n && j < NSC) ? ld2(W, fa * stride + j) : make_double2(0, 0);
+        double2 v = (fa < n && j < NSC) ? ld2(X, fa * xs + j) : make_double2(0, 0);
+        if constexpr (QIN) v = make_double2(v.x - v.y, 0.0);
         ar[s] = v.x; ai[s] = v.y; nai[s] = -v.y;
     }
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int i = 16 * nt + ml;
-        v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
+    for (int m = 0; m < (TWO ? 2 : 1); ++m) {
+        const double *M = m == 0 ? M1 : M2;
+        double *Y = m == 0 ? Y1 : Y2;
 #pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) {
-            const int j = 4 * s + kl;
-            const double2 c = ld2(st->C, i * CLD + j);   // zero-padded 64 x 64
-            accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
-            accr = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[s], c.y, accr, 0, 0, 0);
-            acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
-            acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
-        }
-        if (i < NSC) {
+        for (int nt = 0; nt < 4; ++nt) {
+            const int i = 16 * nt + ml;
+            v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t fr = f0 + kl + 4 * r;
-                if (fr < n) st2(H, fr * stride + i, make_double2(accr[r], acci[r]));
+            for (int s = 0; s < KSTEPS; ++s) {
+                const int j = 4 * s + kl;
+                const double2 c = ld2(M, i * CLD + j);   // zero-padded 64 x 64
+                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
+                if constexpr (!QIN) accr = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[s], c.y, accr, 0, 0, 0);
+                acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
+                if constexpr (!QIN) acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
+            }
+            if (i < NSC) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t fr = f0 + kl + 4 * r;
+                    if (fr < n) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
+                }
             }
         }
     }
@@ -545,7 +601,11 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
     if (a.n > 0x7fffffffll) return WCE_EINVAL;
-    if (a.nblk > 1)
+    if (a.cu && a.nblk > 1)
+        hipLaunchKernelGGL(mmse_solve_fc_kernel<true>, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    else if (a.cu)
+        hipLaunchKernelGGL(mmse_solve_fc_kernel<false>, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    else if (a.nblk > 1)
         hipLaunchKernelGGL(mmse_solve_avg_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
     else
         hipLaunchKernelGGL(mmse_solve_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
@@ -554,11 +614,20 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream)
 {
+    return launch_matvec(st->C, nullptr, W, stride, H, nullptr, stride, n, false, stream);
+}
+
+int launch_matvec(const double *M1, const double *M2, const double *X, int64_t xs, double *Y1, double *Y2,
+                  int64_t ys, int64_t n, bool qin, void *stream)
+{
     if (n <= 0) return WCE_OK;
-    const int64_t tiles = (n + 15) / 16;
-    const int64_t blocks = (tiles + APPLY_WAVES - 1) / APPLY_WAVES;
-    hipLaunchKernelGGL(mmse_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, W, H,
-                       stride, n);
+    const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
+    const dim3 g((unsigned)blocks), b(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (qin && M2) return WCE_EINVAL;
+    if (qin) hipLaunchKernelGGL((matvec_kernel<true, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
+    else if (M2) hipLaunchKernelGGL((matvec_kernel<false, true>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
+    else hipLaunchKernelGGL((matvec_kernel<false, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
     return hip_status(hipGetLastError());
 }
 

@@ -197,11 +197,36 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
         st->bcoef = ow2;
         st->xmask = (1ull << NSC) - 1;
     }
-    for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) {
-            st->C[2 * (i * CLD + j)] = (double)__real__ C[i * n + j];
-            st->C[2 * (i * CLD + j) + 1] = (double)__imag__ C[i * n + j];
+    auto put = [n](double *dst, const std::vector<cld> &M) {
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                dst[2 * (i * CLD + j)] = (double)__real__ M[i * n + j];
+                dst[2 * (i * CLD + j) + 1] = (double)__imag__ M[i * n + j];
+            }
+    };
+    put(st->C, C);
+    // per-frame covariance operators (State::Mg/Mu/Mw), products in 80 bits
+    {
+        std::vector<cld> Mu(n * n), rhs(n * n);
+        if (mode == WCE_MMSE_REF) {
+            std::vector<cld> invF(n * n), Mw(n * n);
+            for (int i = 0; i < n * n; i++) invF[i] = from(invFl[i]);
+            mat_mul(F.data(), n, n, invF.data(), n, Mu.data());
+            for (int j = 0; j < n; j++)
+                for (int c = 0; c < n; c++)
+                    Mw[j * n + c] = mk((long double)(creal_d(F[j * n + c]) - cimag_d(F[j * n + c])), 0.0L);
+            put(st->Mg, invF);
+            put(st->Mw, Mw);
+        } else {
+            for (int i = 0; i < n * n; i++) {
+                rhs[i] = F[i];
+                __imag__ rhs[i] = -__imag__ rhs[i];
+                rhs[i] = rhs[i] / mk((long double)n, 0.0L);
+            }
+            mat_mul(F.data(), n, n, rhs.data(), n, Mu.data());
         }
+        put(st->Mu, Mu);
+    }
     for (int k = 0; k < n; k++) {
         st->h_lt[2 * k] = (double)H_LS[k].re;
         st->h_lt[2 * k + 1] = (double)H_LS[k].im;

@@ -32,6 +32,7 @@ PS_MMSE = 1 << 4
 EQUALIZE = 1 << 5
 LS_ALL = 0xF
 ALL = 0x3F
+FRAME_COV = 1 << 6   # WCE_MMSE_FRAME_COV: PS_MMSE covariance from each frame's own preamble
 
 MMSE_REF = 0
 MMSE_TEXTBOOK = 1
@@ -86,6 +87,7 @@ ABI = {
     "wce_ctx_create": [POINTER(c_void_p), c_int, c_void_p, c_void_p, c_double, c_int],
     "wce_ctx_create_empty": [POINTER(c_void_p), c_int],
     "wce_ctx_destroy": [c_void_p],
+    "wce_ctx_reserve": [c_void_p, c_int64],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
@@ -227,6 +229,10 @@ class Context:
             raise ValueError("tx_pre / rx_pre must hold 53 subcarriers")
         _check(lib.wce_ctx_create(byref(self.handle), device, tp.ctypes.data_as(c_void_p),
                                   rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_ctx_create")
+
+    def reserve(self, n_frames):
+        """Pre-size the WCE_MMSE_FRAME_COV workspace (no allocation inside estimate)."""
+        _check(_lib.wce_ctx_reserve(self.handle, n_frames), "wce_ctx_reserve")
 
     def close(self):
         if self.handle is not None and self.handle.value:

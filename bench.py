@@ -220,7 +220,7 @@ def main():
                            "flop_per_frame": fl_solve, "frames_per_launch": B, "avg_launch_ms": t_solve,
                            "note": "peak = MI355X FP64 (vector = matrix, spec); traffic: see profiles/"}
         ach_apply = FLOP_APPLY * B / (t_apply * 1e-3) / 1e12
-        res["apply_kernel"] = {"kernel": "mmse_apply_kernel (v_mfma_f64_16x16x4)", "avg_launch_ms": t_apply,
+        res["apply_kernel"] = {"kernel": "matvec_kernel<false,false> = H = C W (v_mfma_f64_16x16x4)", "avg_launch_ms": t_apply,
                                "achieved_tflops": ach_apply, "frac_fp64_peak": ach_apply / PEAK_FP64_TFLOPS}
         res["mmse_total_flop_per_frame"] = fl_solve + FLOP_APPLY
         res["mmse_frac_of_roofline"] = value / dist.world * (fl_solve + FLOP_APPLY) / (PEAK_FP64_TFLOPS * 1e12)
@@ -242,6 +242,7 @@ def main():
         if dist.rank == 0:
             res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
             res["front_end"] = bench_front(wce, ctx, stream, B, reps)
+            res["frame_cov"] = bench_frame_cov(wce, make_ctx, stream, B, reps)
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
         res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
@@ -313,6 +314,29 @@ def bench_front(wce, ctx, stream, n, reps):
         out[label] = {"kernel": f"front_kernel<{label == 'preamble'}>", "avg_launch_ms": t,
                       "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_unit": per, "achieved_GBs": gbs,
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
+    return out
+
+
+def bench_frame_cov(wce, make_ctx, stream, n, reps):
+    """PS_MMSE with each frame's own preamble covariance (WCE_MMSE_FRAME_COV,
+    SURVEY 8(f)-4): LT_LS per frame, two (REF: three) batched MFMA matvecs for
+    the rank-1 factors of C_f, then the dense per-frame solve."""
+    s = stream.handle
+    out = {"workload": f"{n} frames, per-frame preamble, PS_MMSE | FRAME_COV"}
+    for label, m in (("textbook", wce.MMSE_TEXTBOOK), ("ref", wce.MMSE_REF)):
+        c = make_ctx(m)
+        tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+        c.synth(tx, rx, pre, n, seed=0x80211, stream=s)
+        H = wce.DeviceArray((n, N))
+        c.reserve(n)
+        fr = c.frames(tx, rx, n, rx_pre=pre)
+        o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+        f = lambda: c.estimate(fr, o, wce.PS_MMSE | wce.FRAME_COV, s)
+        for _ in range(3):
+            f()
+        t = time_events(wce, stream, f, reps)
+        out[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3)}
+        del c
     return out
 
 

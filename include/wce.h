@@ -56,6 +56,12 @@ enum {
 #define WCE_EST_PS_MMSE   (1u << 4)  /* WiFi_channel_estimation_PS_MMSE   main.c:148 */
 #define WCE_EQUALIZE      (1u << 5)  /* WiFi_Equalization.m (no C original) */
 #define WCE_EST_LS_ALL    (0xFu)
+/* PS_MMSE with each frame's own covariance: Rhh_f from the frame's preamble
+ * (wce_frames.rx_pre required) instead of the context's shared preamble, i.e.
+ * main.c's PS_MMSE called with H_EST_LS = that frame's LT_LS (main.c:41-53 per
+ * frame).  C_f = F Rhh_f F^H is rank 1, so it is never formed: two batched
+ * MFMA matrix-vector products give its factors and the solve writes H. */
+#define WCE_MMSE_FRAME_COV (1u << 6)
 
 /* MMSE semantics (DESIGN.md "MMSE contract"):
  *  REF      : main.c:148-212 with the NaN inverse(Ryy) repaired:
@@ -134,6 +140,11 @@ typedef struct {
                                    0 = WCE_EST_PS_LINEAR */
     uint32_t reserved;
 } wce_outputs;
+
+/* Pre-size the context's device workspace for WCE_MMSE_FRAME_COV batches of up
+ * to n_frames (3 KB per frame), so that wce_estimate never allocates.  Without
+ * it the first larger batch allocates (synchronously) and keeps the buffer. */
+int wce_ctx_reserve(wce_ctx *ctx, int64_t n_frames);
 
 /* Run the estimators selected in `mask` over all frames, asynchronously on
  * `stream`.  LS family + equalization: one HBM-streaming kernel; MMSE: the
