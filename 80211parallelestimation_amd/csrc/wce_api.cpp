@@ -18,6 +18,7 @@ struct wce_ctx {
     bool has_host = false;
     State host;                 // host copy when built locally
     int32_t mode = -1;          // State::mode, cached when the state becomes valid
+    bool fuse = true;           // config-5 fusion (wce_debug_set_fusion turns it off for A/B)
     double *ws = nullptr;       // WCE_MMSE_FRAME_COV workspace: h | g | u | w, [ws_frames][64] complex each
     int64_t ws_frames = 0;
 };
@@ -206,14 +207,29 @@ static int check_frames(const wce_frames *in, bool need_blocks)
     return WCE_OK;
 }
 
-int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_stride, void *stream)
+static wce::LsArgs ls_args(const wce_frames *in, const wce_outputs *out, uint32_t mask, uint32_t eq_src)
 {
-    if (!c) return fail(WCE_EINVAL, "null ctx");
-    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
-    int rc = check_frames(in, false);
-    if (rc) return rc;
-    if (in->n_frames == 0) return WCE_OK;
-    if (!W || (in->n_frames > 1 && w_stride < wce::NSC)) return fail(WCE_EINVAL, "bad W");
+    wce::LsArgs a{};
+    a.tx = reinterpret_cast<const double *>(in->tx);
+    a.rx = reinterpret_cast<const double *>(in->rx);
+    a.rx_pre = reinterpret_cast<const double *>(in->rx_pre);
+    a.tx_pre = reinterpret_cast<const double *>(in->tx_pre);
+    a.fs = in->frame_stride; a.bs = in->block_stride; a.ps = in->pre_stride; a.n = in->n_frames; a.blk = in->block;
+    a.matlab = in->semantics == WCE_SEM_MATLAB;
+    a.mask = mask & (WCE_EST_LS_ALL | WCE_EQUALIZE);
+    a.lt = reinterpret_cast<double *>(out->lt_ls);
+    a.lin = reinterpret_cast<double *>(out->ps_linear);
+    a.cub = reinterpret_cast<double *>(out->ps_cubic);
+    a.snc = reinterpret_cast<double *>(out->ps_sinc);
+    a.eq = reinterpret_cast<double *>(out->eq);
+    a.os = out->out_stride; a.eqfs = out->eq_frame_stride; a.eqbs = out->eq_block_stride;
+    a.eq_src = eq_src;
+    if (a.mask & WCE_EQUALIZE) a.mask |= eq_src;   // the blend needs that PS estimate
+    return a;
+}
+
+static wce::SolveArgs solve_args(const wce_frames *in, wce_complex *W, int64_t w_stride)
+{
     wce::SolveArgs a{};
     a.tx = reinterpret_cast<const double *>(in->tx);
     a.rx = reinterpret_cast<const double *>(in->rx);
@@ -223,6 +239,18 @@ int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_s
     a.nblk = ml ? 4 : 1;
     a.w = reinterpret_cast<double *>(W);
     a.ws = w_stride;
+    return a;
+}
+
+int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_stride, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    int rc = check_frames(in, false);
+    if (rc) return rc;
+    if (in->n_frames == 0) return WCE_OK;
+    if (!W || (in->n_frames > 1 && w_stride < wce::NSC)) return fail(WCE_EINVAL, "bad W");
+    wce::SolveArgs a = solve_args(in, W, w_stride);
     DeviceGuard g(c->device);
     rc = wce::launch_mmse_solve(c->d_state, a, stream);
     return rc ? fail(rc, "mmse_solve launch") : WCE_OK;
@@ -263,18 +291,19 @@ int wce_ctx_reserve(wce_ctx *c, int64_t n)
     return ensure_ws(c, n);
 }
 
-// WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvecs) -> solve
-static int mmse_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
+// WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvecs), into
+// the solve arguments.  lt_ready: the caller's LT_LS output already holds H_LT.
+static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready,
+                          wce::SolveArgs &sa, void *stream)
 {
     const int64_t n = in->n_frames;
     if (!in->rx_pre) return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
     int rc = ensure_ws(c, n);
     if (rc) return rc;
     double *hw = c->ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
-    // H_LT of every frame (reuse the caller's LT_LS output when it was requested)
     const double *h = hw;
     int64_t hs = WS_LD;
-    if ((mask & WCE_EST_LT_LS) && out->lt_ls) {
+    if (lt_ready) {
         h = reinterpret_cast<const double *>(out->lt_ls);
         hs = out->out_stride;
     } else {
@@ -292,28 +321,17 @@ static int mmse_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
         if (rc) return fail(rc, "ls launch (H_LT for frame covariance)");
     }
     const State *st = c->d_state;
-    const int32_t mode = c->mode;
-    if (mode == WCE_MMSE_REF) {
+    if (c->mode == WCE_MMSE_REF) {
         rc = wce::launch_matvec(st->Mg, st->Mu, h, hs, gw, uw, WS_LD, n, false, stream);     // g, u
         if (!rc) rc = wce::launch_matvec(st->Mw, nullptr, gw, WS_LD, ww, nullptr, WS_LD, n, true, stream);
     } else {
         rc = wce::launch_matvec(st->Mu, nullptr, h, hs, uw, nullptr, WS_LD, n, false, stream);
     }
     if (rc) return fail(rc, "matvec launch (frame covariance)");
-    wce::SolveArgs a{};
-    a.tx = reinterpret_cast<const double *>(in->tx);
-    a.rx = reinterpret_cast<const double *>(in->rx);
-    a.fs = in->frame_stride; a.bs = in->block_stride; a.n = n;
-    const bool ml = in->semantics == WCE_SEM_MATLAB;
-    a.blk = ml ? 0 : in->block;
-    a.nblk = ml ? 4 : 1;
-    a.w = reinterpret_cast<double *>(out->ps_mmse);
-    a.ws = out->out_stride;
-    a.cu = uw;
-    a.cw = mode == WCE_MMSE_REF ? ww : nullptr;
-    a.cs = WS_LD;
-    rc = wce::launch_mmse_solve(st, a, stream);
-    return rc ? fail(rc, "mmse_solve launch (frame covariance)") : WCE_OK;
+    sa.cu = uw;
+    sa.cw = c->mode == WCE_MMSE_REF ? ww : nullptr;
+    sa.cs = WS_LD;
+    return WCE_OK;
 }
 
 int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
@@ -343,34 +361,39 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
             (n > 1 && out->eq_frame_stride < (wce::NBLK - 1) * out->eq_block_stride + wce::NSC))
             return fail(WCE_EINVAL, "eq strides too small");
     }
+    if ((mask & WCE_MMSE_FRAME_COV) && !in->rx_pre)
+        return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
     DeviceGuard g(c->device);
-    if (mask & (WCE_EST_LS_ALL | WCE_EQUALIZE)) {
-        wce::LsArgs a{};
-        a.tx = reinterpret_cast<const double *>(in->tx);
-        a.rx = reinterpret_cast<const double *>(in->rx);
-        a.rx_pre = reinterpret_cast<const double *>(in->rx_pre);
-        a.tx_pre = reinterpret_cast<const double *>(in->tx_pre);
-        a.fs = in->frame_stride; a.bs = in->block_stride; a.ps = in->pre_stride; a.n = n; a.blk = in->block;
-        a.matlab = in->semantics == WCE_SEM_MATLAB;
-        a.mask = mask & (WCE_EST_LS_ALL | WCE_EQUALIZE);
-        a.lt = reinterpret_cast<double *>(out->lt_ls);
-        a.lin = reinterpret_cast<double *>(out->ps_linear);
-        a.cub = reinterpret_cast<double *>(out->ps_cubic);
-        a.snc = reinterpret_cast<double *>(out->ps_sinc);
-        a.eq = reinterpret_cast<double *>(out->eq);
-        a.os = out->out_stride; a.eqfs = out->eq_frame_stride; a.eqbs = out->eq_block_stride;
-        a.eq_src = eq_src;
-        if (eq) a.mask |= eq_src;   // the blend needs that PS estimate
-        rc = wce::launch_ls(c->d_state, a, stream);
+    const bool ls = (mask & (WCE_EST_LS_ALL | WCE_EQUALIZE)) != 0;
+    const bool mmse = (mask & WCE_EST_PS_MMSE) != 0;
+    // Config-5 fusion: the LS family and equalization ride in the MMSE solve's
+    // epilogue (C semantics); otherwise one HBM-streaming LS pass.
+    const bool fuse = c->fuse && ls && mmse && in->semantics == WCE_SEM_C;
+    const wce::LsArgs la = ls_args(in, out, mask, eq_src);
+    if (ls && !fuse) {
+        rc = wce::launch_ls(c->d_state, la, stream);
         if (rc) return fail(rc, "ls launch");
     }
-    if (mask & WCE_MMSE_FRAME_COV) return mmse_frame_cov(c, in, out, mask, stream);
-    if (mask & WCE_EST_PS_MMSE) {
-        rc = wce_mmse_solve(c, in, out->ps_mmse, out->out_stride, stream);
-        if (rc) return rc;
-        rc = wce_mmse_apply(c, out->ps_mmse, out->ps_mmse, out->out_stride, n, stream);
+    if (!mmse) return WCE_OK;
+    wce::SolveArgs sa = solve_args(in, out->ps_mmse, out->out_stride);
+    const bool fc = (mask & WCE_MMSE_FRAME_COV) != 0;
+    if (fc) {
+        rc = prep_frame_cov(c, in, out, !fuse && (mask & WCE_EST_LT_LS), sa, stream);
         if (rc) return rc;
     }
+    rc = fuse ? wce::launch_mmse_solve_ls(c->d_state, sa, la, stream) : wce::launch_mmse_solve(c->d_state, sa, stream);
+    if (rc) return fail(rc, "mmse_solve launch");
+    if (!fc) {   // H = C W in place (per-frame covariance writes H directly)
+        rc = wce::launch_mmse_apply(c->d_state, sa.w, sa.w, out->out_stride, n, stream);
+        if (rc) return fail(rc, "mmse_apply launch");
+    }
+    return WCE_OK;
+}
+
+extern "C" int wce_debug_set_fusion(wce_ctx *c, int on)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    c->fuse = on != 0;
     return WCE_OK;
 }
 

@@ -104,6 +104,8 @@ struct FrontArgs {
 int launch_ls(const State *st, const LsArgs &a, void *stream);
 int launch_front(const FrontArgs &a, bool preamble, void *stream);
 int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream);
+// solve + LS family + equalization of each frame in one launch (C semantics, one block)
+int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, void *stream);
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream);
 // Y1[f] = M1 X[f] (and Y2[f] = M2 X[f] if M2), M = padded 64 x 64 complex;
 // qin: X replaced by (re X - im X, 0) first.

@@ -24,6 +24,94 @@ namespace wce {
 constexpr int LS_WAVES = 4;   // waves per 256-thread workgroup
 constexpr int LS_FRAMES = 4;  // frames per wave iteration: all loads issued up front
 
+// Per-lane (subcarrier k) constants of the LS family, shared by ls_kernel and
+// the fused MMSE epilogue.
+struct LsLane {
+    double2 tpk, tden, hlt_shared;
+    double cq, s0, s1, s2, s3, alpha, dk0, dk1, dk2;
+    int seg;
+};
+__device__ __forceinline__ LsLane ls_lane(const State *__restrict__ st, const double *tx_pre, int k)
+{
+    LsLane c;
+    const double *txp = tx_pre ? tx_pre : st->tx_pre;
+    c.tpk = ld2(txp, k);
+    c.cq = c.tpk.x - c.tpk.y;                  // real "conj" of main.c:69-70
+    c.tden = make_double2(c.cq * c.tpk.x, c.cq * c.tpk.y);
+    c.hlt_shared = ld2(st->h_lt, k);
+    c.s0 = st->sinc[0][k]; c.s1 = st->sinc[1][k]; c.s2 = st->sinc[2][k]; c.s3 = st->sinc[3][k];
+    // linear interpolation segment (main.c:86-99): k < 19 seg 0, k < 33 seg 1, else seg 2
+    c.seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
+    c.alpha = (double)(k - (c.seg == 0 ? WCE_P0 : (c.seg == 1 ? WCE_P1 : WCE_P2))) * (1.0 / 14.0);
+    c.dk0 = (double)(k - WCE_P0); c.dk1 = (double)(k - WCE_P1); c.dk2 = (double)(k - WCE_P2);
+    return c;
+}
+
+// LT_LS of subcarrier k from the frame's preamble rp (or the shared one)
+template <bool ML>
+__device__ __forceinline__ double2 lt_ls_lane(const LsLane &c, bool have_rp, double2 rp, int k)
+{
+    double2 hlt = c.hlt_shared;
+    if (have_rp) {
+        if (ML)   // WiFi_channel_estimation_LT_LS.m: conj(tx) rx / (conj(tx) tx)
+            hlt = cscale(cmul(cconj(c.tpk), rp), 1.0 / (c.tpk.x * c.tpk.x + c.tpk.y * c.tpk.y));
+        else      // main.c:69-72: real "conj" c = re - im
+            hlt = cdiv(make_double2(c.cq * rp.x, c.cq * rp.y), c.tden);
+    }
+    return k == WCE_DC ? make_double2(0, 0) : hlt;   // main.c:74
+}
+
+// PS_Linear / PS_Cubic / PS_Sinc of subcarrier k from the pilot LS h0..h3
+template <bool ML>
+__device__ __forceinline__ void ps_lane(const LsLane &c, uint32_t mask, double2 h0, double2 h1, double2 h2,
+                                        double2 h3, double2 &hlin, double2 &hcub, double2 &hsnc)
+{
+    hlin = hcub = hsnc = make_double2(0, 0);
+    if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {      // main.c:86-99
+        const double2 lo = c.seg == 0 ? h0 : (c.seg == 1 ? h1 : h2);
+        const double2 hi = c.seg == 0 ? h1 : (c.seg == 1 ? h2 : h3);
+        hlin = cadd(lo, cscale(csub(hi, lo), c.alpha));
+    }
+    if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
+        const double r = 1.0 / 14.0;     // MATLAB (PS_Cubic.m:11-13): 14, 28, 42
+        const double r2 = ML ? 1.0 / 28.0 : r, r3 = ML ? 1.0 / 42.0 : r;
+        const double2 f01 = cscale(csub(h1, h0), r), f12 = cscale(csub(h2, h1), r), f23 = cscale(csub(h3, h2), r);
+        const double2 f012 = cscale(csub(f12, f01), r2), f123 = cscale(csub(f23, f12), r2);
+        const double2 f0123 = cscale(csub(f123, f012), r3);
+        hcub = cadd(cadd(cadd(h0, cscale(f01, c.dk0)), cscale(cscale(f012, c.dk0), c.dk1)),
+                    cscale(cscale(cscale(f0123, c.dk0), c.dk1), c.dk2));
+    }
+    if (mask & WCE_EST_PS_SINC)            // main.c:135-145
+        hsnc = cadd(cadd(cadd(cscale(h0, c.s0), cscale(h1, c.s1)), cscale(h2, c.s2)), cscale(h3, c.s3));
+}
+
+// store the requested LS-family outputs of frame f, subcarrier k, and run
+// WiFi_Equalization.m:1-9 over the frame's 15 blocks
+template <bool EQ>
+__device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
+                                         double2 hcub, double2 hsnc)
+{
+    const int64_t o = f * a.os + k;
+    if ((mask & WCE_EST_LT_LS) && a.lt) st2_nt(a.lt, o, hlt);
+    if ((mask & WCE_EST_PS_LINEAR) && a.lin) st2_nt(a.lin, o, hlin);
+    if ((mask & WCE_EST_PS_CUBIC) && a.cub) st2_nt(a.cub, o, hcub);
+    if ((mask & WCE_EST_PS_SINC) && a.snc) st2_nt(a.snc, o, hsnc);
+    if constexpr (EQ) {
+        const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
+        const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
+        double2 rv[NBLK];
+#pragma unroll
+        for (int b = 0; b < NBLK; b++) rv[b] = ld2(a.rx, rb + b * a.bs);
+#pragma unroll
+        for (int b = 0; b < NBLK; b++) {
+            const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
+            const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
+            const double2 e = k == WCE_DC ? make_double2(0, 0) : cdiv(rv[b], hu);
+            st2_nt(a.eq, eb + b * a.eqbs, e);
+        }
+    }
+}
+
 // ML: MATLAB semantics (WiFi_channel_estimation_*.m): pilot LS averaged over
 // blocks 0..3 -- Linear/Cubic/Sinc are linear in the pilot values, so the
 // 4-block average of the per-block estimates is the per-block formula applied
@@ -35,19 +123,10 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
     const int64_t nw = (int64_t)gridDim.x * LS_WAVES;
     const bool act = lane < NSC;
     const int k = act ? lane : 0;
-    const double *txp = a.tx_pre ? a.tx_pre : st->tx_pre;
-    const double2 tpk = ld2(txp, k);
-    const double cq = tpk.x - tpk.y;           // real "conj" of main.c:69-70
-    const double2 tden = make_double2(cq * tpk.x, cq * tpk.y);
-    const double2 hlt_shared = ld2(st->h_lt, k);
-    const double s0 = st->sinc[0][k], s1 = st->sinc[1][k], s2 = st->sinc[2][k], s3 = st->sinc[3][k];
+    const LsLane c = ls_lane(st, a.tx_pre, k);
     const uint32_t mask = a.mask;
     const bool need_lt = (mask & (WCE_EST_LT_LS | WCE_EQUALIZE)) != 0;
     const bool need_ps = (mask & (WCE_EST_PS_LINEAR | WCE_EST_PS_CUBIC | WCE_EST_PS_SINC | WCE_EQUALIZE)) != 0;
-    // linear interpolation segment (main.c:86-99): k < 19 seg 0, k < 33 seg 1, else seg 2
-    const int seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
-    const double alpha = (double)(k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) * (1.0 / 14.0);
-    const double dk0 = (double)(k - WCE_P0), dk1 = (double)(k - WCE_P1), dk2 = (double)(k - WCE_P2);
     const int pp = lane & 3;
     const int pil = pp == 0 ? WCE_P0 : pp == 1 ? WCE_P1 : pp == 2 ? WCE_P2 : WCE_P3;
     // lanes loading pilots: 4 (one block) or 16 (lane = 4 b + pilot, blocks 0..3)
@@ -84,55 +163,10 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
                 }
                 h0 = shfl_c(hp, 0); h1 = shfl_c(hp, 1); h2 = shfl_c(hp, 2); h3 = shfl_c(hp, 3);
             }
-            double2 hlt = hlt_shared;
-            if (rx_pre) {
-                if (ML)   // WiFi_channel_estimation_LT_LS.m: conj(tx) rx / (conj(tx) tx)
-                    hlt = cscale(cmul(cconj(tpk), rp[u]), 1.0 / (tpk.x * tpk.x + tpk.y * tpk.y));
-                else      // main.c:69-72: real "conj" c = re - im
-                    hlt = cdiv(make_double2(cq * rp[u].x, cq * rp[u].y), tden);
-            }
-            if (k == 26) hlt = make_double2(0, 0);   // main.c:74
-            double2 hlin = make_double2(0, 0);
-            if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {
-                const double2 lo = seg == 0 ? h0 : (seg == 1 ? h1 : h2);
-                const double2 hi = seg == 0 ? h1 : (seg == 1 ? h2 : h3);
-                hlin = cadd(lo, cscale(csub(hi, lo), alpha));
-            }
-            double2 hcub = make_double2(0, 0);
-            if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
-                const double r = 1.0 / 14.0;     // MATLAB (PS_Cubic.m:11-13): 14, 28, 42
-                const double r2 = ML ? 1.0 / 28.0 : r, r3 = ML ? 1.0 / 42.0 : r;
-                const double2 f01 = cscale(csub(h1, h0), r), f12 = cscale(csub(h2, h1), r),
-                              f23 = cscale(csub(h3, h2), r);
-                const double2 f012 = cscale(csub(f12, f01), r2), f123 = cscale(csub(f23, f12), r2);
-                const double2 f0123 = cscale(csub(f123, f012), r3);
-                hcub = cadd(cadd(cadd(h0, cscale(f01, dk0)), cscale(cscale(f012, dk0), dk1)),
-                            cscale(cscale(cscale(f0123, dk0), dk1), dk2));
-            }
-            double2 hsnc = make_double2(0, 0);
-            if (mask & WCE_EST_PS_SINC)            // main.c:135-145
-                hsnc = cadd(cadd(cadd(cscale(h0, s0), cscale(h1, s1)), cscale(h2, s2)), cscale(h3, s3));
-            if (act) {
-                const int64_t o = f * a.os + k;
-                if ((mask & WCE_EST_LT_LS) && a.lt) st2_nt(a.lt, o, hlt);
-                if ((mask & WCE_EST_PS_LINEAR) && a.lin) st2_nt(a.lin, o, hlin);
-                if ((mask & WCE_EST_PS_CUBIC) && a.cub) st2_nt(a.cub, o, hcub);
-                if ((mask & WCE_EST_PS_SINC) && a.snc) st2_nt(a.snc, o, hsnc);
-            }
-            if (EQ && act) {   // WiFi_Equalization.m:1-9
-                const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
-                const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
-                double2 rv[NBLK];
-#pragma unroll
-                for (int b = 0; b < NBLK; b++) rv[b] = ld2(a.rx, rb + b * a.bs);
-#pragma unroll
-                for (int b = 0; b < NBLK; b++) {
-                    const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
-                    const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
-                    const double2 e = k == 26 ? make_double2(0, 0) : cdiv(rv[b], hu);
-                    st2_nt(a.eq, eb + b * a.eqbs, e);
-                }
-            }
+            const double2 hlt = lt_ls_lane<ML>(c, rx_pre, rp[u], k);
+            double2 hlin, hcub, hsnc;
+            ps_lane<ML>(c, mask, h0, h1, h2, h3, hlin, hcub, hsnc);
+            if (act) ls_store<EQ>(a, f, k, mask, hlt, hlin, hcub, hsnc);
         }
     }
 }
@@ -399,6 +433,46 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kerne
     if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, w);
 }
 
+// Config 5 fused: the MMSE solve of one frame, then -- with the wave's
+// registers free -- that frame's LS family and equalization from the same
+// resident data (pilots from LDS, rx blocks streamed).  The HBM traffic of the
+// LS path overlaps the VALU-bound solve instead of running as its own pass.
+// C semantics, one block.  FC: per-frame covariance (H written directly).
+template <bool FC, bool EQ>
+__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_kernel(const State *__restrict__ st,
+                                                                                    SolveArgs a, LsArgs l)
+{
+    __shared__ SolveLds s;
+    const int64_t f = blockIdx.x;
+    if (f >= a.n) return;
+    const int lane = threadIdx.x;
+    const bool act = lane < NSC;
+    const int k = act ? lane : 0;
+    const double2 wz = solve_block<FC>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
+    if constexpr (FC) {
+        const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+        const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+        double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
+        if (act) st2(a.w, f * a.ws + lane, cmul(uf, t));
+    } else {
+        if (act) st2(a.w, f * a.ws + lane, wz);
+    }
+    // ---- LS family + equalization of frame f (main.c:66-146, WiFi_Equalization.m)
+    const uint32_t mask = l.mask;
+    if (!mask) return;
+    const double2 rp = l.rx_pre ? ld2(l.rx_pre, f * l.ps + k) : make_double2(0, 0);
+    const LsLane c = ls_lane(st, l.tx_pre, k);
+    // pilot LS from the frame data the solve staged in LDS (pilots are in X in both modes)
+    const double2 h0 = cdiv(s.rx[WCE_P0], s.x[WCE_P0]), h1 = cdiv(s.rx[WCE_P1], s.x[WCE_P1]);
+    const double2 h2 = cdiv(s.rx[WCE_P2], s.x[WCE_P2]), h3 = cdiv(s.rx[WCE_P3], s.x[WCE_P3]);
+    const double2 hlt = lt_ls_lane<false>(c, l.rx_pre != nullptr, rp, k);
+    double2 hlin, hcub, hsnc;
+    ps_lane<false>(c, mask, h0, h1, h2, h3, hlin, hcub, hsnc);
+    if (act) ls_store<EQ>(l, f, k, mask, hlt, hlin, hcub, hsnc);
+}
+
 // MATLAB semantics (WiFi_channel_estimation_PS_MMSE.m): the estimate is the
 // mean of the per-block MMSE estimates of blocks 0..nblk-1.  H = C W is linear
 // in W, so the mean is taken on W and the apply kernel runs once.
@@ -609,6 +683,22 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
         hipLaunchKernelGGL(mmse_solve_avg_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
     else
         hipLaunchKernelGGL(mmse_solve_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    const dim3 g((unsigned)a.n), b(64);
+    hipStream_t s = (hipStream_t)stream;
+    const bool eq = (l.mask & WCE_EQUALIZE) && l.eq;
+    if (a.cu) {
+        if (eq) hipLaunchKernelGGL((mmse_solve_ls_kernel<true, true>), g, b, 0, s, st, a, l);
+        else hipLaunchKernelGGL((mmse_solve_ls_kernel<true, false>), g, b, 0, s, st, a, l);
+    } else {
+        if (eq) hipLaunchKernelGGL((mmse_solve_ls_kernel<false, true>), g, b, 0, s, st, a, l);
+        else hipLaunchKernelGGL((mmse_solve_ls_kernel<false, false>), g, b, 0, s, st, a, l);
+    }
     return hip_status(hipGetLastError());
 }
 

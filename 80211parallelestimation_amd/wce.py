@@ -88,6 +88,7 @@ ABI = {
     "wce_ctx_create_empty": [POINTER(c_void_p), c_int],
     "wce_ctx_destroy": [c_void_p],
     "wce_ctx_reserve": [c_void_p, c_int64],
+    "wce_debug_set_fusion": [c_void_p, c_int],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
@@ -140,6 +141,8 @@ def load(path: str = LIB_PATH):
         raise WceError(-5, f"libwce.so not built at {path}; run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
     for name, args in ABI.items():
+        if name.startswith("wce_debug_") and not hasattr(lib, name):
+            continue   # debug hooks are optional (older builds in A/B harnesses)
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = None if name in _VOID else (ctypes.c_char_p if name in _STR else c_int)
@@ -229,6 +232,10 @@ class Context:
             raise ValueError("tx_pre / rx_pre must hold 53 subcarriers")
         _check(lib.wce_ctx_create(byref(self.handle), device, tp.ctypes.data_as(c_void_p),
                                   rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_ctx_create")
+
+    def set_fusion(self, on: bool):
+        """A/B switch: LS family + equalization fused into the MMSE solve (default on)."""
+        _check(_lib.wce_debug_set_fusion(self.handle, int(bool(on))), "wce_debug_set_fusion")
 
     def reserve(self, n_frames):
         """Pre-size the WCE_MMSE_FRAME_COV workspace (no allocation inside estimate)."""

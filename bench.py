@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--frames-per-gpu", type=int, default=65536)
     ap.add_argument("--mode", choices=["textbook", "ref"], default="textbook")
     ap.add_argument("--ls-frames", type=int, default=1 << 20, help="config-2 LS batch (past the 256 MiB MALL)")
+    ap.add_argument("--c5-frames", type=int, default=131072, help="config-5 frames per GPU (1,048,576 / 8)")
     ap.add_argument("--no-extras", action="store_true", help="headline only (for profiling runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
@@ -243,6 +244,7 @@ def main():
             res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
             res["front_end"] = bench_front(wce, ctx, stream, B, reps)
             res["frame_cov"] = bench_frame_cov(wce, make_ctx, stream, B, reps)
+            res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
         res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
@@ -315,6 +317,29 @@ def bench_front(wce, ctx, stream, n, reps):
                       "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_unit": per, "achieved_GBs": gbs,
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
     return out
+
+
+def bench_config5(wce, ctx, stream, n, reps):
+    """BASELINE configs[4] per GPU: all 5 estimators + per-symbol equalization,
+    per-frame preamble, 1,048,576 / 8 frames on this GPU.  Algorithmic bytes
+    per frame (fp64): rx 15x53 + tx block 0 + rx_pre in, 5 H + eq out."""
+    s = stream.handle
+    tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+    hlt, _, _, _ = ctx.shared()
+    ctx.synth(tx, rx, pre, n, seed=0x80211, stream=s)
+    outs = [wce.DeviceArray((n, N)) for _ in range(5)]
+    eq = wce.DeviceArray((n, NBLK, N))
+    o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, 0)
+    fr = ctx.frames(tx, rx, n, rx_pre=pre)
+    f = lambda: ctx.estimate(fr, o, wce.ALL, s)
+    for _ in range(3):
+        f()
+    t = time_events(wce, stream, f, reps)
+    bytes_frame = (NBLK * N + N + N) * 16 + (5 * N + NBLK * N) * 16
+    return {"workload": "BASELINE configs[4] share of one GPU: LT_LS + PS_Linear/Cubic/Sinc + PS_MMSE + "
+                        "equalization, per-frame preamble, fp64", "frames": n, "ms_per_step": t,
+            "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_frame": bytes_frame,
+            "achieved_GBs": bytes_frame * n / (t * 1e-3) / 1e9}
 
 
 def bench_frame_cov(wce, make_ctx, stream, n, reps):

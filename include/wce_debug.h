@@ -11,6 +11,10 @@ int wce_debug_reference_invF(long double *out);
 /* the State wce_ctx_create builds: C (53*53 {re,im}), H_LT (53), sinc table (4*53), {a, b}, X mask */
 int wce_debug_build_state(const double *tx_pre, const double *rx_pre, double ow2, int mode, double *C,
                           double *h_lt, double *sinc, double *ab, unsigned long long *xmask);
+/* A/B switch for the config-5 fusion (LS family + equalization in the MMSE
+ * solve's epilogue); on by default.  ctx is a wce_ctx* (include/wce.h). */
+struct wce_ctx;
+int wce_debug_set_fusion(struct wce_ctx *ctx, int on);
 #ifdef __cplusplus
 }
 #endif

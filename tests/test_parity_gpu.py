@@ -270,3 +270,27 @@ def test_state_blob_roundtrip(gpu_wce, golden):
     b = c2.estimate_host(tx, rx, mask=gpu_wce.ALL)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("mode", ["ref", "textbook"])
+@pytest.mark.parametrize("frame_cov", [False, True])
+def test_config5_fusion_matches_separate_passes(gpu_wce, golden, mode, frame_cov):
+    """LS family + equalization fused into the MMSE solve's epilogue (config 5)
+    reproduces the separate LS pass and MMSE launches."""
+    inp = golden["inputs"]
+    m = gpu_wce.MMSE_REF if mode == "ref" else gpu_wce.MMSE_TEXTBOOK
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m)
+    B = 1500
+    tx, rx, pre = _synth(ctx, gpu_wce, B, seed=77, rx_pre=True)
+    txh, rxh, preh = tx.numpy(), rx.numpy(), pre.numpy()
+    mask = gpu_wce.ALL | (gpu_wce.FRAME_COV if frame_cov else 0)
+    res = []
+    for fuse in (True, False):
+        ctx.set_fusion(fuse)
+        res.append(ctx.estimate_host(txh, rxh, rx_pre=preh, mask=mask))
+    ctx.set_fusion(True)
+    for name in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc", "ps_mmse"):
+        assert normrel(res[0][name], res[1][name]).max() < 1e-14, name
+    eq0, eq1 = res[0]["eq"].reshape(B, -1), res[1]["eq"].reshape(B, -1)
+    assert normrel(eq0, eq1).max() < 1e-14
+    assert np.all(res[0]["eq"][:, :, 26] == 0)
