@@ -224,6 +224,7 @@ static wce::LsArgs ls_args(const wce_frames *in, const wce_outputs *out, uint32_
     a.eq = reinterpret_cast<double *>(out->eq);
     a.os = out->out_stride; a.eqfs = out->eq_frame_stride; a.eqbs = out->eq_block_stride;
     a.eq_src = eq_src;
+    a.f32 = (out->flags & WCE_OUT_LS_F32) != 0;
     if (a.mask & WCE_EQUALIZE) a.mask |= eq_src;   // the blend needs that PS estimate
     return a;
 }
@@ -352,6 +353,7 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     if ((mask & WCE_EST_PS_CUBIC) && !out->ps_cubic) return fail(WCE_EINVAL, "ps_cubic output missing");
     if ((mask & WCE_EST_PS_SINC) && !out->ps_sinc) return fail(WCE_EINVAL, "ps_sinc output missing");
     if ((mask & WCE_EST_PS_MMSE) && !out->ps_mmse) return fail(WCE_EINVAL, "ps_mmse output missing");
+    if (out->flags & ~WCE_OUT_LS_F32) return fail(WCE_EINVAL, "unknown output flags");
     uint32_t eq_src = out->eq_source ? out->eq_source : WCE_EST_PS_LINEAR;
     if (eq) {
         if (!out->eq) return fail(WCE_EINVAL, "eq output missing");
@@ -378,7 +380,8 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     wce::SolveArgs sa = solve_args(in, out->ps_mmse, out->out_stride);
     const bool fc = (mask & WCE_MMSE_FRAME_COV) != 0;
     if (fc) {
-        rc = prep_frame_cov(c, in, out, !fuse && (mask & WCE_EST_LT_LS), sa, stream);
+        const bool lt_ready = !fuse && (mask & WCE_EST_LT_LS) && !(out->flags & WCE_OUT_LS_F32);
+        rc = prep_frame_cov(c, in, out, lt_ready, sa, stream);
         if (rc) return rc;
     }
     rc = fuse ? wce::launch_mmse_solve_ls(c->d_state, sa, la, stream) : wce::launch_mmse_solve(c->d_state, sa, stream);

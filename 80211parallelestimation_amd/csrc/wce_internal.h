@@ -65,7 +65,7 @@ struct LsArgs {
     int32_t blk;
     uint32_t mask;
     int32_t matlab;
-    int32_t pad0;
+    int32_t f32;              // WCE_OUT_LS_F32: outputs are complex float
     double *lt, *lin, *cub, *snc, *eq;
     int64_t os, eqfs, eqbs;
     uint32_t eq_src;

@@ -87,15 +87,30 @@ __device__ __forceinline__ void ps_lane(const LsLane &c, uint32_t mask, double2 
 
 // store the requested LS-family outputs of frame f, subcarrier k, and run
 // WiFi_Equalization.m:1-9 over the frame's 15 blocks
+typedef float v2f __attribute__((ext_vector_type(2)));
+// one output element: complex double, or complex float (WCE_OUT_LS_F32)
+__device__ __forceinline__ void st_out(double *p, int64_t idx, double2 v, bool f32)
+{
+    if (f32) {
+        v2f t = {(float)v.x, (float)v.y};
+        __builtin_nontemporal_store(t, reinterpret_cast<v2f *>(p) + idx);
+    } else {
+        st2_nt(p, idx, v);
+    }
+}
+
+// store the requested LS-family outputs of frame f, subcarrier k, and run
+// WiFi_Equalization.m:1-9 over the frame's 15 blocks
 template <bool EQ>
 __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
                                          double2 hcub, double2 hsnc)
 {
     const int64_t o = f * a.os + k;
-    if ((mask & WCE_EST_LT_LS) && a.lt) st2_nt(a.lt, o, hlt);
-    if ((mask & WCE_EST_PS_LINEAR) && a.lin) st2_nt(a.lin, o, hlin);
-    if ((mask & WCE_EST_PS_CUBIC) && a.cub) st2_nt(a.cub, o, hcub);
-    if ((mask & WCE_EST_PS_SINC) && a.snc) st2_nt(a.snc, o, hsnc);
+    const bool f32 = a.f32 != 0;
+    if ((mask & WCE_EST_LT_LS) && a.lt) st_out(a.lt, o, hlt, f32);
+    if ((mask & WCE_EST_PS_LINEAR) && a.lin) st_out(a.lin, o, hlin, f32);
+    if ((mask & WCE_EST_PS_CUBIC) && a.cub) st_out(a.cub, o, hcub, f32);
+    if ((mask & WCE_EST_PS_SINC) && a.snc) st_out(a.snc, o, hsnc, f32);
     if constexpr (EQ) {
         const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
         const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
@@ -107,7 +122,7 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
             const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
             const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
             const double2 e = k == WCE_DC ? make_double2(0, 0) : cdiv(rv[b], hu);
-            st2_nt(a.eq, eb + b * a.eqbs, e);
+            st_out(a.eq, eb + b * a.eqbs, e, f32);
         }
     }
 }

@@ -32,6 +32,7 @@ PS_MMSE = 1 << 4
 EQUALIZE = 1 << 5
 LS_ALL = 0xF
 ALL = 0x3F
+OUT_LS_F32 = 1         # wce_outputs.flags: LS family + eq stored as complex float
 FRAME_COV = 1 << 6   # WCE_MMSE_FRAME_COV: PS_MMSE covariance from each frame's own preamble
 
 MMSE_REF = 0
@@ -77,7 +78,7 @@ class Outputs(ctypes.Structure):
     _fields_ = [("lt_ls", c_void_p), ("ps_linear", c_void_p), ("ps_cubic", c_void_p), ("ps_sinc", c_void_p),
                 ("ps_mmse", c_void_p), ("eq", c_void_p), ("out_stride", c_int64),
                 ("eq_frame_stride", c_int64), ("eq_block_stride", c_int64), ("eq_source", c_uint32),
-                ("reserved", c_uint32)]
+                ("flags", c_uint32)]
 
 
 _lib = None
@@ -331,7 +332,7 @@ class Context:
         return sym, pre, ow2
 
     def estimate_host(self, tx, rx, rx_pre=None, mask=ALL, block=0, eq_source=PS_LINEAR, semantics=SEM_C,
-                      tx_pre=None):
+                      tx_pre=None, ls_f32=False):
         """Convenience: host numpy frames [B][15][53] -> dict of host outputs."""
         tx, rx = _as_c128(tx), _as_c128(rx)
         B = tx.shape[0]
@@ -341,10 +342,13 @@ class Context:
         dpre = DeviceArray.from_numpy(_as_c128(rx_pre)) if rx_pre is not None else None
         names = [("lt_ls", LT_LS), ("ps_linear", PS_LINEAR), ("ps_cubic", PS_CUBIC), ("ps_sinc", PS_SINC),
                  ("ps_mmse", PS_MMSE)]
-        outs = {n: DeviceArray((B, NSC), zero=True) for n, bit in names if mask & bit}
-        deq = DeviceArray((B, NBLK, NSC), zero=True) if mask & EQUALIZE else None
+        lsdt = np.complex64 if ls_f32 else np.complex128
+        outs = {n: DeviceArray((B, NSC), np.complex128 if n == "ps_mmse" else lsdt, zero=True)
+                for n, bit in names if mask & bit}
+        deq = DeviceArray((B, NBLK, NSC), lsdt, zero=True) if mask & EQUALIZE else None
         o = Outputs(*[(outs[n].addr if n in outs else None) for n, _ in names],
-                    deq.addr if deq is not None else None, NSC, NBLK * NSC, NSC, eq_source, 0)
+                    deq.addr if deq is not None else None, NSC, NBLK * NSC, NSC, eq_source,
+                    OUT_LS_F32 if ls_f32 else 0)
         dtp = DeviceArray.from_numpy(_as_c128(tx_pre)) if tx_pre is not None else None
         fr = self.frames(dtx, drx, B, rx_pre=dpre, block=block, semantics=semantics, tx_pre=dtp)
         self.estimate(fr, o, mask)

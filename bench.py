@@ -322,24 +322,31 @@ def bench_front(wce, ctx, stream, n, reps):
 def bench_config5(wce, ctx, stream, n, reps):
     """BASELINE configs[4] per GPU: all 5 estimators + per-symbol equalization,
     per-frame preamble, 1,048,576 / 8 frames on this GPU.  Algorithmic bytes
-    per frame (fp64): rx 15x53 + tx block 0 + rx_pre in, 5 H + eq out."""
+    per frame: rx 15x53 + tx block 0 + rx_pre in, 5 H + eq out.  Reported in
+    fp64 and in the config's mixed precision (fp64 solve, LS family + eq
+    stored fp32: WCE_OUT_LS_F32)."""
     s = stream.handle
     tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
-    hlt, _, _, _ = ctx.shared()
     ctx.synth(tx, rx, pre, n, seed=0x80211, stream=s)
-    outs = [wce.DeviceArray((n, N)) for _ in range(5)]
-    eq = wce.DeviceArray((n, NBLK, N))
-    o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, 0)
     fr = ctx.frames(tx, rx, n, rx_pre=pre)
-    f = lambda: ctx.estimate(fr, o, wce.ALL, s)
-    for _ in range(3):
-        f()
-    t = time_events(wce, stream, f, reps)
-    bytes_frame = (NBLK * N + N + N) * 16 + (5 * N + NBLK * N) * 16
-    return {"workload": "BASELINE configs[4] share of one GPU: LT_LS + PS_Linear/Cubic/Sinc + PS_MMSE + "
-                        "equalization, per-frame preamble, fp64", "frames": n, "ms_per_step": t,
-            "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_frame": bytes_frame,
-            "achieved_GBs": bytes_frame * n / (t * 1e-3) / 1e9}
+    res = {"workload": "BASELINE configs[4] share of one GPU: LT_LS + PS_Linear/Cubic/Sinc + PS_MMSE + "
+                       "equalization, per-frame preamble, fused (LS family in the MMSE solve epilogue)",
+           "frames": n}
+    for label, f32 in (("fp64", False), ("mixed_fp64_solve_fp32_ls", True)):
+        dt = np.complex64 if f32 else np.complex128
+        outs = [wce.DeviceArray((n, N), dt) for _ in range(4)] + [wce.DeviceArray((n, N))]
+        eq = wce.DeviceArray((n, NBLK, N), dt)
+        o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32 if f32 else 0)
+        f = lambda: ctx.estimate(fr, o, wce.ALL, s)
+        for _ in range(3):
+            f()
+        t = time_events(wce, stream, f, reps)
+        ob = 8 if f32 else 16
+        bytes_frame = (NBLK * N + N + N) * 16 + N * 16 + (4 * N + NBLK * N) * ob
+        res[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_frame": bytes_frame,
+                      "achieved_GBs": bytes_frame * n / (t * 1e-3) / 1e9}
+        del outs, eq
+    return res
 
 
 def bench_frame_cov(wce, make_ctx, stream, n, reps):

@@ -138,8 +138,15 @@ typedef struct {
     int64_t eq_block_stride;
     uint32_t eq_source;         /* PS estimate blended with H_LT (WiFi_RX.m:60 uses PS_Linear);
                                    0 = WCE_EST_PS_LINEAR */
-    uint32_t reserved;
+    uint32_t flags;             /* WCE_OUT_* */
 } wce_outputs;
+
+/* wce_outputs.flags.  WCE_OUT_LS_F32: the LS family (lt_ls, ps_linear,
+ * ps_cubic, ps_sinc) and eq are stored as complex float ({re, im} float, 8 B),
+ * computed in fp64 and rounded once (BASELINE configs[4] "mixed fp64 solve /
+ * fp32 interp"; <= 1e-7 relative).  ps_mmse stays complex double.  Strides
+ * count elements of each buffer's own type. */
+#define WCE_OUT_LS_F32 (1u << 0)
 
 /* Pre-size the context's device workspace for WCE_MMSE_FRAME_COV batches of up
  * to n_frames (3 KB per frame), so that wce_estimate never allocates.  Without

@@ -294,3 +294,25 @@ def test_config5_fusion_matches_separate_passes(gpu_wce, golden, mode, frame_cov
     eq0, eq1 = res[0]["eq"].reshape(B, -1), res[1]["eq"].reshape(B, -1)
     assert normrel(eq0, eq1).max() < 1e-14
     assert np.all(res[0]["eq"][:, :, 26] == 0)
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+def test_ls_outputs_f32(gpu_wce, golden, fuse):
+    """WCE_OUT_LS_F32 (BASELINE configs[4] mixed precision): LS family and eq
+    stored as complex float, within 1e-7 of the fp64 outputs (G4 gate 1e-6);
+    PS_MMSE unchanged in fp64."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    ctx.set_fusion(fuse)
+    B = 700
+    tx, rx, pre = _synth(ctx, gpu_wce, B, seed=5, rx_pre=True)
+    txh, rxh, preh = tx.numpy(), rx.numpy(), pre.numpy()
+    ref = ctx.estimate_host(txh, rxh, rx_pre=preh, mask=gpu_wce.ALL)
+    got = ctx.estimate_host(txh, rxh, rx_pre=preh, mask=gpu_wce.ALL, ls_f32=True)
+    for name in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc"):
+        assert got[name].dtype == np.complex64
+        assert normrel(got[name].astype(np.complex128), ref[name]).max() < 1e-7, name
+    assert got["ps_mmse"].dtype == np.complex128
+    assert normrel(got["ps_mmse"], ref["ps_mmse"]).max() < 1e-14
+    e32 = got["eq"].reshape(B, -1).astype(np.complex128)
+    assert normrel(e32, ref["eq"].reshape(B, -1)).max() < 1e-7
