@@ -7,11 +7,14 @@ export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc
 mkdir -p "$OUT"
+# PMC_EXTRAS=1: profile every bench leg (LS, front end, config 5, ...), not just the headline
+EXTRAS=--no-extras
+[ -n "$PMC_EXTRAS" ] && EXTRAS=
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 run() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$name" -o run --pmc "$@" \
-     -- python3 "$ROOT/bench.py" --no-extras --no-cpu-baseline --steps 5 --warmup 1 ${BENCH_ARGS} \
+     -- python3 "$ROOT/bench.py" $EXTRAS --steps 5 --no-cpu-baseline --warmup 1 ${BENCH_ARGS} \
      > "$OUT/$name.log" 2>&1
 }
 run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU &&
