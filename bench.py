@@ -253,7 +253,9 @@ def main():
         if dist.rank == 0:
             res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
             res["front_end"] = bench_front(wce, ctx, stream, B, reps)
-            res["frame_cov"] = bench_frame_cov(wce, make_ctx, stream, B, reps)
+            # rank 0 only: contexts built locally (make_ctx would broadcast: a collective)
+            local_ctx = lambda m: wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m, device=dev)
+            res["frame_cov"] = bench_frame_cov(wce, local_ctx, stream, B, reps)
             res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
