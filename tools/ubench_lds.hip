@@ -20,6 +20,16 @@ __global__ __launch_bounds__(64, 3) void kern(double *out, int iters)
                 if (q == (it & 7)) buf[it & 1][p + 8 * r] = v;
             } else if constexpr (MODE == 1) {   // full write: 64 lanes
                 buf[it & 1][(lane + r) & 63] = v;
+            } else if constexpr (MODE == 4) {   // masked write, 8 lanes, two b64 halves
+                if (q == (it & 7)) {
+                    double *d = reinterpret_cast<double *>(&buf[it & 1][p + 8 * r]);
+                    d[0] = v.x;
+                    d[1] = v.y;
+                }
+            } else if constexpr (MODE == 5) {   // masked write, 8 lanes, b64 (re only)
+                if (q == (it & 7)) reinterpret_cast<double *>(&buf[it & 1][p + 8 * r])[0] = v.x;
+            } else if constexpr (MODE == 6) {   // masked write, 8 lanes, b32
+                if (q == (it & 7)) reinterpret_cast<float *>(&buf[it & 1][p + 8 * r])[0] = (float)v.x;
             } else if constexpr (MODE == 2) {   // broadcast read, 8 distinct addresses
                 double2 t = buf[it & 1][p + 8 * r];
                 acc.x += t.x; acc.y += t.y;
@@ -44,9 +54,10 @@ int main()
     double *d;
     (void)hipMalloc(&d, blocks * sizeof(double));
     double *h = new double[blocks];
-    const char *names[4] = {"ds_write_b128 8 lanes", "ds_write_b128 64 lanes", "ds_read_b128 bcast(8 addr)",
-                            "ds_read_b128 64 addr"};
-    for (int m = 0; m < 4; m++) {
+    const char *names[7] = {"ds_write_b128 8 lanes", "ds_write_b128 64 lanes", "ds_read_b128 bcast(8 addr)",
+                            "ds_read_b128 64 addr", "2x ds_write_b64 8 lanes", "ds_write_b64 8 lanes",
+                            "ds_write_b32 8 lanes"};
+    for (int m = 0; m < 7; m++) {
         hipEvent_t a, b;
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
@@ -56,6 +67,9 @@ int main()
             if (m == 1) hipLaunchKernelGGL(kern<1>, dim3(blocks), dim3(64), 0, 0, d, iters);
             if (m == 2) hipLaunchKernelGGL(kern<2>, dim3(blocks), dim3(64), 0, 0, d, iters);
             if (m == 3) hipLaunchKernelGGL(kern<3>, dim3(blocks), dim3(64), 0, 0, d, iters);
+            if (m == 4) hipLaunchKernelGGL(kern<4>, dim3(blocks), dim3(64), 0, 0, d, iters);
+            if (m == 5) hipLaunchKernelGGL(kern<5>, dim3(blocks), dim3(64), 0, 0, d, iters);
+            if (m == 6) hipLaunchKernelGGL(kern<6>, dim3(blocks), dim3(64), 0, 0, d, iters);
             (void)hipEventRecord(b);
             (void)hipEventSynchronize(b);
         }
