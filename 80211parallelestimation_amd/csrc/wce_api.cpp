@@ -193,6 +193,7 @@ static int check_frames(const wce_frames *in, bool need_blocks)
     if (!in) return fail(WCE_EINVAL, "null frames");
     if (in->n_frames < 0) return fail(WCE_EINVAL, "n_frames < 0");
     if (in->n_frames == 0) return WCE_OK;
+    if (in->n_frames > INT32_MAX) return fail(WCE_EINVAL, "n_frames > 2^31 - 1 (one wave per frame in a 1-D grid)");
     if (!in->tx || !in->rx) return fail(WCE_EINVAL, "tx/rx required");
     if (in->block < 0 || in->block >= wce::NBLK) return fail(WCE_EINVAL, "block out of range");
     if (in->semantics != WCE_SEM_C && in->semantics != WCE_SEM_MATLAB) return fail(WCE_EINVAL, "bad semantics");

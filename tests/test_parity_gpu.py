@@ -213,10 +213,35 @@ def test_argument_errors(gpu_wce, golden):
         ctx.estimate(ctx.frames(d, d, 4), good, 1 << 9)
     with pytest.raises(gpu_wce.WceError):
         gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], -1.0)
+    with pytest.raises(gpu_wce.WceError):                            # beyond the 1-D grid of frames
+        ctx.estimate(ctx.frames(d, d, 1 << 31), good, gpu_wce.LT_LS)
+    with pytest.raises(gpu_wce.WceError):                            # unknown output flag
+        bad = gpu_wce.Outputs(h.addr, None, None, None, None, None, N, 0, 0, 0, 1 << 5)
+        ctx.estimate(ctx.frames(d, d, 4), bad, gpu_wce.LT_LS)
     empty = gpu_wce.Context(empty=True)
     with pytest.raises(gpu_wce.WceError) as e:
         empty.estimate(empty.frames(d, d, 4), good, gpu_wce.LT_LS)
     assert e.value.code == -4
+
+
+def test_nonfinite_inputs_stay_local(gpu_wce, golden, oracle):
+    """A null pilot (tx = 0, an erased symbol) makes that frame's PS estimates
+    non-finite -- the reference divides by it too (main.c:82-84) -- without
+    touching its neighbours; LT_LS of the frame is unaffected."""
+    r = golden["ref"]
+    ctx = gpu_wce.Context(r["pre_tx"][0], r["pre_rx"][0], r["ow2"], gpu_wce.MMSE_REF)
+    tx, rx = frames_from_block0(r["frames_tx"], r["frames_rx"])
+    tx[3, 0, PILOTS[1]] = 0.0
+    for fuse in (True, False):
+        ctx.set_fusion(fuse)
+        out = ctx.estimate_host(tx, rx, mask=gpu_wce.ALL)
+        assert not np.all(np.isfinite(out["ps_linear"][3]))
+        assert not np.all(np.isfinite(out["ps_sinc"][3]))
+        assert np.all(np.isfinite(out["lt_ls"][3]))
+        for f in (2, 4):
+            assert normrel(out["ps_linear"][f], oracle.ps_linear(tx[f, 0], rx[f, 0])) < TOL_LS
+            assert normrel(out["ps_mmse"][f], from_split(r["ps_mmse_ref"][0][f])) < TOL
+    ctx.set_fusion(True)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
