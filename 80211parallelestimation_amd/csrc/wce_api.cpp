@@ -122,6 +122,26 @@ int wce_ctx_create(wce_ctx **out, int device, const wce_complex *tx_pre, const w
     return WCE_OK;
 }
 
+int wce_ctx_create_cov(wce_ctx **out, int device, const wce_complex *tx_pre, const wce_complex *rx_pre,
+                       const wce_complex *Rhh, double ow2)
+{
+    if (!out || !tx_pre || !rx_pre || !Rhh) return fail(WCE_EINVAL, "null argument");
+    if (!(ow2 > 0)) return fail(WCE_EINVAL, "ow2 must be > 0");
+    State *h = new (std::nothrow) State;
+    if (!h) return fail(WCE_ENOMEM, "alloc");
+    int rc = wce_state_build_cov(h, sizeof(State), tx_pre, rx_pre, Rhh, ow2);
+    if (rc) { delete h; return fail(rc, "covariance state build"); }
+    wce_ctx *c = nullptr;
+    rc = wce_ctx_create_empty(&c, device);
+    if (rc) { delete h; return rc; }
+    rc = wce_ctx_load_state(c, h, sizeof(State));
+    if (!rc) { c->host = *h; c->has_host = true; }
+    delete h;
+    if (rc) { wce_ctx_destroy(c); return rc; }
+    *out = c;
+    return WCE_OK;
+}
+
 int wce_ctx_destroy(wce_ctx *c)
 {
     if (!c) return WCE_OK;

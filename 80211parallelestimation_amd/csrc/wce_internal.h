@@ -55,6 +55,7 @@ const ldc *host_reference_F();
 // main.c:66-75 in long double.
 void host_lt_ls(const ldc *tx_pre, const ldc *rx_pre, ldc *H);
 // Fill a host State from F / invF / H_LS (long double) for `mode`.
+int host_apply_cov(State *st, const ldc *F, const wce_complex *Rhh);
 int host_build_state(State *st, const ldc *F, const ldc *invF, const ldc *H_LS,
                      const ldc *tx_pre, double ow2, int mode);
 

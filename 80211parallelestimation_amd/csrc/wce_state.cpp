@@ -292,6 +292,43 @@ extern "C" int wce_debug_build_state(const double *tx_pre, const double *rx_pre,
 
 extern "C" size_t wce_state_size(void) { return sizeof(wce::State); }
 
+namespace wce {
+// WCE_MMSE_COV: the TEXTBOOK state with C = F Rhh F' from a caller's Rhh (80-bit products)
+int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
+{
+    const int n = NSC;
+    std::vector<cld> F(n * n), R(n * n), t1(n * n), C(n * n), FH(n * n);
+    for (int i = 0; i < n * n; i++) {
+        F[i] = from(Fl[i]);
+        R[i] = mk((long double)Rhh[i].re, (long double)Rhh[i].im);
+    }
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < n; c++) {
+            cld v = F[c * n + r];
+            __imag__ v = -__imag__ v;
+            FH[r * n + c] = v;   // F' (conjugate transpose)
+        }
+    mat_mul(R.data(), n, n, FH.data(), n, t1.data());
+    mat_mul(F.data(), n, n, t1.data(), n, C.data());
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            st->C[2 * (i * CLD + j)] = (double)__real__ C[i * n + j];
+            st->C[2 * (i * CLD + j) + 1] = (double)__imag__ C[i * n + j];
+        }
+    st->mode = WCE_MMSE_COV;
+    return WCE_OK;
+}
+}  // namespace wce
+
+extern "C" int wce_state_build_cov(void *out, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
+                                   const wce_complex *Rhh, double ow2)
+{
+    if (!Rhh) return WCE_EINVAL;
+    int rc = wce_state_build(out, bytes, tx_pre, rx_pre, ow2, WCE_MMSE_TEXTBOOK);
+    if (rc) return rc;
+    return wce::host_apply_cov(static_cast<wce::State *>(out), wce::host_reference_F(), Rhh);
+}
+
 extern "C" int wce_state_build(void *out, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
                                double ow2, int mode)
 {

@@ -37,6 +37,7 @@ FRAME_COV = 1 << 6   # WCE_MMSE_FRAME_COV: PS_MMSE covariance from each frame's 
 
 MMSE_REF = 0
 MMSE_TEXTBOOK = 1
+MMSE_COV = 2       # TEXTBOOK with a caller-supplied channel covariance Rhh
 FFT_SIZE = 64            # front end: 64-point DFT per OFDM block (WiFi_RX.m:10)
 SAMPLES_PER_BLOCK = 80   # 64 + 16-sample cyclic prefix (WiFi_RX.m:12)
 SEM_C = 0          # main.c semantics
@@ -89,6 +90,8 @@ ABI = {
     "wce_ctx_create_empty": [POINTER(c_void_p), c_int],
     "wce_ctx_destroy": [c_void_p],
     "wce_ctx_reserve": [c_void_p, c_int64],
+    "wce_ctx_create_cov": [POINTER(c_void_p), c_int, c_void_p, c_void_p, c_void_p, c_double],
+    "wce_state_build_cov": [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_double],
     "wce_debug_set_fusion": [c_void_p, c_int],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
@@ -220,17 +223,25 @@ def _addr(x):
 class Context:
     """wce_ctx: shared (frame-independent) state resident on one device."""
 
-    def __init__(self, tx_pre=None, rx_pre=None, ow2=None, mode=MMSE_REF, device=0, empty=False):
+    def __init__(self, tx_pre=None, rx_pre=None, ow2=None, mode=MMSE_REF, device=0, empty=False, Rhh=None):
         lib = load()
         self.handle = c_void_p()
         self.device = device
-        self.mode = mode
+        self.mode = MMSE_COV if Rhh is not None else mode
         if empty:
             _check(lib.wce_ctx_create_empty(byref(self.handle), device), "wce_ctx_create_empty")
             return
         tp, rp = _as_c128(tx_pre), _as_c128(rx_pre)
         if tp.shape != (NSC,) or rp.shape != (NSC,):
             raise ValueError("tx_pre / rx_pre must hold 53 subcarriers")
+        if Rhh is not None:   # WCE_MMSE_COV: model channel covariance (53 x 53, time domain)
+            R = _as_c128(Rhh)
+            if R.shape != (NSC, NSC):
+                raise ValueError("Rhh must be 53 x 53")
+            _check(lib.wce_ctx_create_cov(byref(self.handle), device, tp.ctypes.data_as(c_void_p),
+                                          rp.ctypes.data_as(c_void_p), R.ctypes.data_as(c_void_p), float(ow2)),
+                   "wce_ctx_create_cov")
+            return
         _check(lib.wce_ctx_create(byref(self.handle), device, tp.ctypes.data_as(c_void_p),
                                   rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_ctx_create")
 
@@ -359,12 +370,18 @@ class Context:
         return res
 
 
-def state_blob(tx_pre, rx_pre, ow2, mode=MMSE_REF) -> np.ndarray:
+def state_blob(tx_pre, rx_pre, ow2, mode=MMSE_REF, Rhh=None) -> np.ndarray:
     """The shared state built on the host (no device): bytes to broadcast."""
     lib = load()
     n = lib.wce_state_size()
     blob = np.zeros(n, np.uint8)
     tp, rp = _as_c128(tx_pre), _as_c128(rx_pre)
+    if Rhh is not None:
+        R = _as_c128(Rhh)
+        _check(lib.wce_state_build_cov(blob.ctypes.data_as(c_void_p), n, tp.ctypes.data_as(c_void_p),
+                                       rp.ctypes.data_as(c_void_p), R.ctypes.data_as(c_void_p), float(ow2)),
+               "wce_state_build_cov")
+        return blob
     _check(lib.wce_state_build(blob.ctypes.data_as(c_void_p), n, tp.ctypes.data_as(c_void_p),
                                rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_state_build")
     return blob

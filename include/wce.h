@@ -69,7 +69,12 @@ enum {
  *  TEXTBOOK : WiFi_channel_estimation_PS_MMSE.m per block:
  *             H = C X (X C X' + ow2 I)^-1 rx, C = F Rhh F', X = diag(tx).
  * Both run the same kernel: H = C X (a X C X' + b I)^-1 rx. */
-enum { WCE_MMSE_REF = 0, WCE_MMSE_TEXTBOOK = 1 };
+enum { WCE_MMSE_REF = 0, WCE_MMSE_TEXTBOOK = 1, WCE_MMSE_COV = 2 };
+/*  COV      : TEXTBOOK with a caller-supplied channel covariance Rhh instead
+ *             of the single-preamble estimate ifft(H_LT) ifft(H_LT)' (e.g. a
+ *             power-delay-profile model or an average over many preambles):
+ *             C = F Rhh F', generally full rank -- the dense per-frame solve
+ *             is then the only way to apply it.  See wce_state_build_cov. */
 
 typedef struct wce_ctx wce_ctx;
 
@@ -86,6 +91,12 @@ int wce_ctx_create(wce_ctx **ctx, int device, const wce_complex *tx_pre,
 int wce_ctx_create_empty(wce_ctx **ctx, int device);
 int wce_ctx_destroy(wce_ctx *ctx);
 
+/* WCE_MMSE_COV: Rhh is the 53 x 53 time-domain channel covariance (row-major,
+ * Hermitian positive semidefinite, host); tx_pre/rx_pre still give H_LT for
+ * LT_LS and equalization. */
+int wce_ctx_create_cov(wce_ctx **ctx, int device, const wce_complex *tx_pre, const wce_complex *rx_pre,
+                       const wce_complex *Rhh, double ow2);
+
 /* Device pointer and size of the packed shared state (C, H_LT, tx_pre, sinc
  * table, MMSE coefficients): the single buffer a multi-GPU run broadcasts
  * from rank 0.  After writing it externally call wce_ctx_mark_ready. */
@@ -98,6 +109,8 @@ int wce_ctx_mark_ready(wce_ctx *ctx);
 size_t wce_state_size(void);
 int wce_state_build(void *host_state, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
                     double ow2, int mmse_mode);
+int wce_state_build_cov(void *host_state, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
+                        const wce_complex *Rhh, double ow2);
 int wce_ctx_load_state(wce_ctx *ctx, const void *host_state, size_t bytes);
 
 /* Copy back the shared vectors (host outputs, may be NULL): H_LT (53),

@@ -113,3 +113,27 @@ def test_no_device_fails_loudly(wce):
     assert e.value.code in (-5, -2)
     with pytest.raises(wce.WceError):
         wce.WiFi_channel_estimation_PS_Linear(np.ones(N), np.ones(N))
+
+
+def _pdp_cov(L=53, decay=0.12):
+    """Exponential power-delay-profile channel covariance (time domain, full rank)."""
+    p = np.exp(-decay * np.arange(L))
+    return np.diag(p / p.sum()).astype(np.complex128) * 1e-4
+
+
+def test_cov_state_C_is_F_Rhh_FH(wce, golden):
+    """WCE_MMSE_COV: State::C = F Rhh F' (80-bit products), a = 1, b = ow2."""
+    inp = golden["inputs"]
+    R = _pdp_cov()
+    R[3, 7] = R[7, 3] = 2e-6 + 0j       # not diagonal: exercise the full product
+    R[5, 11], R[11, 5] = 1e-6 + 3e-7j, 1e-6 - 3e-7j
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    C = blob[:64 * 64 * 16].view(np.complex128).reshape(64, 64)[:53, :53]
+    t = np.arange(53)
+    F = np.exp(-2j * np.pi * np.outer(t, t).astype(np.longdouble) / 53).astype(np.clongdouble)
+    ref = (F @ R.astype(np.clongdouble) @ F.conj().T).astype(np.complex128)
+    assert np.max(np.abs(C - ref)) / np.max(np.abs(ref)) < 1e-14
+    a, b, ow2 = blob[-48:-24].view(np.float64)
+    mode, magic = blob[-16:-8].view(np.int32)
+    assert (a, b, ow2, mode, magic) == (1.0, inp["ow2"], inp["ow2"], wce.MMSE_COV, 0x80211)
+    assert blob[-24:-16].view(np.uint64)[0] == (1 << 53) - 1    # X = diag(tx) over all 53

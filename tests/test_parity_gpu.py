@@ -341,3 +341,25 @@ def test_ls_outputs_f32(gpu_wce, golden, fuse):
     assert normrel(got["ps_mmse"], ref["ps_mmse"]).max() < 1e-14
     e32 = got["eq"].reshape(B, -1).astype(np.complex128)
     assert normrel(e32, ref["eq"].reshape(B, -1)).max() < 1e-7
+
+
+def test_model_covariance_dense_solve(gpu_wce, golden, oracle):
+    """WCE_MMSE_COV: a full-rank power-delay-profile Rhh (C = F Rhh F'), where
+    the dense 53x53 per-frame solve is irreplaceable; against the long double
+    unified solve with the same C, on frames with their own random channels."""
+    inp = golden["inputs"]
+    p = np.exp(-0.12 * np.arange(N))
+    R = np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    hlt, C, a, b = ctx.shared()
+    assert (a, b) == (1.0, inp["ow2"])
+    B = 800
+    tx, rx, _ = _synth(ctx, gpu_wce, B, seed=31)
+    txh, rxh = tx.numpy(), rx.numpy()
+    out = ctx.estimate_host(txh, rxh, mask=gpu_wce.PS_MMSE | gpu_wce.LT_LS)
+    assert normrel(out["lt_ls"][0], oracle.lt_ls(inp["tx_pre"], inp["rx_pre"])) < 1e-13
+    ones = np.ones(N, np.uint8)
+    rng = np.random.default_rng(8)
+    for f in np.concatenate([[0, B - 1], rng.choice(B, 10, replace=False)]):
+        exp = oracle.mmse_unified(C, ones, a, b, txh[f, 0], rxh[f, 0])
+        assert normrel(out["ps_mmse"][f], exp) < TOL, f
