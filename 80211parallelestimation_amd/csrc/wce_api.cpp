@@ -250,9 +250,14 @@ static wce::LsArgs ls_args(const wce_frames *in, const wce_outputs *out, uint32_
     return a;
 }
 
-static wce::SolveArgs solve_args(const wce_frames *in, wce_complex *W, int64_t w_stride)
+static wce::SolveArgs solve_args(const wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_stride)
 {
     wce::SolveArgs a{};
+    if (c->mode == WCE_MMSE_TEXTBOOK) {   // C = c c': Ryy built from the shared vector
+        a.cu = c->d_state->cvec;
+        a.cw = nullptr;
+        a.cs = 0;
+    }
     a.tx = reinterpret_cast<const double *>(in->tx);
     a.rx = reinterpret_cast<const double *>(in->rx);
     a.fs = in->frame_stride; a.bs = in->block_stride; a.n = in->n_frames;
@@ -272,7 +277,7 @@ int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_s
     if (rc) return rc;
     if (in->n_frames == 0) return WCE_OK;
     if (!W || (in->n_frames > 1 && w_stride < wce::NSC)) return fail(WCE_EINVAL, "bad W");
-    wce::SolveArgs a = solve_args(in, W, w_stride);
+    wce::SolveArgs a = solve_args(c, in, W, w_stride);
     DeviceGuard g(c->device);
     rc = wce::launch_mmse_solve(c->d_state, a, stream);
     return rc ? fail(rc, "mmse_solve launch") : WCE_OK;
@@ -353,6 +358,7 @@ static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
     sa.cu = uw;
     sa.cw = c->mode == WCE_MMSE_REF ? ww : nullptr;
     sa.cs = WS_LD;
+    sa.hout = 1;
     return WCE_OK;
 }
 
@@ -398,7 +404,7 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
         if (rc) return fail(rc, "ls launch");
     }
     if (!mmse) return WCE_OK;
-    wce::SolveArgs sa = solve_args(in, out->ps_mmse, out->out_stride);
+    wce::SolveArgs sa = solve_args(c, in, out->ps_mmse, out->out_stride);
     const bool fc = (mask & WCE_MMSE_FRAME_COV) != 0;
     if (fc) {
         const bool lt_ready = !fuse && (mask & WCE_EST_LT_LS) && !(out->flags & WCE_OUT_LS_F32);

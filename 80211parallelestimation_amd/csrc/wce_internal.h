@@ -28,6 +28,8 @@ struct State {
     double Mg[CLD * CLD * 2];
     double Mu[CLD * CLD * 2];
     double Mw[CLD * CLD * 2];
+    double cvec[NPAD * 2];     // TEXTBOOK: C = c c' with c = F ifft(H_LT): the Ryy build
+                               // a X c c' X' needs one complex product per element
     double h_lt[NPAD * 2];     // LT_LS of the shared preamble (main.c:66-75)
     double tx_pre[NPAD * 2];   // shared tx preamble FFT
     double sinc[4][NPAD];      // sinc((k - P_p)/14) in double (utils.c:727-733)
@@ -79,10 +81,12 @@ struct SolveArgs {
     int32_t nblk;             // blocks averaged per frame (1; 4 in MATLAB semantics)
     double *w;
     int64_t ws;
-    // per-frame covariance (null = shared C): C_f = cu_f cw_f^T, rows of stride cs;
-    // cw == null: cw_f = conj(cu_f).  Output is then H itself (no apply step).
+    // rank-1 covariance (null = dense State::C): C_f = cu_f cw_f^T, rows of
+    // stride cs (0: one shared pair); cw == null: cw_f = conj(cu_f).
     const double *cu, *cw;
     int64_t cs;
+    int32_t hout;             // 1: write H = cu (cw . W) directly (no apply step)
+    int32_t pad1;
 };
 struct SynthArgs {
     double *tx, *rx, *rx_pre;

@@ -331,6 +331,12 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     for (int bb = 0; bb < BLK; ++bb) cmsub_conj(P[bb], zp, A[BLK][bb]);
 }
 
+#ifndef WCE_PREFETCH_C
+#define WCE_PREFETCH_C 0
+#endif
+#ifndef WCE_ABLATE_RYY   // timing-only build: Ryy = b I (no C loads, no build)
+#define WCE_ABLATE_RYY 0
+#endif
 #ifndef WCE_SOLVE_WAVES_PER_SIMD
 #define WCE_SOLVE_WAVES_PER_SIMD 3
 #endif
@@ -344,6 +350,20 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
+    const double ac = st->acoef, bc = st->bcoef;
+    double2 A[RB][RB];
+    const bool cbuild = !FC && ac != 0.0 && !WCE_ABLATE_RYY;
+#if WCE_PREFETCH_C
+    // C's 28 blocks are issued before the frame's own loads: the two memory
+    // round trips (C from L2, tx/rx from HBM) overlap instead of queueing.
+    // Unconditional (no branch around A: a branch-defined A spills).
+    if constexpr (!FC) {
+#pragma unroll
+        for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+            for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
+    }
+#endif
     {
         const bool act = lane < NSC;
         const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
@@ -355,8 +375,6 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
         s.rd[lane] = 0.0;
     }
     wave_lds_sync();
-    const double ac = st->acoef, bc = st->bcoef;
-    double2 A[RB][RB];
     {
         if (FC && ac != 0.0) {   // a X u w^T X': both factors staged in the pivot buffers
             const bool act = lane < NSC;
@@ -371,7 +389,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = cmul(s.u[0][p + 8 * aa], s.u[1][q + 8 * bb]);
             wave_lds_sync();   // publish_col<0> reuses s.u[0]
-        } else if (!FC && ac != 0.0) {   // a X C X'  (C zero-padded: no bounds checks)
+        } else if (WCE_PREFETCH_C ? !FC : cbuild) {   // a X C X'  (C zero-padded: no bounds checks)
             double2 yr[RB], xc[RB];
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa) {
@@ -381,8 +399,13 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
-                for (int bb = 0; bb <= aa; ++bb)
+                for (int bb = 0; bb <= aa; ++bb) {
+#if WCE_PREFETCH_C
+                    A[aa][bb] = cmul(cmul(yr[aa], A[aa][bb]), xc[bb]);
+#else
                     A[aa][bb] = cmul(cmul(yr[aa], ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb)), xc[bb]);
+#endif
+                }
         } else {
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
@@ -439,12 +462,15 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     return cmul(s.x[lane], s.z[lane]);
 }
 
+// R1: Ryy built from the rank-1 factors SolveArgs::cu/cw (TEXTBOOK: State::cvec)
+// instead of the dense State::C (COV mode, or a = 0).
+template <bool R1>
 __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
     const int64_t f = blockIdx.x;
     if (f >= a.n) return;
-    const double2 w = solve_block<false>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
+    const double2 w = solve_block<R1>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
     if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, w);
 }
 
@@ -453,7 +479,7 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kerne
 // resident data (pilots from LDS, rx blocks streamed).  The HBM traffic of the
 // LS path overlaps the VALU-bound solve instead of running as its own pass.
 // C semantics, one block.  FC: per-frame covariance (H written directly).
-template <bool FC, bool EQ>
+template <bool R1, bool HOUT, bool EQ>
 __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_kernel(const State *__restrict__ st,
                                                                                     SolveArgs a, LsArgs l)
 {
@@ -463,8 +489,8 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     const int lane = threadIdx.x;
     const bool act = lane < NSC;
     const int k = act ? lane : 0;
-    const double2 wz = solve_block<FC>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
-    if constexpr (FC) {
+    const double2 wz = solve_block<R1>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
+    if constexpr (HOUT) {
         const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
         const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
         double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
@@ -491,15 +517,15 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
 // MATLAB semantics (WiFi_channel_estimation_PS_MMSE.m): the estimate is the
 // mean of the per-block MMSE estimates of blocks 0..nblk-1.  H = C W is linear
 // in W, so the mean is taken on W and the apply kernel runs once.
-__global__ __launch_bounds__(64, 2) void mmse_solve_avg_kernel(const State *__restrict__ st,
-                                                                                     SolveArgs a)
+template <bool R1>
+__global__ __launch_bounds__(64, 2) void mmse_solve_avg_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
     const int64_t f = blockIdx.x;
     if (f >= a.n) return;
     double2 acc = make_double2(0.0, 0.0);
     for (int b = 0; b < a.nblk; ++b) {
-        acc = cadd(acc, solve_block<false>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f));
+        acc = cadd(acc, solve_block<R1>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f));
         wave_lds_sync();   // the next block overwrites s
     }
     if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, cscale(acc, 1.0 / a.nblk));
@@ -690,30 +716,39 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
     if (a.n > 0x7fffffffll) return WCE_EINVAL;
-    if (a.cu && a.nblk > 1)
-        hipLaunchKernelGGL(mmse_solve_fc_kernel<true>, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
-    else if (a.cu)
-        hipLaunchKernelGGL(mmse_solve_fc_kernel<false>, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
-    else if (a.nblk > 1)
-        hipLaunchKernelGGL(mmse_solve_avg_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
-    else
-        hipLaunchKernelGGL(mmse_solve_kernel, dim3((unsigned)a.n), dim3(64), 0, (hipStream_t)stream, st, a);
+    if (a.hout && !a.cu) return WCE_EINVAL;
+    const dim3 g((unsigned)a.n), b(64);
+    hipStream_t s = (hipStream_t)stream;
+    const bool avg = a.nblk > 1;
+    if (a.hout) {
+        if (avg) hipLaunchKernelGGL(mmse_solve_fc_kernel<true>, g, b, 0, s, st, a);
+        else hipLaunchKernelGGL(mmse_solve_fc_kernel<false>, g, b, 0, s, st, a);
+    } else if (a.cu) {
+        if (avg) hipLaunchKernelGGL(mmse_solve_avg_kernel<true>, g, b, 0, s, st, a);
+        else hipLaunchKernelGGL(mmse_solve_kernel<true>, g, b, 0, s, st, a);
+    } else {
+        if (avg) hipLaunchKernelGGL(mmse_solve_avg_kernel<false>, g, b, 0, s, st, a);
+        else hipLaunchKernelGGL(mmse_solve_kernel<false>, g, b, 0, s, st, a);
+    }
     return hip_status(hipGetLastError());
 }
 
 int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
+    if (a.hout && !a.cu) return WCE_EINVAL;
     const dim3 g((unsigned)a.n), b(64);
     hipStream_t s = (hipStream_t)stream;
     const bool eq = (l.mask & WCE_EQUALIZE) && l.eq;
-    if (a.cu) {
-        if (eq) hipLaunchKernelGGL((mmse_solve_ls_kernel<true, true>), g, b, 0, s, st, a, l);
-        else hipLaunchKernelGGL((mmse_solve_ls_kernel<true, false>), g, b, 0, s, st, a, l);
-    } else {
-        if (eq) hipLaunchKernelGGL((mmse_solve_ls_kernel<false, true>), g, b, 0, s, st, a, l);
-        else hipLaunchKernelGGL((mmse_solve_ls_kernel<false, false>), g, b, 0, s, st, a, l);
-    }
+#define WCE_LAUNCH_SLS(R1, HOUT)                                                                        \
+    do {                                                                                                \
+        if (eq) hipLaunchKernelGGL((mmse_solve_ls_kernel<R1, HOUT, true>), g, b, 0, s, st, a, l);       \
+        else hipLaunchKernelGGL((mmse_solve_ls_kernel<R1, HOUT, false>), g, b, 0, s, st, a, l);         \
+    } while (0)
+    if (a.hout) WCE_LAUNCH_SLS(true, true);
+    else if (a.cu) WCE_LAUNCH_SLS(true, false);
+    else WCE_LAUNCH_SLS(false, false);
+#undef WCE_LAUNCH_SLS
     return hip_status(hipGetLastError());
 }
 

@@ -187,6 +187,10 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
             hh[t] = s / mk((long double)n, 0.0L);
         }
         mat_mul(F.data(), n, n, hh.data(), 1, Fh.data());
+        for (int i = 0; i < n; i++) {
+            st->cvec[2 * i] = (double)__real__ Fh[i];
+            st->cvec[2 * i + 1] = (double)__imag__ Fh[i];
+        }
         for (int i = 0; i < n; i++)      // F (h h') F' = (F h)(F h)'
             for (int j = 0; j < n; j++) {
                 cld cj = Fh[j];
