@@ -62,6 +62,36 @@ __device__ __forceinline__ void st2_nt(double *p, int64_t idx, double2 v)
     __builtin_nontemporal_store(t, reinterpret_cast<v2d *>(p) + idx);
 }
 
+// Sum over the 8 lanes l ^ {8, 16, 32} (same l & 7) without the LDS pipe:
+// xor 8 = DPP row_ror:8 inside each 16-lane row, xor 16 / 32 = gfx950's
+// v_permlane16/32_swap (swapping a copy with itself pairs lane l with l ^ 16
+// / l ^ 32; the two halves of the result sum to x + x^16 / x + x^32).  Same
+// pairs and order as the __shfl_xor butterfly, so results are bit-identical.
+__device__ __forceinline__ double dpp_ror8(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x128, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x128, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double sum_xor16(double v)
+{
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double sum_xor32(double v)
+{
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double2 sum_over_p(double2 w)
+{
+    w.x += dpp_ror8(w.x);
+    w.y += dpp_ror8(w.y);
+    return make_double2(sum_xor32(sum_xor16(w.x)), sum_xor32(sum_xor16(w.y)));
+}
+
 // wave-local LDS ordering (one wave owns the buffer; no workgroup barrier)
 __device__ __forceinline__ void wave_lds_sync()
 {

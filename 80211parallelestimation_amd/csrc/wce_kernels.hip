@@ -16,6 +16,11 @@
 #include "wce_internal.h"
 #include "wce_device.h"
 
+// A/B and timing-only switches (tools/variants.sh); defaults are the product.
+#ifndef WCE_BS_SHFL      // A/B: back-substitution butterfly through ds_bpermute
+#define WCE_BS_SHFL 0
+#endif
+
 namespace wce {
 
 // =====================================================================
@@ -305,9 +310,13 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     constexpr int NROW = (BLK == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
     // w_j = r_j * (conj(u_53,j) - sum_{i solved} conj(u_ij) z_i),  j = 8*BLK + q
     double2 w = P[BLK];
+#if WCE_BS_SHFL
     w = cadd(w, shfl_xor_c(w, 8));
     w = cadd(w, shfl_xor_c(w, 16));
     w = cadd(w, shfl_xor_c(w, 32));
+#else
+    w = sum_over_p(w);   // DPP + permlane swaps: no LDS traffic
+#endif
     w = cscale(w, rq[BLK]);
     s.blk[lane] = A[BLK][BLK];
     wave_lds_sync();
