@@ -123,18 +123,20 @@ class Dist:
 
 
 def pmc_traffic(kernel: str, launches_frames: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_summary.json, tools/pmc_passes.sh): FETCH_SIZE (KiB, x2 for
-    gfx950's half-counted 16-B/lane streaming reads, MI355X_MICROARCH.md HBM) +
-    WRITE_SIZE (KiB).  The summary was taken at 65,536 frames per launch."""
+    """HBM bytes per launch of `kernel` (a substring of the demangled name,
+    e.g. "mmse_solve_kernel<true>") from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_summary.json, tools/pmc_passes.sh): FETCH_SIZE (KiB, x2
+    for gfx950's half-counted 16-B/lane streaming reads, MI355X_MICROARCH.md
+    HBM) + WRITE_SIZE (KiB).  The summary was taken at 65,536 frames per launch."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    k = d.get("wce::" + kernel)
-    if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+    keys = [k for k in d if kernel in k and "FETCH_SIZE" in d[k] and "WRITE_SIZE" in d[k]]
+    if not keys:
         return None, None
+    k = d[sorted(keys, key=len)[0]]
     b = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0
     return b * launches_frames / 65536.0, os.path.basename(files[-1])
 
@@ -222,11 +224,13 @@ def main():
         t_apply = time_events(wce, stream, lambda: ctx.mmse_apply(W, H, B, N, s), reps)
         fl_solve = FLOP_SOLVE_TXT if mode == wce.MMSE_TEXTBOOK else FLOP_SOLVE_REF
         ach = fl_solve * B / (t_solve * 1e-3) / 1e12
-        res["roofline"] = {"bound": "mfma", "kernel": "mmse_solve_kernel (fp64 VALU Cholesky)",
+        kname = "mmse_solve_kernel<true>" if mode == wce.MMSE_TEXTBOOK else "mmse_solve_kernel<false>"
+        traffic, tsrc = pmc_traffic(kname, B)
+        res["roofline"] = {"bound": "mfma", "kernel": f"{kname} (fp64 VALU LDL^H solve)",
                            "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("mmse_solve_kernel", B)[0],
+                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": traffic,
                            "traffic_unit": "bytes/launch (FETCH_SIZEx2 + WRITE_SIZE)",
-                           "traffic_source": pmc_traffic("mmse_solve_kernel", B)[1],
+                           "traffic_source": tsrc,
                            "algorithmic_bytes": 3 * 848 * B,
                            "flop_per_frame": fl_solve, "frames_per_launch": B, "avg_launch_ms": t_solve,
                            "note": "peak = MI355X FP64 (vector = matrix, spec); traffic: see profiles/"}
@@ -325,9 +329,12 @@ def bench_front(wce, ctx, stream, n, reps):
             f()
         t = time_events(wce, stream, f, reps)
         gbs = per * units / (t * 1e-3) / 1e9
-        out[label] = {"kernel": f"front_kernel<{label == 'preamble'}>", "avg_launch_ms": t,
+        kn = f"front_kernel<{'true' if label == 'preamble' else 'false'}>"
+        traffic, _ = pmc_traffic(kn, n)
+        out[label] = {"kernel": kn, "avg_launch_ms": t,
                       "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_unit": per, "achieved_GBs": gbs,
-                      "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
+                      "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS,
+                      "algorithmic_bytes": per * units, "traffic": traffic}
     return out
 
 
