@@ -3,7 +3,7 @@
 Frames are independent, so a batch is partitioned over ranks (one process
 per GPU) with no data-path collective.  The only exchange is one broadcast
 of the packed shared state (wce::State: C, H_LT, tx_pre, sinc table, MMSE
-coefficients; ~68 KB) from the rank that built it -- the analogue of the
+coefficients, per-frame covariance operators; ~260 KB) from the rank that built it -- the analogue of the
 reference's MPI_Bcast of F/Ryy (main_mpi.c:687-688, 727-728).  With the
 "nccl" backend torch.distributed is RCCL over xGMI; "gloo" is used by the
 CPU tests.
