@@ -5,9 +5,11 @@
  *   wce_cli [frames] [mode: ref|textbook] [reps]
  *
  * Builds the shared state from a synthetic 802.11 preamble, generates the
- * frames on the device, runs LT_LS + PS_Linear/Cubic/Sinc + PS_MMSE +
- * equalization, and prints frames/s per configuration.  Exit code != 0 on
- * any wce error.
+ * frames (with per-frame preambles) on the device, runs LT_LS +
+ * PS_Linear/Cubic/Sinc + PS_MMSE + equalization in main.c and MATLAB
+ * semantics, per-frame-covariance MMSE, fp32 LS outputs and the time-domain
+ * front end, and prints frames/s per configuration.  Exit code != 0 on any
+ * wce error.
  */
 #include <math.h>
 #include <stdio.h>
@@ -70,24 +72,64 @@ int main(int argc, char **argv)
     void *stream;
     CHECK(wce_stream_create(&stream));
     const size_t fr = (size_t)WCE_NBLK * WCE_NSC;
-    wce_complex *tx, *rx, *h[5], *eq;
+    wce_complex *tx, *rx, *pre, *h[5], *eq;
     CHECK(wce_malloc((void **)&tx, B * fr * sizeof(wce_complex)));
     CHECK(wce_malloc((void **)&rx, B * fr * sizeof(wce_complex)));
+    CHECK(wce_malloc((void **)&pre, B * WCE_NSC * sizeof(wce_complex)));
     CHECK(wce_malloc((void **)&eq, B * fr * sizeof(wce_complex)));
     for (int i = 0; i < 5; i++) CHECK(wce_malloc((void **)&h[i], B * WCE_NSC * sizeof(wce_complex)));
-    CHECK(wce_synth_frames(ctx, tx, rx, NULL, fr, WCE_NSC, WCE_NSC, 0, B, 0x80211ull, NULL, A, ow2, stream));
-    wce_frames in = {tx, rx, NULL, NULL, (int64_t)fr, WCE_NSC, WCE_NSC, B, 0, 0};
+    CHECK(wce_synth_frames(ctx, tx, rx, pre, fr, WCE_NSC, WCE_NSC, 0, B, 0x80211ull, NULL, A, ow2, stream));
+    CHECK(wce_ctx_reserve(ctx, B));
+    wce_frames in = {tx, rx, NULL, NULL, (int64_t)fr, WCE_NSC, WCE_NSC, B, 0, WCE_SEM_C};
+    wce_frames in_pre = {tx, rx, pre, NULL, (int64_t)fr, WCE_NSC, WCE_NSC, B, 0, WCE_SEM_C};
+    wce_frames in_ml = {tx, rx, pre, NULL, (int64_t)fr, WCE_NSC, WCE_NSC, B, 0, WCE_SEM_MATLAB};
     wce_outputs out = {h[0], h[1], h[2], h[3], h[4], eq, WCE_NSC, (int64_t)fr, WCE_NSC, 0, 0};
-    struct { const char *name; unsigned mask; } cfg[] = {
-        {"LT_LS+PS_Linear", WCE_EST_LT_LS | WCE_EST_PS_LINEAR},
-        {"LS family (4 estimators)", WCE_EST_LS_ALL},
-        {"PS_MMSE", WCE_EST_PS_MMSE},
-        {"all 5 + equalization", WCE_EST_LS_ALL | WCE_EST_PS_MMSE | WCE_EQUALIZE},
+    wce_outputs out32 = out;
+    out32.flags = WCE_OUT_LS_F32;   /* same buffers, half the bytes used */
+    const unsigned all = WCE_EST_LS_ALL | WCE_EST_PS_MMSE | WCE_EQUALIZE;
+    struct { const char *name; const wce_frames *in; const wce_outputs *out; unsigned mask; } cfg[] = {
+        {"LT_LS+PS_Linear (per-frame preamble)", &in_pre, &out, WCE_EST_LT_LS | WCE_EST_PS_LINEAR},
+        {"LS family (4 estimators)", &in, &out, WCE_EST_LS_ALL},
+        {"PS_MMSE", &in, &out, WCE_EST_PS_MMSE},
+        {"PS_MMSE per-frame covariance", &in_pre, &out, WCE_EST_PS_MMSE | WCE_MMSE_FRAME_COV},
+        {"all 5 + equalization (fused)", &in_pre, &out, all},
+        {"all 5 + eq, fp32 LS outputs", &in_pre, &out32, all},
+        {"all 5 + eq, MATLAB semantics", &in_ml, &out, all},
     };
     printf("wce_cli: %ld frames, MMSE mode %s, %s\n", B, mode ? "textbook" : "ref", wce_version());
     for (unsigned c = 0; c < sizeof(cfg) / sizeof(cfg[0]); c++) {
-        float ms = time_it(stream, ctx, &in, &out, cfg[c].mask, reps);
-        printf("  %-26s %9.3f ms  %.3e frames/s\n", cfg[c].name, ms, B / (ms * 1e-3));
+        float ms = time_it(stream, ctx, cfg[c].in, cfg[c].out, cfg[c].mask, reps);
+        printf("  %-38s %9.3f ms  %.3e frames/s\n", cfg[c].name, ms, B / (ms * 1e-3));
+    }
+    /* time-domain front end (WiFi_blocks_extraction.m): 15 x 80 samples per frame */
+    {
+        const size_t ns = (size_t)WCE_NBLK * WCE_SAMPLES_PER_BLOCK;
+        wce_complex *samples, *lptot;
+        double *sig2;
+        CHECK(wce_malloc((void **)&samples, B * ns * sizeof(wce_complex)));
+        CHECK(wce_malloc((void **)&lptot, B * 160 * sizeof(wce_complex)));
+        CHECK(wce_malloc((void **)&sig2, B * sizeof(double)));
+        CHECK(wce_memset(samples, 0, B * ns * sizeof(wce_complex)));
+        CHECK(wce_memset(lptot, 0, B * 160 * sizeof(wce_complex)));
+        void *e0, *e1;
+        float ms = 0;
+        CHECK(wce_event_create(&e0));
+        CHECK(wce_event_create(&e1));
+        CHECK(wce_front_end_blocks(ctx, samples, (int64_t)ns, B, WCE_NBLK, rx, (int64_t)fr, WCE_NSC, stream));
+        CHECK(wce_event_record(e0, stream));
+        for (int i = 0; i < reps; i++) {
+            CHECK(wce_front_end_preamble(ctx, lptot, 160, 160, B, pre, WCE_NSC, sig2, stream));
+            CHECK(wce_front_end_blocks(ctx, samples, (int64_t)ns, B, WCE_NBLK, rx, (int64_t)fr, WCE_NSC, stream));
+        }
+        CHECK(wce_event_record(e1, stream));
+        CHECK(wce_event_elapsed_ms(&ms, e0, e1));
+        ms /= reps;
+        printf("  %-38s %9.3f ms  %.3e frames/s\n", "front end (LTF + 15 blocks)", ms, B / (ms * 1e-3));
+        wce_event_destroy(e0);
+        wce_event_destroy(e1);
+        wce_free(samples);
+        wce_free(lptot);
+        wce_free(sig2);
     }
     /* spot check: LT_LS of frame 0 at DC must be 0 (main.c:74) */
     wce_complex h0[WCE_NSC];
@@ -98,6 +140,7 @@ int main(int argc, char **argv)
         return 3;
     }
     for (int i = 0; i < 5; i++) wce_free(h[i]);
+    wce_free(pre);
     wce_free(tx);
     wce_free(rx);
     wce_free(eq);
