@@ -264,6 +264,9 @@ def main():
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
         res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
+        refc = cpu_reference(args.cpu_seconds / 2)
+        if refc is not None:
+            res["cpu_baseline"]["reference_code"] = refc
 
     if dist.rank == 0:
         print(json.dumps(res), flush=True)
@@ -388,6 +391,54 @@ def bench_frame_cov(wce, make_ctx, stream, n, reps):
         t = time_events(wce, stream, f, reps)
         out[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3)}
         del c
+    return out
+
+
+def cpu_reference(budget_s):
+    """The reference's OWN sequential code (oracle/_ref/libref.so, compiled
+    from its main.c/utils.c by oracle/Makefile; 1 core), when that library was
+    built and travelled with the snapshot: LT_LS + PS_Linear (config 2) and
+    REF-mode PS_MMSE through its matrix routines (NaN inverse(Ryy) repaired,
+    per-frame inverse(F) hoisted)."""
+    import ctypes
+    lib_path = os.path.join(REPO, "oracle", "_ref", "libref.so")
+    if not os.path.exists(lib_path):
+        return None
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py
+    lib = ctypes.CDLL(lib_path)
+    P = ctypes.c_void_p
+    lib.refh_bench_ls.restype = ctypes.c_double
+    lib.refh_bench_ls.argtypes = [ctypes.c_int] + [P] * 6
+    lib.refh_bench_mmse.restype = ctypes.c_double
+    lib.refh_bench_mmse.argtypes = [ctypes.c_int, P, P, P, ctypes.c_double, P, P, P]
+    LD = np.clongdouble
+    inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
+    ref = dict(np.load(os.path.join(REPO, "tests", "golden", "ref_vectors.npz")))
+    rng = np.random.default_rng(0)
+    p = lambda a: a.ctypes.data_as(P)
+    out = {"kind": "reference", "cores": 1,
+           "source": "oracle/_ref/libref.so = /root/reference main.c + utils.c, g++ -O2 (oracle/Makefile)"}
+    n = 100000
+    tx = np.ascontiguousarray(np.repeat(inp["tx_symb"][0][None], n, 0).astype(LD))
+    rx = np.ascontiguousarray((np.repeat(inp["rx_symb"][0][None], n, 0)
+                               * (1 + 0.01 * rng.standard_normal((n, 1)))).astype(LD))
+    pre = np.ascontiguousarray((np.repeat(inp["rx_pre"][None], n, 0)
+                                * (1 + 0.01 * rng.standard_normal((n, 1)))).astype(LD))
+    tpre = np.ascontiguousarray(inp["tx_pre"].astype(LD))
+    h1, h2 = np.zeros((n, N), LD), np.zeros((n, N), LD)
+    t = lib.refh_bench_ls(n, p(tpre), p(pre), p(tx), p(rx), p(h1), p(h2))
+    out["ls_config2"] = {"value": n / t, "unit": "frames/s", "sample": f"{n} frames, {t:.2f} s"}
+    F = np.ascontiguousarray(oracle_py.from_split(ref["F"]))
+    invF = np.ascontiguousarray(oracle_py.from_split(ref["invF"]))
+    hls = np.ascontiguousarray(oracle_py.lt_ls(inp["tx_pre"], inp["rx_pre"]).astype(LD))
+    H = np.zeros((n, N), LD)
+    t1 = lib.refh_bench_mmse(1, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(invF), p(H))
+    m = int(max(1, min(n, budget_s / max(t1, 1e-6))))
+    t = lib.refh_bench_mmse(m, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(invF), p(H))
+    out["mmse_ref_mode"] = {"value": m / t, "unit": "frames/s", "sample": f"{m} frames, {t:.2f} s",
+                            "note": "the reference's literal PS_MMSE also spends ~4 s per frame inverting F "
+                                    "and returns NaN; both are removed here"}
     return out
 
 

@@ -108,4 +108,31 @@ void refh_mmse_repaired(ldc *tx_symbols, ldc *rx_symbols, ldc *Fflat, double ow2
     free(buf);
 }
 
+// ---- CPU baselines timed by bench.py (the reference's own sequential code) ----
+// Frames are [n][53] long double complex.  Return wall seconds.
+
+// LT_LS (per-frame preamble) + PS_Linear: BASELINE configs[1], main.c:66-101
+double refh_bench_ls(int n, ldc *tx_pre, ldc *rx_pre, ldc *tx, ldc *rx, ldc *H_lt, ldc *H_lin)
+{
+    const double t0 = omp_get_wtime();
+    for (int f = 0; f < n; f++) {
+        const size_t o = (size_t)f * SAMPUTIL;
+        WiFi_channel_estimation_LT_LS(tx_pre, rx_pre + o, H_lt + o);
+        WiFi_channel_estimation_PS_Linear(tx + o, rx + o, H_lin + o);
+    }
+    return omp_get_wtime() - t0;
+}
+
+// PS_MMSE, main.c:148-212 with its own matrix routines, the NaN inverse(Ryy)
+// repaired and the per-frame 4-s inverse(F) hoisted (invF given): REF mode
+double refh_bench_mmse(int n, ldc *tx, ldc *rx, ldc *F, double ow2, ldc *H_ls, ldc *invF, ldc *H)
+{
+    const double t0 = omp_get_wtime();
+    for (int f = 0; f < n; f++) {
+        const size_t o = (size_t)f * SAMPUTIL;
+        refh_mmse_repaired(tx + o, rx + o, F, ow2, H_ls, invF, H + o, NULL);
+    }
+    return omp_get_wtime() - t0;
+}
+
 }  // extern "C"
