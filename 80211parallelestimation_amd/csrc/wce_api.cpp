@@ -24,6 +24,10 @@ struct wce_ctx {
 };
 
 static constexpr int64_t WS_LD = 64;   // row stride (complex) of the workspace vectors
+// workspace arrays of [frames][WS_LD] complex: h | g | u | w | aux (per-block
+// MMSE dots).  MATLAB block averaging without FRAME_COV uses arrays 0..3 as
+// the per-block W rows [frames * 4][WS_LD].
+static constexpr int64_t WS_ARRAYS = 5;
 
 static thread_local std::string g_err;
 
@@ -277,6 +281,8 @@ int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_s
     if (rc) return rc;
     if (in->n_frames == 0) return WCE_OK;
     if (!W || (in->n_frames > 1 && w_stride < wce::NSC)) return fail(WCE_EINVAL, "bad W");
+    if (in->semantics != WCE_SEM_C)
+        return fail(WCE_EINVAL, "wce_mmse_solve (profiling entry) takes C semantics; MATLAB runs via wce_estimate");
     wce::SolveArgs a = solve_args(c, in, W, w_stride);
     DeviceGuard g(c->device);
     rc = wce::launch_mmse_solve(c->d_state, a, stream);
@@ -306,7 +312,7 @@ static int ensure_ws(wce_ctx *c, int64_t n)
         c->ws = nullptr;
         c->ws_frames = 0;
     }
-    HIPCHECK(hipMalloc(&c->ws, (size_t)n * 4 * WS_LD * 2 * sizeof(double)), "hipMalloc(workspace)");
+    HIPCHECK(hipMalloc(&c->ws, (size_t)n * WS_ARRAYS * WS_LD * 2 * sizeof(double)), "hipMalloc(workspace)");
     c->ws_frames = n;
     return WCE_OK;
 }
@@ -406,17 +412,34 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     if (!mmse) return WCE_OK;
     wce::SolveArgs sa = solve_args(c, in, out->ps_mmse, out->out_stride);
     const bool fc = (mask & WCE_MMSE_FRAME_COV) != 0;
+    const bool split = sa.nblk > 1;   // MATLAB: one wave per (frame, block), averaged after
+    if (split && n * sa.nblk > INT32_MAX) return fail(WCE_EINVAL, "n_frames * 4 > 2^31 - 1 (MATLAB semantics)");
+    if (fc || split) {
+        rc = ensure_ws(c, n);
+        if (rc) return rc;
+    }
     if (fc) {
         const bool lt_ready = !fuse && (mask & WCE_EST_LT_LS) && !(out->flags & WCE_OUT_LS_F32);
         rc = prep_frame_cov(c, in, out, lt_ready, sa, stream);
         if (rc) return rc;
     }
+    double *aux = c->ws ? c->ws + (WS_ARRAYS - 1) * n * WS_LD * 2 : nullptr;
+    if (split) {
+        sa.split = 1;
+        if (fc) {
+            sa.dots = aux;
+        } else {
+            sa.w = c->ws;
+            sa.ws = WS_LD;
+        }
+    }
     rc = fuse ? wce::launch_mmse_solve_ls(c->d_state, sa, la, stream) : wce::launch_mmse_solve(c->d_state, sa, stream);
     if (rc) return fail(rc, "mmse_solve launch");
-    if (!fc) {   // H = C W in place (per-frame covariance writes H directly)
-        rc = wce::launch_mmse_apply(c->d_state, sa.w, sa.w, out->out_stride, n, stream);
-        if (rc) return fail(rc, "mmse_apply launch");
-    }
+    double *H = reinterpret_cast<double *>(out->ps_mmse);
+    if (fc && split) rc = wce::launch_fc_finish(sa, aux, H, out->out_stride, stream);
+    else if (split) rc = wce::launch_matvec_avg(c->d_state->C, c->ws, WS_LD, sa.nblk, H, out->out_stride, n, stream);
+    else if (!fc) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream);   // H = C W in place
+    if (rc) return fail(rc, "mmse apply launch");
     return WCE_OK;
 }
 

@@ -86,7 +86,9 @@ struct SolveArgs {
     const double *cu, *cw;
     int64_t cs;
     int32_t hout;             // 1: write H = cu (cw . W) directly (no apply step)
-    int32_t pad1;
+    int32_t split;            // MATLAB averaging: nblk waves per frame, wave g = f*nblk + b
+                              // writes W_b to w[g*ws] (or, with hout, cw . W_b to dots[g])
+    double *dots;
 };
 struct SynthArgs {
     double *tx, *rx, *rx_pre;
@@ -116,6 +118,11 @@ int launch_mmse_apply(const State *st, const double *W, double *H, int64_t strid
 // qin: X replaced by (re X - im X, 0) first.
 int launch_matvec(const double *M1, const double *M2, const double *X, int64_t xs, double *Y1, double *Y2,
                   int64_t ys, int64_t n, bool qin, void *stream);
+// Y[f] = M mean_b X[f*nb + b]  (MATLAB block average folded into the apply)
+int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, double *Y, int64_t ys, int64_t n,
+                      void *stream);
+// H[f] = cu_f * mean_b dots[f*nb + b]  (per-frame covariance, MATLAB averaging)
+int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 
 }  // namespace wce

@@ -473,14 +473,17 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 
 // R1: Ryy built from the rank-1 factors SolveArgs::cu/cw (TEXTBOOK: State::cvec)
 // instead of the dense State::C (COV mode, or a = 0).
+// split (MATLAB averaging): one wave per (frame, block), W_b to row g of a.w.
 template <bool R1>
 __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
-    const int64_t f = blockIdx.x;
+    const int64_t g = blockIdx.x;
+    const int64_t f = a.split ? g / a.nblk : g;
+    const int b = a.split ? (int)(g - f * a.nblk) : 0;
     if (f >= a.n) return;
-    const double2 w = solve_block<R1>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
-    if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, w);
+    const double2 w = solve_block<R1>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
+    if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, w);
 }
 
 // Config 5 fused: the MMSE solve of one frame, then -- with the wave's
@@ -523,51 +526,43 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     if (act) ls_store<EQ>(l, f, k, mask, hlt, hlin, hcub, hsnc);
 }
 
-// MATLAB semantics (WiFi_channel_estimation_PS_MMSE.m): the estimate is the
-// mean of the per-block MMSE estimates of blocks 0..nblk-1.  H = C W is linear
-// in W, so the mean is taken on W and the apply kernel runs once.
-template <bool R1>
-__global__ __launch_bounds__(64, 2) void mmse_solve_avg_kernel(const State *__restrict__ st, SolveArgs a)
-{
-    __shared__ SolveLds s;
-    const int64_t f = blockIdx.x;
-    if (f >= a.n) return;
-    double2 acc = make_double2(0.0, 0.0);
-    for (int b = 0; b < a.nblk; ++b) {
-        acc = cadd(acc, solve_block<R1>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f));
-        wave_lds_sync();   // the next block overwrites s
-    }
-    if (threadIdx.x < NSC) st2(a.w, f * a.ws + threadIdx.x, cscale(acc, 1.0 / a.nblk));
-}
-
 // Per-frame covariance (WCE_MMSE_FRAME_COV): C_f = u_f w_f^T, so the product
 // C_f W_f collapses to u_f (w_f . W_f): a wave reduction replaces the MFMA
-// apply, and the kernel writes H directly.  Averages nblk blocks (MATLAB).
-template <bool AVG>
-__global__ __launch_bounds__(64, AVG ? 2 : WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_kernel(
-    const State *__restrict__ st, SolveArgs a)
+// apply, and the kernel writes H directly.  split (MATLAB): one wave per
+// (frame, block) writes its w_f . W_b to dots[g]; fc_finish averages.
+__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_kernel(const State *__restrict__ st,
+                                                                                    SolveArgs a)
 {
     __shared__ SolveLds s;
-    const int64_t f = blockIdx.x;
+    const int64_t g = blockIdx.x;
+    const int64_t f = a.split ? g / a.nblk : g;
+    const int b = a.split ? (int)(g - f * a.nblk) : 0;
     if (f >= a.n) return;
     const int lane = threadIdx.x;
     const bool act = lane < NSC;
-    double2 dot = make_double2(0.0, 0.0);
-    const int nb = AVG ? a.nblk : 1;
-    for (int b = 0; b < nb; ++b) {
-        const double2 wz = solve_block<true>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
-        const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
-        const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
-        double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
+    const double2 wz = solve_block<true>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
+    const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+    const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+    double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
-        dot = cadd(dot, t);
-        if (AVG) wave_lds_sync();   // the next block overwrites s
+    for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
+    if (a.split) {
+        if (lane == 0) st2(a.dots, g, t);
+    } else if (act) {
+        st2(a.w, f * a.ws + lane, cmul(uf, t));
     }
-    if (act) {
-        const double2 uf = ld2(a.cu, f * a.cs + lane);
-        st2(a.w, f * a.ws + lane, cmul(uf, AVG ? cscale(dot, 1.0 / a.nblk) : dot));
-    }
+}
+
+// H[f] = cu_f * mean_b dots[f*nblk + b]: one wave per frame, lane = subcarrier
+__global__ __launch_bounds__(256) void fc_finish_kernel(SolveArgs a, const double *__restrict__ dots, double *H,
+                                                        int64_t hs)
+{
+    const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (f >= a.n || lane >= NSC) return;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int b = 0; b < a.nblk; ++b) acc = cadd(acc, ld2(dots, f * a.nblk + b));
+    st2(H, f * hs + lane, cmul(ld2(a.cu, f * a.cs + lane), cscale(acc, 1.0 / a.nblk)));
 }
 
 // =====================================================================
@@ -583,7 +578,9 @@ constexpr int APPLY_WAVES = 4;
 
 // Y1[f] = M1 X[f] (and Y2[f] = M2 X[f]) for 16-frame tiles; M padded 64 x 64.
 // QIN: the input is replaced by (re X - im X, 0) (main.c:188's real "conj").
-template <bool QIN, bool TWO>
+// NB > 1: the input of frame f is the mean of rows f*NB .. f*NB+NB-1 of X
+// (MATLAB's block average, summed in block order like the reference's mean).
+template <bool QIN, bool TWO, int NB = 1>
 __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ M1, const double *__restrict__ M2,
                                                      const double *X, int64_t xs, double *Y1, double *Y2,
                                                      int64_t ys, int64_t n)
@@ -597,7 +594,16 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
         const int j = 4 * s + kl;
-        double2 v = (fa < n && j < NSC) ? ld2(X, fa * xs + j) : make_double2(0, 0);
+        double2 v = make_double2(0, 0);
+        if (fa < n && j < NSC) {
+            if constexpr (NB == 1) {
+                v = ld2(X, fa * xs + j);
+            } else {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) v = cadd(v, ld2(X, (fa * NB + b) * xs + j));
+                v = cscale(v, 1.0 / NB);
+            }
+        }
         if constexpr (QIN) v = make_double2(v.x - v.y, 0.0);
         ar[s] = v.x; ai[s] = v.y; nai[s] = -v.y;
     }
@@ -724,21 +730,23 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
 int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
-    if (a.n > 0x7fffffffll) return WCE_EINVAL;
+    const int64_t waves = a.split ? a.n * a.nblk : a.n;
+    if (waves > 0x7fffffffll) return WCE_EINVAL;
     if (a.hout && !a.cu) return WCE_EINVAL;
-    const dim3 g((unsigned)a.n), b(64);
+    if (a.nblk > 1 && !a.split) return WCE_EINVAL;   // block averaging runs split
+    const dim3 g((unsigned)waves), b(64);
     hipStream_t s = (hipStream_t)stream;
-    const bool avg = a.nblk > 1;
-    if (a.hout) {
-        if (avg) hipLaunchKernelGGL(mmse_solve_fc_kernel<true>, g, b, 0, s, st, a);
-        else hipLaunchKernelGGL(mmse_solve_fc_kernel<false>, g, b, 0, s, st, a);
-    } else if (a.cu) {
-        if (avg) hipLaunchKernelGGL(mmse_solve_avg_kernel<true>, g, b, 0, s, st, a);
-        else hipLaunchKernelGGL(mmse_solve_kernel<true>, g, b, 0, s, st, a);
-    } else {
-        if (avg) hipLaunchKernelGGL(mmse_solve_avg_kernel<false>, g, b, 0, s, st, a);
-        else hipLaunchKernelGGL(mmse_solve_kernel<false>, g, b, 0, s, st, a);
-    }
+    if (a.hout) hipLaunchKernelGGL(mmse_solve_fc_kernel, g, b, 0, s, st, a);
+    else if (a.cu) hipLaunchKernelGGL(mmse_solve_kernel<true>, g, b, 0, s, st, a);
+    else hipLaunchKernelGGL(mmse_solve_kernel<false>, g, b, 0, s, st, a);
+    return hip_status(hipGetLastError());
+}
+
+int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    hipLaunchKernelGGL(fc_finish_kernel, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a,
+                       dots, H, hs);
     return hip_status(hipGetLastError());
 }
 
@@ -764,6 +772,17 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream)
 {
     return launch_matvec(st->C, nullptr, W, stride, H, nullptr, stride, n, false, stream);
+}
+
+int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, double *Y, int64_t ys, int64_t n,
+                      void *stream)
+{
+    if (n <= 0) return WCE_OK;
+    if (nb != 4) return WCE_EINVAL;   // MATLAB semantics averages blocks 1..4
+    const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
+    hipLaunchKernelGGL((matvec_kernel<false, false, 4>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       M, nullptr, X, xs, Y, nullptr, ys, n);
+    return hip_status(hipGetLastError());
 }
 
 int launch_matvec(const double *M1, const double *M2, const double *X, int64_t xs, double *Y1, double *Y2,

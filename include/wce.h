@@ -161,8 +161,9 @@ typedef struct {
  * count elements of each buffer's own type. */
 #define WCE_OUT_LS_F32 (1u << 0)
 
-/* Pre-size the context's device workspace for WCE_MMSE_FRAME_COV batches of up
- * to n_frames (3 KB per frame), so that wce_estimate never allocates.  Without
+/* Pre-size the context's device workspace (WCE_MMSE_FRAME_COV and MATLAB-
+ * semantics PS_MMSE) for batches of up to n_frames (5 KB per frame), so that
+ * wce_estimate never allocates.  Without
  * it the first larger batch allocates (synchronously) and keeps the buffer. */
 int wce_ctx_reserve(wce_ctx *ctx, int64_t n_frames);
 

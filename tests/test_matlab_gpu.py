@@ -121,3 +121,5 @@ def test_matlab_semantics_errors(gpu_wce, golden):
         ctx.estimate(ctx.frames(tx, rx, 2, semantics=7), o, gpu_wce.PS_LINEAR)
     with pytest.raises(gpu_wce.WceError):   # MATLAB semantics reads 4 blocks: block stride >= 53
         ctx.estimate(ctx.frames(tx, rx, 2, block_stride=1, semantics=gpu_wce.SEM_MATLAB), o, gpu_wce.PS_LINEAR)
+    with pytest.raises(gpu_wce.WceError):   # the profiling entry point takes C semantics only
+        ctx.mmse_solve(ctx.frames(tx, rx, 2, semantics=gpu_wce.SEM_MATLAB), h, N)
