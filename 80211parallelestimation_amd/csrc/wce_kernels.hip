@@ -30,9 +30,6 @@ constexpr int LS_WAVES = 4;   // waves per 256-thread workgroup
 #ifndef WCE_LS_FRAMES
 #define WCE_LS_FRAMES 4
 #endif
-#ifndef WCE_LS_MINBLOCKS
-#define WCE_LS_MINBLOCKS 1
-#endif
 constexpr int LS_FRAMES = WCE_LS_FRAMES;  // frames per wave iteration: all loads issued up front
 
 // Per-lane (subcarrier k) constants of the LS family, shared by ls_kernel and
@@ -143,7 +140,7 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
 // 4-block average of the per-block estimates is the per-block formula applied
 // to the averaged pilots -- proper conj in LT_LS, cubic divisors 14/28/42.
 template <bool EQ, bool ML>
-__global__ __launch_bounds__(256, WCE_LS_MINBLOCKS) void ls_kernel(const State *__restrict__ st, LsArgs a)
+__global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
 {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * LS_WAVES;
