@@ -78,9 +78,10 @@ enum { WCE_MMSE_REF = 0, WCE_MMSE_TEXTBOOK = 1, WCE_MMSE_COV = 2 };
 
 typedef struct wce_ctx wce_ctx;
 
-/* Build the shared state on the host (F, the reference's cofactor invF in
- * 80-bit long double, H_LT from the shared preamble, the MMSE covariance C,
- * the sinc table) and upload it to `device`.  tx_pre/rx_pre: the shared
+/* Build the shared state on the host (F as main.c:18-26 builds it, the
+ * reference's cofactor invF of utils.c:141-170 in 80-bit long double, H_LT
+ * from the shared preamble (main.c:66-75), the MMSE covariance C of
+ * main.c:186-203, the sinc table of utils.c:727-733) and upload it to `device`.  tx_pre/rx_pre: the shared
  * preamble FFTs (53 each, host).  The first call in a process spends
  * ~0.5 s (8 threads) on invF; later calls reuse it. */
 int wce_ctx_create(wce_ctx **ctx, int device, const wce_complex *tx_pre,
@@ -168,7 +169,8 @@ typedef struct {
 int wce_ctx_reserve(wce_ctx *ctx, int64_t n_frames);
 
 /* Run the estimators selected in `mask` over all frames, asynchronously on
- * `stream`.  LS family + equalization: one HBM-streaming kernel; MMSE: the
+ * `stream`.  Replaces the per-frame calls of main.c:37-54 (and the frame
+ * loops of main_openmp.c / main_mpi.c) with one batched call.  LS family + equalization: one HBM-streaming kernel; MMSE: the
  * LDS/register-resident Cholesky solve kernel followed by the MFMA GEMM
  * (the ps_mmse buffer doubles as the solve->GEMM workspace). */
 int wce_estimate(wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
