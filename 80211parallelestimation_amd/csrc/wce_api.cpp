@@ -443,6 +443,60 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     return WCE_OK;
 }
 
+struct wce_plan {
+    int device = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+int wce_plan_create(wce_plan **out_plan, wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask)
+{
+    if (!out_plan || !c || !in || !out) return fail(WCE_EINVAL, "null argument");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    DeviceGuard g(c->device);
+    // size the workspace now: nothing may allocate while the stream is captured
+    if ((mask & WCE_MMSE_FRAME_COV) || (in->semantics == WCE_SEM_MATLAB && (mask & WCE_EST_PS_MMSE))) {
+        int rc = ensure_ws(c, in->n_frames);
+        if (rc) return rc;
+    }
+    hipStream_t cs = nullptr;
+    HIPCHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan capture stream");
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) { (void)hipStreamDestroy(cs); return hipfail(e, "hipStreamBeginCapture"); }
+    const int rc = wce_estimate(c, in, out, mask, cs);   // validates, then records the launches
+    hipGraph_t graph = nullptr;
+    e = hipStreamEndCapture(cs, &graph);
+    (void)hipStreamDestroy(cs);
+    if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+    if (e != hipSuccess) return hipfail(e, "hipStreamEndCapture");
+    wce_plan *p = new (std::nothrow) wce_plan;
+    if (!p) { (void)hipGraphDestroy(graph); return fail(WCE_ENOMEM, "alloc"); }
+    p->device = c->device;
+    p->graph = graph;
+    e = hipGraphInstantiate(&p->exec, graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) { (void)hipGraphDestroy(graph); delete p; return hipfail(e, "hipGraphInstantiate"); }
+    *out_plan = p;
+    return WCE_OK;
+}
+
+int wce_plan_launch(wce_plan *p, void *stream)
+{
+    if (!p || !p->exec) return fail(WCE_EINVAL, "null plan");
+    DeviceGuard g(p->device);
+    HIPCHECK(hipGraphLaunch(p->exec, (hipStream_t)stream), "hipGraphLaunch");
+    return WCE_OK;
+}
+
+int wce_plan_destroy(wce_plan *p)
+{
+    if (!p) return WCE_OK;
+    DeviceGuard g(p->device);
+    if (p->exec) (void)hipGraphExecDestroy(p->exec);
+    if (p->graph) (void)hipGraphDestroy(p->graph);
+    delete p;
+    return WCE_OK;
+}
+
 extern "C" int wce_debug_set_fusion(wce_ctx *c, int on)
 {
     if (!c) return fail(WCE_EINVAL, "null ctx");

@@ -90,6 +90,9 @@ ABI = {
     "wce_ctx_create_empty": [POINTER(c_void_p), c_int],
     "wce_ctx_destroy": [c_void_p],
     "wce_ctx_reserve": [c_void_p, c_int64],
+    "wce_plan_create": [POINTER(c_void_p), c_void_p, c_void_p, c_void_p, c_uint32],
+    "wce_plan_launch": [c_void_p, c_void_p],
+    "wce_plan_destroy": [c_void_p],
     "wce_ctx_create_cov": [POINTER(c_void_p), c_int, c_void_p, c_void_p, c_void_p, c_double],
     "wce_state_build_cov": [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_double],
     "wce_debug_set_fusion": [c_void_p, c_int],
@@ -249,6 +252,10 @@ class Context:
         """A/B switch: LS family + equalization fused into the MMSE solve (default on)."""
         _check(_lib.wce_debug_set_fusion(self.handle, int(bool(on))), "wce_debug_set_fusion")
 
+    def plan(self, frames: "Frames", outputs: "Outputs", mask: int) -> "Plan":
+        """Capture one estimate call into a HIP graph (wce_plan_create)."""
+        return Plan(self, frames, outputs, mask)
+
     def reserve(self, n_frames):
         """Pre-size the WCE_MMSE_FRAME_COV workspace (no allocation inside estimate)."""
         _check(_lib.wce_ctx_reserve(self.handle, n_frames), "wce_ctx_reserve")
@@ -368,6 +375,32 @@ class Context:
         if deq is not None:
             res["eq"] = deq.numpy()
         return res
+
+
+class Plan:
+    """wce_plan: a captured wce_estimate call, replayed with one graph launch.
+    Keeps references to the frames/outputs structs (the buffers they point
+    to must outlive the plan)."""
+
+    def __init__(self, ctx, frames, outputs, mask):
+        self.handle = c_void_p()
+        self._keep = (ctx, frames, outputs)
+        _check(_lib.wce_plan_create(byref(self.handle), ctx.handle, byref(frames), byref(outputs), mask),
+               "wce_plan_create")
+
+    def launch(self, stream=None):
+        _check(_lib.wce_plan_launch(self.handle, stream), "wce_plan_launch")
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            _lib.wce_plan_destroy(self.handle)
+            self.handle = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
 
 
 def state_blob(tx_pre, rx_pre, ow2, mode=MMSE_REF, Rhh=None) -> np.ndarray:

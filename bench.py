@@ -261,6 +261,7 @@ def main():
             local_ctx = lambda m: wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m, device=dev)
             res["frame_cov"] = bench_frame_cov(wce, local_ctx, stream, B, reps)
             res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
+            res["small_batch"] = bench_small_batch(wce, ctx, stream)
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
         res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
@@ -339,6 +340,33 @@ def bench_front(wce, ctx, stream, n, reps):
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS,
                       "algorithmic_bytes": per * units, "traffic": traffic}
     return out
+
+
+def bench_small_batch(wce, ctx, stream, n=1024, calls=200):
+    """Serving-style small batches (all 5 estimators + equalization, per-frame
+    preamble, 1,024 frames per call): direct wce_estimate calls vs one
+    captured HIP-graph plan replayed (wce_plan), host wall clock per call."""
+    s = stream.handle
+    tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+    ctx.synth(tx, rx, pre, n, seed=5, stream=s)
+    outs = [wce.DeviceArray((n, N)) for _ in range(5)]
+    eq = wce.DeviceArray((n, NBLK, N))
+    o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, 0)
+    fr = ctx.frames(tx, rx, n, rx_pre=pre)
+    plan = ctx.plan(fr, o, wce.ALL)
+    res = {"workload": f"{n} frames per call, all 5 estimators + equalization, per-frame preamble", "calls": calls}
+    for label, f in (("direct", lambda: ctx.estimate(fr, o, wce.ALL, s)), ("plan", lambda: plan.launch(s))):
+        for _ in range(20):
+            f()
+        stream.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            f()
+        stream.synchronize()
+        dt = (time.perf_counter() - t0) / calls
+        res[label] = {"us_per_call": dt * 1e6, "frames_per_s": n / dt}
+    plan.close()
+    return res
 
 
 def bench_config5(wce, ctx, stream, n, reps):

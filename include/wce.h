@@ -176,6 +176,19 @@ int wce_ctx_reserve(wce_ctx *ctx, int64_t n_frames);
 int wce_estimate(wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
                  uint32_t mask, void *stream);
 
+/* Launch plans: one wce_estimate call (fixed buffers, strides, mask, batch)
+ * captured into a HIP graph once and replayed with a single graph launch --
+ * for serving loops that re-run small batches into the same buffers, where
+ * per-call host checks and kernel launch latency dominate.  Arguments are
+ * validated and the workspace sized at creation; the plan keeps raw
+ * pointers, so the buffers must outlive it.  NULL stream: the plan uses a
+ * private stream for capture; launches go to the stream given. */
+typedef struct wce_plan wce_plan;
+int wce_plan_create(wce_plan **plan, wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
+                    uint32_t mask);
+int wce_plan_launch(wce_plan *plan, void *stream);
+int wce_plan_destroy(wce_plan *plan);
+
 /* The two MMSE stages, exposed for profiling:
  *   solve: W[f] = X_f (a X_f C X_f' + b I)^-1 rx_f        (FP64 VALU, per frame)
  *   apply: H[f] = C W[f]                                  (FP64 MFMA batched GEMM)

@@ -363,3 +363,37 @@ def test_model_covariance_dense_solve(gpu_wce, golden, oracle):
     for f in np.concatenate([[0, B - 1], rng.choice(B, 10, replace=False)]):
         exp = oracle.mmse_unified(C, ones, a, b, txh[f, 0], rxh[f, 0])
         assert normrel(out["ps_mmse"][f], exp) < TOL, f
+
+
+@pytest.mark.parametrize("mask_name", ["ALL", "MMSE_FC_ML"])
+def test_plan_graph_replay_matches_estimate(gpu_wce, golden, mask_name):
+    """wce_plan (HIP graph capture of one estimate call) replays to bit-identical
+    outputs, including the workspace-using per-frame-covariance MATLAB path."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_TEXTBOOK)
+    B = 384
+    tx, rx, pre = _synth(ctx, gpu_wce, B, seed=12, rx_pre=True)
+    if mask_name == "ALL":
+        mask, sem = gpu_wce.ALL, gpu_wce.SEM_C
+    else:
+        mask, sem = gpu_wce.PS_MMSE | gpu_wce.FRAME_COV, gpu_wce.SEM_MATLAB
+    outs = [gpu_wce.DeviceArray((B, N), zero=True) for _ in range(5)]
+    eq = gpu_wce.DeviceArray((B, NBLK, N), zero=True)
+    o = gpu_wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, 0)
+    fr = ctx.frames(tx, rx, B, rx_pre=pre, semantics=sem)
+    ctx.estimate(fr, o, mask)
+    gpu_wce.synchronize()
+    ref = [x.numpy() for x in outs] + [eq.numpy()]
+    for x in outs + [eq]:
+        assert gpu_wce.load().wce_memset(x.addr, 0, x.nbytes) == 0
+    plan = ctx.plan(fr, o, mask)
+    st = gpu_wce.Stream()
+    for _ in range(3):
+        plan.launch(st.handle)
+    st.synchronize()
+    got = [x.numpy() for x in outs] + [eq.numpy()]
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    plan.close()
+    with pytest.raises(gpu_wce.WceError):   # invalid calls fail at creation, nothing captured
+        ctx.plan(ctx.frames(tx, rx, B, block=99), o, mask)
