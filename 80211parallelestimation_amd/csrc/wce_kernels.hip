@@ -321,16 +321,15 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     w = sum_over_p(w);   // DPP + permlane swaps: no LDS traffic
 #endif
     w = cscale(w, rq[BLK]);
-    s.blk[lane] = A[BLK][BLK];
+    // L = u r of the diagonal block, strictly lower part only, scaled and
+    // masked once by its owner (r depends on the column q only)
+    s.blk[lane] = (q < p) ? cscale(A[BLK][BLK], rq[BLK]) : make_double2(0.0, 0.0);
     wave_lds_sync();
     // lb[t] = L[8*BLK + t][8*BLK + q] for q < t, else 0: a lane's w_q is left
     // untouched once row q is solved, so it ends holding z_q
     double2 lb[NROW];
 #pragma unroll
-    for (int t = 0; t < NROW; ++t) {
-        const double2 v = cscale(s.blk[8 * t + q], rq[BLK]);
-        lb[t] = (q < t) ? v : make_double2(0.0, 0.0);
-    }
+    for (int t = 0; t < NROW; ++t) lb[t] = s.blk[8 * t + q];
 #pragma unroll
     for (int t = NROW - 1; t >= 0; --t) {
         const double2 z = readlane_c(w, t);                   // lane t = (0, t) holds w_t = z_t
