@@ -19,6 +19,7 @@ struct wce_ctx {
     State host;                 // host copy when built locally
     int32_t mode = -1;          // State::mode, cached when the state becomes valid
     bool fuse = true;           // config-5 fusion (wce_debug_set_fusion turns it off for A/B)
+    bool bdot = true;           // rank-1 C: second bordered row, no back-solve / GEMM (A/B switch)
     double *ws = nullptr;       // WCE_MMSE_FRAME_COV workspace: h | g | u | w, [ws_frames][64] complex each
     int64_t ws_frames = 0;
 };
@@ -261,6 +262,12 @@ static wce::SolveArgs solve_args(const wce_ctx *c, const wce_frames *in, wce_com
         a.cu = c->d_state->cvec;
         a.cw = nullptr;
         a.cs = 0;
+        a.hout = c->bdot;
+    } else if (c->mode == WCE_MMSE_REF && c->bdot) {   // C_ref = u w^T (a = 0: no Ryy build)
+        a.cu = c->d_state->cvec;
+        a.cw = c->d_state->cwvec;
+        a.cs = 0;
+        a.hout = 1;
     }
     a.tx = reinterpret_cast<const double *>(in->tx);
     a.rx = reinterpret_cast<const double *>(in->rx);
@@ -284,6 +291,10 @@ int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_s
     if (in->semantics != WCE_SEM_C)
         return fail(WCE_EINVAL, "wce_mmse_solve (profiling entry) takes C semantics; MATLAB runs via wce_estimate");
     wce::SolveArgs a = solve_args(c, in, W, w_stride);
+    if (a.hout) {   // the profiling pair solve -> apply keeps W = X z: rank-1 build only
+        a.hout = 0;
+        if (c->mode != WCE_MMSE_TEXTBOOK) a.cu = a.cw = nullptr;
+    }
     DeviceGuard g(c->device);
     rc = wce::launch_mmse_solve(c->d_state, a, stream);
     return rc ? fail(rc, "mmse_solve launch") : WCE_OK;
@@ -426,7 +437,7 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     double *aux = c->ws ? c->ws + (WS_ARRAYS - 1) * n * WS_LD * 2 : nullptr;
     if (split) {
         sa.split = 1;
-        if (fc) {
+        if (sa.hout) {
             sa.dots = aux;
         } else {
             sa.w = c->ws;
@@ -436,9 +447,9 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     rc = fuse ? wce::launch_mmse_solve_ls(c->d_state, sa, la, stream) : wce::launch_mmse_solve(c->d_state, sa, stream);
     if (rc) return fail(rc, "mmse_solve launch");
     double *H = reinterpret_cast<double *>(out->ps_mmse);
-    if (fc && split) rc = wce::launch_fc_finish(sa, aux, H, out->out_stride, stream);
+    if (sa.hout && split) rc = wce::launch_fc_finish(sa, aux, H, out->out_stride, stream);
     else if (split) rc = wce::launch_matvec_avg(c->d_state->C, c->ws, WS_LD, sa.nblk, H, out->out_stride, n, stream);
-    else if (!fc) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream);   // H = C W in place
+    else if (!sa.hout) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream);   // H = C W in place
     if (rc) return fail(rc, "mmse apply launch");
     return WCE_OK;
 }
@@ -494,6 +505,13 @@ int wce_plan_destroy(wce_plan *p)
     if (p->exec) (void)hipGraphExecDestroy(p->exec);
     if (p->graph) (void)hipGraphDestroy(p->graph);
     delete p;
+    return WCE_OK;
+}
+
+extern "C" int wce_debug_set_border_dot(wce_ctx *c, int on)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    c->bdot = on != 0;
     return WCE_OK;
 }
 

@@ -28,8 +28,9 @@ struct State {
     double Mg[CLD * CLD * 2];
     double Mu[CLD * CLD * 2];
     double Mw[CLD * CLD * 2];
-    double cvec[NPAD * 2];     // TEXTBOOK: C = c c' with c = F ifft(H_LT): the Ryy build
-                               // a X c c' X' needs one complex product per element
+    double cvec[NPAD * 2];     // rank-1 factors of the shared C = u w^T: u = cvec and
+    double cwvec[NPAD * 2];    // w = conj(cvec) (TEXTBOOK: c = F ifft(H_LT)) or w = cwvec
+                               // (REF: u = F g, w = FH^T q, main.c:186-203)
     double h_lt[NPAD * 2];     // LT_LS of the shared preamble (main.c:66-75)
     double tx_pre[NPAD * 2];   // shared tx preamble FFT
     double sinc[4][NPAD];      // sinc((k - P_p)/14) in double (utils.c:727-733)

@@ -355,7 +355,12 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 // not guaranteed: callers store lanes < 53 only).
 // FC: per-frame rank-1 covariance C_f = cu_f cw_f^T (SolveArgs::cu/cw, frame f)
 // instead of the shared State::C.
-template <bool FC>
+// DOT (rank-1 C = u w^T only): a second bordered row 54 = (w o x)^T rides in
+// the padding lanes of register row 6.  Eliminating pivots 0..52 then leaves
+// the Schur complement -w^T X Ryy^-1 rx in element (54, 53), so H = u s with
+// s = w^T X z needs neither the back-substitution nor the C W product; the
+// function returns s (wave-uniform) instead of x_lane z_lane.
+template <bool FC, bool DOT = false>
 __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
                                                int64_t base, int64_t f)
 {
@@ -433,6 +438,17 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
             for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
         }
+        if constexpr (DOT) {   // bordered row 54 = (w o x)^T; (54, 53) starts at 0 since x_53 = 0
+            const bool act = lane < NSC;
+            const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+            const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+            s.blk[lane] = cmul(wf, s.x[lane]);
+            wave_lds_sync();
+            if (p == NSC + 1 - 8 * (RB - 1)) {
+#pragma unroll
+                for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = s.blk[q + 8 * bb];
+            }
+        }
     }
     // pivot 0 and its column
     double r = rcp_nr(readlane_f64(A[0][0].x, 0));
@@ -446,6 +462,18 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     ldl_panel<5>(A, s, p, q, r);
     ldl_panel<6>(A, s, p, q, r);
     wave_lds_sync();
+    if constexpr (DOT) {
+        // the last step (pivot 52) updates no trailing element: apply its
+        // rank-1 term to (54, 53) here.  Lanes of register block (6, 6):
+        // (54, 53) = 53, (54, 52) = 52, (53, 52) = 44; r = r_52.
+        constexpr int R54 = 8 * (NSC + 1 - 8 * (RB - 1)), R53 = 8 * (NSC - 8 * (RB - 1)), C52 = NSC - 1 - 8 * (RB - 1);
+        const double2 e = readlane_c(A[RB - 1][RB - 1], R54 + C52 + 1);
+        const double2 l54 = readlane_c(A[RB - 1][RB - 1], R54 + C52);
+        const double2 l53 = readlane_c(A[RB - 1][RB - 1], R53 + C52);
+        double2 t = e;
+        cmsub_conj(t, cscale(l54, r), l53);
+        return make_double2(-t.x, -t.y);   // s = -S(54, 53)
+    }
     // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
     double rq[RB];
 #pragma unroll
@@ -503,14 +531,9 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     const int lane = threadIdx.x;
     const bool act = lane < NSC;
     const int k = act ? lane : 0;
-    const double2 wz = solve_block<R1>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
-    if constexpr (HOUT) {
-        const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
-        const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
-        double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
-        if (act) st2(a.w, f * a.ws + lane, cmul(uf, t));
+    const double2 wz = solve_block<R1, HOUT>(st, a, s, f * a.fs + (int64_t)a.blk * a.bs, f);
+    if constexpr (HOUT) {   // wz = s = w^T X z: H = u s
+        if (act) st2(a.w, f * a.ws + lane, cmul(ld2(a.cu, f * a.cs + lane), wz));
     } else {
         if (act) st2(a.w, f * a.ws + lane, wz);
     }
@@ -528,10 +551,11 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     if (act) ls_store<EQ>(l, f, k, mask, hlt, hlin, hcub, hsnc);
 }
 
-// Per-frame covariance (WCE_MMSE_FRAME_COV): C_f = u_f w_f^T, so the product
-// C_f W_f collapses to u_f (w_f . W_f): a wave reduction replaces the MFMA
-// apply, and the kernel writes H directly.  split (MATLAB): one wave per
-// (frame, block) writes its w_f . W_b to dots[g]; fc_finish averages.
+// Rank-1 covariance (TEXTBOOK / REF shared factors, or WCE_MMSE_FRAME_COV per
+// frame): C_f = u_f w_f^T, so H = u_f s with s = w_f^T X z from the second
+// bordered row (solve_block<., DOT>) -- no back-substitution, no C W GEMM.
+// split (MATLAB): one wave per (frame, block) writes its s_b to dots[g];
+// fc_finish averages.
 __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_kernel(const State *__restrict__ st,
                                                                                     SolveArgs a)
 {
@@ -541,17 +565,11 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_ke
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
     if (f >= a.n) return;
     const int lane = threadIdx.x;
-    const bool act = lane < NSC;
-    const double2 wz = solve_block<true>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
-    const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
-    const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
-    double2 t = act ? cmul(wf, wz) : make_double2(0, 0);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
+    const double2 sd = solve_block<true, true>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
     if (a.split) {
-        if (lane == 0) st2(a.dots, g, t);
-    } else if (act) {
-        st2(a.w, f * a.ws + lane, cmul(uf, t));
+        if (lane == 0) st2(a.dots, g, sd);
+    } else if (lane < NSC) {
+        st2(a.w, f * a.ws + lane, cmul(ld2(a.cu, f * a.cs + lane), sd));
     }
 }
 

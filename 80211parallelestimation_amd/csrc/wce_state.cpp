@@ -172,6 +172,18 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
                 Rhh[r * n + c] = g[r] * mk((long double)(creal_d(g[c]) - cimag_d(g[c])), 0.0L);
         mat_mul(Rhh.data(), n, n, FH.data(), n, t1.data());            // main.c:191
         mat_mul(F.data(), n, n, t1.data(), n, C.data());               // main.c:203 (F*Rhy, X4 applied per frame)
+        // the same C as rank-1 factors: C = (F g)(FH^T q)^T
+        for (int i = 0; i < n; i++) {
+            cld ui = mk(0, 0), wi = mk(0, 0);
+            for (int c = 0; c < n; c++) {
+                ui = ui + F[i * n + c] * g[c];
+                wi = wi + FH[c * n + i] * mk((long double)(creal_d(g[c]) - cimag_d(g[c])), 0.0L);
+            }
+            st->cvec[2 * i] = (double)__real__ ui;
+            st->cvec[2 * i + 1] = (double)__imag__ ui;
+            st->cwvec[2 * i] = (double)__real__ wi;
+            st->cwvec[2 * i + 1] = (double)__imag__ wi;
+        }
         st->acoef = 0.0;                 // addition() returns Id+Id (utils.c:117): Ryy = 2 ow2 I
         st->bcoef = 2.0 * ow2;
         st->xmask = (1ull << WCE_P0) | (1ull << WCE_P1) | (1ull << WCE_P2) | (1ull << WCE_P3);

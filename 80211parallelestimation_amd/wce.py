@@ -96,6 +96,7 @@ ABI = {
     "wce_ctx_create_cov": [POINTER(c_void_p), c_int, c_void_p, c_void_p, c_void_p, c_double],
     "wce_state_build_cov": [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_double],
     "wce_debug_set_fusion": [c_void_p, c_int],
+    "wce_debug_set_border_dot": [c_void_p, c_int],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
@@ -255,6 +256,10 @@ class Context:
     def plan(self, frames: "Frames", outputs: "Outputs", mask: int) -> "Plan":
         """Capture one estimate call into a HIP graph (wce_plan_create)."""
         return Plan(self, frames, outputs, mask)
+
+    def set_border_dot(self, on: bool):
+        """A/B switch: rank-1 covariance via a second bordered row (default on)."""
+        _check(_lib.wce_debug_set_border_dot(self.handle, int(bool(on))), "wce_debug_set_border_dot")
 
     def reserve(self, n_frames):
         """Pre-size the WCE_MMSE_FRAME_COV workspace (no allocation inside estimate)."""

@@ -15,6 +15,10 @@ int wce_debug_build_state(const double *tx_pre, const double *rx_pre, double ow2
  * solve's epilogue); on by default.  ctx is a wce_ctx* (include/wce.h). */
 struct wce_ctx;
 int wce_debug_set_fusion(struct wce_ctx *ctx, int on);
+/* A/B switch for the rank-1 path (TEXTBOOK / REF / FRAME_COV): a second
+ * bordered row replaces the back-substitution and the C W product; on by
+ * default.  Off: back-substitution + MFMA apply (shared modes). */
+int wce_debug_set_border_dot(struct wce_ctx *ctx, int on);
 #ifdef __cplusplus
 }
 #endif

@@ -397,3 +397,26 @@ def test_plan_graph_replay_matches_estimate(gpu_wce, golden, mask_name):
     plan.close()
     with pytest.raises(gpu_wce.WceError):   # invalid calls fail at creation, nothing captured
         ctx.plan(ctx.frames(tx, rx, B, block=99), o, mask)
+
+
+@pytest.mark.parametrize("mode", ["ref", "textbook"])
+@pytest.mark.parametrize("sem", ["c", "matlab"])
+def test_border_dot_matches_backsolve_path(gpu_wce, golden, mode, sem):
+    """Rank-1 covariance: the second bordered row (s = w^T X z from the Schur
+    complement, H = u s) reproduces back-substitution + C W on the MFMA."""
+    inp = golden["inputs"]
+    m = gpu_wce.MMSE_REF if mode == "ref" else gpu_wce.MMSE_TEXTBOOK
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m)
+    hlt = ctx.shared()[0]
+    B = 1000
+    tx, rx, pre = _synth(ctx, gpu_wce, B, seed=41, h_shared=hlt, rx_pre=True)
+    txh, rxh, preh = tx.numpy(), rx.numpy(), pre.numpy()
+    semantics = gpu_wce.SEM_C if sem == "c" else gpu_wce.SEM_MATLAB
+    res = []
+    for on in (True, False):
+        ctx.set_border_dot(on)
+        res.append(ctx.estimate_host(txh, rxh, rx_pre=preh, mask=gpu_wce.ALL, semantics=semantics))
+    ctx.set_border_dot(True)
+    assert normrel(res[0]["ps_mmse"], res[1]["ps_mmse"]).max() < 1e-11
+    for name in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc"):
+        assert np.array_equal(res[0][name], res[1][name]), name
