@@ -1,17 +1,26 @@
 // wce_kernels.hip -- gfx950 (CDNA4) kernels of the 802.11 channel-estimation
 // engine.  Written for wave64 / MI355X only.
 //
-//   ls_kernel          LT_LS + PS_Linear/Cubic/Sinc + equalization,
-//                      one wave per frame, HBM streaming (main.c:66-146,
-//                      WiFi_Equalization.m).
-//   mmse_solve_kernel  per-frame Ryy = a X C X' + b I, Cholesky with the rx
-//                      vector bordered on as row 53 (forward solve for free),
-//                      blocked back-substitution; the 54x54 lower triangle
-//                      lives in registers on an 8x8 lane grid (block-cyclic),
-//                      LDS only carries the pivot column broadcast.
-//                      (main.c:148-212 / WiFi_channel_estimation_PS_MMSE.m)
-//   mmse_apply_kernel  H = C W for 16-frame tiles on v_mfma_f64_16x16x4_f64.
-//   synth_kernel       counter-RNG synthetic frames (bench / tests).
+//   ls_kernel             LT_LS + PS_Linear/Cubic/Sinc + equalization, one
+//                         wave per frame, HBM streaming (main.c:66-146,
+//                         WiFi_Equalization.m); C or MATLAB semantics.
+//   solve_block           the per-frame MMSE core: Ryy = a X C X' + b I built
+//                         in registers (8x8 lane grid, block-cyclic 28 blocks),
+//                         square-root-free LDL' with conj(rx) bordered on as
+//                         row 53 (forward solve for free), LDS only for the
+//                         pivot-column broadcast (main.c:148-212 /
+//                         WiFi_channel_estimation_PS_MMSE.m).  Two read-outs:
+//   mmse_solve_fc_kernel    rank-1 C = u w^T (REF, TEXTBOOK, per-frame C): a
+//                           second bordered row (w o x)^T leaves s = w^T X z in
+//                           the Schur complement; H = u s, one launch.
+//   mmse_solve_kernel       dense C (COV): blocked back-substitution, W = X z;
+//   matvec_kernel           then H = C W on v_mfma_f64_16x16x4_f64 (also the
+//                           per-frame covariance factors, MATLAB block mean).
+//   mmse_solve_ls_kernel  config 5: either solve with the LS family and
+//                         equalization of the same frame in its epilogue.
+//   fc_finish_kernel      MATLAB averaging of the per-block s values.
+//   synth_kernel          counter-RNG synthetic frames (bench / tests).
+// The time-domain front end is in wce_front.hip.
 #include <hip/hip_runtime.h>
 #include "wce_internal.h"
 #include "wce_device.h"
