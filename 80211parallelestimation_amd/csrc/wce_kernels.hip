@@ -400,6 +400,17 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
         s.rd[lane] = 0.0;
     }
     wave_lds_sync();
+    if constexpr (DOT) {
+        if (ac == 0.0) {   // REF (main.c): Ryy = 2 ow2 I is diagonal, z = rx / b -- no factorisation
+            const bool act = lane < NSC;
+            const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+            const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+            double2 t = act ? cmul(cmul(wf, s.x[lane]), s.rx[lane]) : make_double2(0, 0);
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
+            return cscale(t, 1.0 / bc);   // s = w^T X rx / b
+        }
+    }
     {
         if (FC && ac != 0.0) {   // a X u w^T X': both factors staged in the pivot buffers
             const bool act = lane < NSC;
