@@ -525,8 +525,9 @@ def cpu_baseline(ctx, tx, rx, B, mode, budget_s):
         t_tot += t
     frames = reps * m
     return {"value": frames / t_tot, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"{frames} frames ({m} distinct bench frames x {reps}), same unified MMSE algorithm in fp64, "
-                      f"OpenMP over frames, {t_tot:.2f} s wall",
+            "sample": f"{frames} frames ({m} distinct bench frames x {reps}): the unified dense MMSE in fp64 "
+                      f"(LDL^H + back-substitution + C w, the GPU's dense-C path), OpenMP over frames, "
+                      f"{t_tot:.2f} s wall",
             "reference_main_c_seconds_per_frame": 232.6,
             "reference_note": "main.c PS_MMSE itself: ~200-233 s/frame on 1 core, output NaN (SURVEY 0-1); "
                               "its OpenMP path segfaults"}
