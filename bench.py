@@ -126,14 +126,14 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def pmc_traffic(kernel: str, launches_frames: int):
+def pmc_traffic(kernel: str, launches_frames: int, which: str = "pmc_summary"):
     """HBM bytes per launch of `kernel` (a substring of the demangled name,
     e.g. "mmse_solve_kernel<true>") from the committed rocprofv3 PMC summary
     (profiles/*_pmc_summary.json, tools/pmc_passes.sh): FETCH_SIZE (KiB, x2
     for gfx950's half-counted 16-B/lane streaming reads, MI355X_MICROARCH.md
     HBM) + WRITE_SIZE (KiB).  The summary was taken at 65,536 frames per launch."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{which}.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -229,7 +229,7 @@ def main():
         fl_alg = FLOP_SOLVE_TXT + FLOP_APPLY if mode == wce.MMSE_TEXTBOOK else FLOP_SOLVE_REF + FLOP_APPLY
         ach = fl_alg * B / (t_step * 1e-3) / 1e12
         kname = "mmse_solve_fc_kernel"
-        traffic, tsrc = pmc_traffic(kname, B)
+        traffic, tsrc = pmc_traffic(kname, B, "pmc_headline")
         res["roofline"] = {"bound": "mfma", "kernel": f"{kname} (fp64 VALU LDL^H, bordered by conj(rx) and (w o x)^T)",
                            "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                            "frac": ach / PEAK_FP64_TFLOPS, "traffic": traffic,

@@ -8,7 +8,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
 d = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_bench.json")))
-pm = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_pmc_summary.json")))
+pm = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_pmc_headline.json")))
 r = d["roofline"]
 refc = d["cpu_baseline"].get("reference_code", {})
 table = f"""| Quantity | Value |
@@ -37,7 +37,7 @@ if k:
     v = {c: x / 65536 for c, x in pm[k[0]].items()}
     busy = 3 * v["SQ_ACTIVE_INST_VALU"] / v["SQ_WAVE_CYCLES"]
     traffic = (2 * pm[k[0]]["FETCH_SIZE"] + pm[k[0]]["WRITE_SIZE"]) * 1024 / 1e6
-    pmc = f"""**PMC**, `mmse_solve_fc_kernel`, per frame (= per wave), averaged over the bench's launches of it. Source: `profiles/{rnd}_pmc_summary.json`, collected with `tools/refresh_profiles.sh`, one pass per counter group.
+    pmc = f"""**PMC**, `mmse_solve_fc_kernel`, headline run only (TEXTBOOK), per frame (= per wave). Source: `profiles/{rnd}_pmc_headline.json`, collected with `tools/refresh_profiles.sh`, one pass per counter group.
 - {v['SQ_INSTS_VALU']:,.0f} VALU instructions, of which {v['SQ_INSTS_VALU_FMA_F64']:,.0f} are `FMA_F64` and {v['SQ_INSTS_VALU_MUL_F64']:,.0f} `MUL_F64`.
 - {v['SQ_INSTS_LDS']:,.0f} LDS instructions with {v['SQ_LDS_BANK_CONFLICT']:.0f} bank conflicts.
 - VALU active {v['SQ_ACTIVE_INST_VALU']:,.0f} of {v['SQ_WAVE_CYCLES']:,.0f} quad-cycles per wave. Over 3 co-resident waves that is ≈{100 * busy:.0f}% of SIMD time.

@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/pmc
+OUT=$ROOT/gpurun_out/${PMC_DIR:-pmc}
 mkdir -p "$OUT"
 # PMC_EXTRAS=1: profile every bench leg (LS, front end, config 5, ...), not just the headline
 EXTRAS=--no-extras
