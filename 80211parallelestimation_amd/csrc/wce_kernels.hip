@@ -148,7 +148,13 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
 // blocks 0..3 -- Linear/Cubic/Sinc are linear in the pilot values, so the
 // 4-block average of the per-block estimates is the per-block formula applied
 // to the averaged pilots -- proper conj in LT_LS, cubic divisors 14/28/42.
-template <bool EQ, bool ML>
+#ifndef WCE_LS_NO_LIGHT   // A/B: route config 2 through the generic LS kernel
+#define WCE_LS_NO_LIGHT 0
+#endif
+// LIGHT: the request is a subset of LT_LS | PS_Linear (BASELINE configs[1]);
+// the Cubic/Sinc constants and paths compile out, which keeps the kernel under
+// 128 VGPRs (4 waves/SIMD: twice the loads in flight of the generic kernel).
+template <bool EQ, bool ML, bool LIGHT = false>
 __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
     const bool act = lane < NSC;
     const int k = act ? lane : 0;
     const LsLane c = ls_lane(st, a.tx_pre, k);
-    const uint32_t mask = a.mask;
+    const uint32_t mask = LIGHT ? (a.mask & (WCE_EST_LT_LS | WCE_EST_PS_LINEAR)) : a.mask;
     const bool need_lt = (mask & (WCE_EST_LT_LS | WCE_EQUALIZE)) != 0;
     const bool need_ps = (mask & (WCE_EST_PS_LINEAR | WCE_EST_PS_CUBIC | WCE_EST_PS_SINC | WCE_EQUALIZE)) != 0;
     const int pp = lane & 3;
@@ -221,13 +227,20 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 // =====================================================================
 constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
 
+constexpr int CVS = 9;    // row stride (complex) of the panel transpose buffer: conflict-free b128 rows
+
 struct SolveLds {
     double2 u[2][64];     // pivot column k (unscaled A[:, k]) ping-pong
     double2 x[64];        // masked tx of the frame (diagonal of X), 0 past 53
     double2 rx[64];
-    double2 blk[64];      // diagonal 8x8 block of u during back-substitution
-    double2 z[64];        // solution
-    double rd[64];        // r_k = 1 / d_k, 0 past 52
+    union {
+        struct {
+            double2 blk[64];  // diagonal 8x8 block of u during back-substitution
+            double2 z[64];    // solution
+            double rd[64];    // r_k = 1 / d_k, 0 past 52
+        };
+        double2 conv[56 * CVS];   // row-per-lane panels: block column -> rows (dot_panel)
+    };
 };
 
 __device__ __forceinline__ double rcp_nr(double d)
@@ -262,9 +275,22 @@ __device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double
 
 // Publish column k (unscaled) from the lanes that own it (q == kq).  Only
 // stores sit under the branch: no register is redefined in it.
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+#ifndef WCE_ABLATE_PUBLISH   // timing-only build: no pivot-column stores after pivot 0
+#define WCE_ABLATE_PUBLISH 0
+#endif
 template <int KB>
 __device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 *buf, int p, int q, int kq)
 {
+    if (WCE_ABLATE_PUBLISH == 1 && KB + kq > 0) return;
+    if (WCE_ABLATE_PUBLISH == 2 && KB + kq > 0) {   // one masked store per step
+        if (q == kq) buf[p + 8 * KB] = A[KB][KB];
+        return;
+    }
+    if (WCE_ABLATE_PUBLISH == 3 && KB + kq > 0) {   // one full-wave store per step
+        buf[lane_id() & 63] = A[KB][KB];
+        return;
+    }
     if (q == kq) {
 #pragma unroll
         for (int aa = KB; aa < RB; ++aa) buf[p + 8 * aa] = A[aa][KB];
@@ -311,6 +337,70 @@ __device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int
     for (int kq = 0; kq < NK - 1; ++kq) ldl_step<KB, true>(A, s, p, q, r, rsel, kq);
     ldl_step<KB, false>(A, s, p, q, r, rsel, NK - 1);
     if (p == 0 && q < NK) s.rd[8 * KB + q] = rsel;   // one store per panel
+}
+
+// ---------------------------------------------------------------------
+// Row-per-lane panels (the rank-1 read-out path, DOT).  Publishing pivot
+// column k+1 from the block-cyclic grid takes 7 - KB masked ds_write_b128 per
+// step (8 owner lanes each), and those stores, not the FMAs, set the pace:
+// with one store per step the same kernel runs 1.9x faster (A/B,
+// profiles/r01_ab_publish.txt).  So panel KB (block column KB = columns
+// 8KB .. 8KB+7, every row) is held transposed: lane l holds P[c] = A[l][8KB+c].
+// Column k+1 is then ONE register across the wave and goes out in one
+// full-wave store.  In-panel updates P[c] -= (r_k P[kq]) conj(A[8KB+c][k])
+// take the wave-uniform operand from the published column (LDS broadcast);
+// the trailing blocks aa >= bb > KB stay block-cyclic as before.  At a panel's
+// last step block column KB+1 is updated, written once to LDS by all lanes and
+// read back transposed (6 - KB stores + 8 reads per panel).
+// ---------------------------------------------------------------------
+template <int KB>
+__device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q,
+                                        int lane)
+{
+#pragma unroll
+    for (int aa = KB; aa < RB; ++aa) s.conv[(p + 8 * aa) * CVS + q] = A[aa][KB];
+    wave_lds_sync();
+    const int l = lane < 56 ? lane : 55;   // lanes 56..63 carry a copy of row 55 (never read)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) P[c] = s.conv[l * CVS + c];
+}
+
+template <int KB>
+__device__ __forceinline__ void dot_panel(double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q, int lane,
+                                          double &r)
+{
+    static_assert(KB + 1 < RB, "the last block column runs ldl_panel");
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) {
+        const int k = 8 * KB + kq;
+        const double2 *col = s.u[k & 1];
+        double2 *next = s.u[(k + 1) & 1];
+        const double rk = r;
+        double2 Ur[RB];
+#pragma unroll
+        for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
+        if (kq < 7) {
+            const double2 t = cscale(P[kq], rk);
+            cmsub_conj(P[kq + 1], t, col[8 * KB + kq + 1]);   // lookahead: column k+1
+            r = rcp_nr(readlane_f64(P[kq + 1].x, k + 1));
+            next[lane] = P[kq + 1];                           // publish: one store
+#pragma unroll
+            for (int c = kq + 2; c < 8; ++c) cmsub_conj(P[c], t, col[8 * KB + c]);
+            upd_cols_from<KB + 1>(A, Ur, col, q, rk);
+        } else {
+            upd_col<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
+            if constexpr (KB + 2 < RB) {
+                to_rows<KB + 1>(A, P, s, p, q, lane);
+                r = rcp_nr(readlane_f64(P[0].x, k + 1));
+                next[lane] = P[0];
+            } else {   // block column 6 stays block-cyclic (ldl_panel<6>)
+                r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
+                publish_col<KB + 1>(A, next, p, q, 0);
+            }
+            upd_cols_from<KB + 2>(A, Ur, col, q, rk);
+        }
+        wave_lds_sync();
+    }
 }
 
 // Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
@@ -369,6 +459,86 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 // the Schur complement -w^T X Ryy^-1 rx in element (54, 53), so H = u s with
 // s = w^T X z needs neither the back-substitution nor the C W product; the
 // function returns s (wave-uniform) instead of x_lane z_lane.
+#ifndef WCE_DOT_CYCLIC   // A/B: the rank-1 read-out on the all-block-cyclic factorisation
+#define WCE_DOT_CYCLIC 0
+#endif
+// The rank-1 read-out path (a != 0): Ryy = a (x o u)(w o x')^T + b I bordered
+// by conj(rx) (row 53) and (w o x)^T (row 54), factorised with row-per-lane
+// panels 0..5 (dot_panel) and the block-cyclic last panel; returns
+// s = -S(54, 53) = w^T X Ryy^-1 rx.
+__device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
+                                              int64_t f, double ac, double bc)
+{
+    const int lane = threadIdx.x;
+    const int p = lane >> 3, q = lane & 7;
+    {
+        const bool act = lane < NSC;
+        const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+        const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+        const double2 xl = s.x[lane];
+        s.u[0][lane] = cscale(cmul(xl, uf), ac);
+        s.u[1][lane] = cmul(wf, cconj(xl));
+        s.blk[lane] = cmul(wf, xl);
+    }
+    wave_lds_sync();
+    double2 A[RB][RB];
+    double2 P[8];
+    {   // panel 0 in rows: P[c] = a x_l u_l w_c conj(x_c) + b [l == c]
+        const double2 ul = s.u[0][lane];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            P[c] = cmul(ul, s.u[1][c]);
+            P[c].x += (lane == c) ? bc : 0.0;
+        }
+        if (lane == NSC) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) P[c] = cconj(s.rx[c]);
+        }
+        if (lane == NSC + 1) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) P[c] = s.blk[c];
+        }
+    }
+    // trailing blocks aa >= bb >= 1, block-cyclic
+#pragma unroll
+    for (int aa = 1; aa < RB; ++aa)
+#pragma unroll
+        for (int bb = 1; bb <= aa; ++bb) A[aa][bb] = cmul(s.u[0][p + 8 * aa], s.u[1][q + 8 * bb]);
+    const double bdiag = (p == q) ? bc : 0.0;
+#pragma unroll
+    for (int aa = 1; aa < RB - 1; ++aa) A[aa][aa].x += bdiag;
+    A[RB - 1][RB - 1].x += (p == q && p < NSC - 8 * (RB - 1)) ? bc : 0.0;
+    if (p == NSC - 8 * (RB - 1)) {   // row 53 = conj(rx)
+#pragma unroll
+        for (int bb = 1; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
+    }
+    if (p == NSC + 1 - 8 * (RB - 1)) {   // row 54 = (w o x)^T
+#pragma unroll
+        for (int bb = 1; bb < RB; ++bb) A[RB - 1][bb] = s.blk[q + 8 * bb];
+    }
+    wave_lds_sync();   // s.u[0] is reused by the first publish
+    double r = rcp_nr(readlane_f64(P[0].x, 0));
+    s.u[0][lane] = P[0];
+    wave_lds_sync();
+    dot_panel<0>(A, P, s, p, q, lane, r);
+    dot_panel<1>(A, P, s, p, q, lane, r);
+    dot_panel<2>(A, P, s, p, q, lane, r);
+    dot_panel<3>(A, P, s, p, q, lane, r);
+    dot_panel<4>(A, P, s, p, q, lane, r);
+    dot_panel<5>(A, P, s, p, q, lane, r);
+    ldl_panel<6>(A, s, p, q, r);
+    // the last step (pivot 52) updates no trailing element: apply its rank-1
+    // term to (54, 53) here.  Lanes of register block (6, 6): (54, 53) = 53,
+    // (54, 52) = 52, (53, 52) = 44; r = r_52.
+    constexpr int R54 = 8 * (NSC + 1 - 8 * (RB - 1)), R53 = 8 * (NSC - 8 * (RB - 1)), C52 = NSC - 1 - 8 * (RB - 1);
+    const double2 e = readlane_c(A[RB - 1][RB - 1], R54 + C52 + 1);
+    const double2 l54 = readlane_c(A[RB - 1][RB - 1], R54 + C52);
+    const double2 l53 = readlane_c(A[RB - 1][RB - 1], R53 + C52);
+    double2 t = e;
+    cmsub_conj(t, cscale(l54, r), l53);
+    return make_double2(-t.x, -t.y);   // s = -S(54, 53)
+}
+
 template <bool FC, bool DOT = false>
 __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
                                                int64_t base, int64_t f)
@@ -410,6 +580,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
             for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
             return cscale(t, 1.0 / bc);   // s = w^T X rx / b
         }
+        if (!WCE_DOT_CYCLIC) return dot_factor(st, a, s, f, ac, bc);
     }
     {
         if (FC && ac != 0.0) {   // a X u w^T X': both factors staged in the pivot buffers
@@ -757,12 +928,16 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
     if (blocks > 256 * 8) blocks = 256 * 8;      // grid-stride the rest
     const bool eq = (a.mask & WCE_EQUALIZE) && a.eq;
     const dim3 g((unsigned)blocks), b(256);
+    const bool light = !WCE_LS_NO_LIGHT && !eq && (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0;
+    hipStream_t s = (hipStream_t)stream;
     if (a.matlab) {
-        if (eq) hipLaunchKernelGGL((ls_kernel<true, true>), g, b, 0, (hipStream_t)stream, st, a);
-        else hipLaunchKernelGGL((ls_kernel<false, true>), g, b, 0, (hipStream_t)stream, st, a);
+        if (eq) hipLaunchKernelGGL((ls_kernel<true, true>), g, b, 0, s, st, a);
+        else if (light) hipLaunchKernelGGL((ls_kernel<false, true, true>), g, b, 0, s, st, a);
+        else hipLaunchKernelGGL((ls_kernel<false, true>), g, b, 0, s, st, a);
     } else {
-        if (eq) hipLaunchKernelGGL((ls_kernel<true, false>), g, b, 0, (hipStream_t)stream, st, a);
-        else hipLaunchKernelGGL((ls_kernel<false, false>), g, b, 0, (hipStream_t)stream, st, a);
+        if (eq) hipLaunchKernelGGL((ls_kernel<true, false>), g, b, 0, s, st, a);
+        else if (light) hipLaunchKernelGGL((ls_kernel<false, false, true>), g, b, 0, s, st, a);
+        else hipLaunchKernelGGL((ls_kernel<false, false>), g, b, 0, s, st, a);
     }
     return hip_status(hipGetLastError());
 }

@@ -16,6 +16,8 @@ ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--frames", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--mode", type=int, default=1)
+ap.add_argument("--entry", choices=["solve", "estimate"], default="solve",
+                help="estimate: the headline wce_estimate(PS_MMSE) (rank-1 bordered-dot kernel)")
 args = ap.parse_args()
 
 mods = []
@@ -40,6 +42,9 @@ for name, m in mods:
     W = m.DeviceArray((B, N), zero=True)
     st = m.Stream()
     fr = ctx.frames(tx, rx, B)
+    if args.entry == "estimate":
+        outs = m.Outputs(None, None, None, None, W.addr, None, N, 0, 0, 0, 0)
+        ctx.mmse_solve = lambda fr, W, n, s, c=ctx, o=outs, mm=m: c.estimate(fr, o, mm.PS_MMSE, s)
     state.append((name, m, ctx, fr, W, st, tx, rx, hs))
 import time
 t0 = time.perf_counter()
