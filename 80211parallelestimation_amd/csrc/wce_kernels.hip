@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 // =====================================================================
 constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
 
-constexpr int CVS = 9;    // row stride (complex) of the panel transpose buffer: conflict-free b128 rows
+constexpr int CVS = 9;    // row stride (complex) of the panel transpose buffer
 
 struct SolveLds {
     double2 u[2][64];     // pivot column k (unscaled A[:, k]) ping-pong
@@ -242,6 +242,10 @@ struct SolveLds {
         double2 conv[56 * CVS];   // row-per-lane panels: block column -> rows (dot_panel)
     };
 };
+// conv element (row, c) at row * 9 + c: the odd row stride keeps both the
+// block-cyclic stores and the row reads bank-conflict free (an XOR swizzle of
+// an unpadded buffer measured 1% slower: address VALU).
+__device__ __forceinline__ int conv_idx(int row, int c) { return row * CVS + c; }
 
 __device__ __forceinline__ double rcp_nr(double d)
 {
@@ -342,9 +346,8 @@ __device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int
 // ---------------------------------------------------------------------
 // Row-per-lane panels (the rank-1 read-out path, DOT).  Publishing pivot
 // column k+1 from the block-cyclic grid takes 7 - KB masked ds_write_b128 per
-// step (8 owner lanes each), and those stores, not the FMAs, set the pace:
-// with one store per step the same kernel runs 1.9x faster (A/B,
-// profiles/r01_ab_publish.txt).  So panel KB (block column KB = columns
+// step (8 owner lanes each); an LDS store costs its issuing SIMD far more than
+// its 16 B suggest (profiles/r01_ab_publish.txt).  So panel KB (block column KB = columns
 // 8KB .. 8KB+7, every row) is held transposed: lane l holds P[c] = A[l][8KB+c].
 // Column k+1 is then ONE register across the wave and goes out in one
 // full-wave store.  In-panel updates P[c] -= (r_k P[kq]) conj(A[8KB+c][k])
@@ -358,18 +361,25 @@ __device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)
                                         int lane)
 {
 #pragma unroll
-    for (int aa = KB; aa < RB; ++aa) s.conv[(p + 8 * aa) * CVS + q] = A[aa][KB];
+    for (int aa = KB; aa < RB; ++aa) s.conv[conv_idx(p + 8 * aa, q)] = A[aa][KB];
     wave_lds_sync();
     const int l = lane < 56 ? lane : 55;   // lanes 56..63 carry a copy of row 55 (never read)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) P[c] = s.conv[l * CVS + c];
+    for (int c = 0; c < 8; ++c) P[c] = s.conv[conv_idx(l, c)];
 }
 
+#ifndef WCE_ROWP_PANELS   // panels 0 .. WCE_ROWP_PANELS-1 in row form; the rest block-cyclic
+#define WCE_ROWP_PANELS 6
+#endif
+constexpr int ROWP = WCE_ROWP_PANELS;
+static_assert(ROWP >= 1 && ROWP < RB, "the last block column runs ldl_panel");
+
+// Panel KB in row form.  Entering: P = block column KB, u_{8KB} published,
+// r = r_{8KB}.
 template <int KB>
 __device__ __forceinline__ void dot_panel(double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q, int lane,
                                           double &r)
 {
-    static_assert(KB + 1 < RB, "the last block column runs ldl_panel");
 #pragma unroll
     for (int kq = 0; kq < 8; ++kq) {
         const int k = 8 * KB + kq;
@@ -380,7 +390,7 @@ __device__ __forceinline__ void dot_panel(double2 (&A)[RB][RB], double2 (&P)[8],
 #pragma unroll
         for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
         if (kq < 7) {
-            const double2 t = cscale(P[kq], rk);
+            const double2 t = cscale(P[kq], rk);              // r_k u_k at this lane's row
             cmsub_conj(P[kq + 1], t, col[8 * KB + kq + 1]);   // lookahead: column k+1
             r = rcp_nr(readlane_f64(P[kq + 1].x, k + 1));
             next[lane] = P[kq + 1];                           // publish: one store
@@ -389,11 +399,11 @@ __device__ __forceinline__ void dot_panel(double2 (&A)[RB][RB], double2 (&P)[8],
             upd_cols_from<KB + 1>(A, Ur, col, q, rk);
         } else {
             upd_col<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
-            if constexpr (KB + 2 < RB) {
+            if constexpr (KB + 1 < ROWP) {
                 to_rows<KB + 1>(A, P, s, p, q, lane);
                 r = rcp_nr(readlane_f64(P[0].x, k + 1));
                 next[lane] = P[0];
-            } else {   // block column 6 stays block-cyclic (ldl_panel<6>)
+            } else {   // block column KB+1 on runs block-cyclic (ldl_panel)
                 r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
                 publish_col<KB + 1>(A, next, p, q, 0);
             }
@@ -521,11 +531,11 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     s.u[0][lane] = P[0];
     wave_lds_sync();
     dot_panel<0>(A, P, s, p, q, lane, r);
-    dot_panel<1>(A, P, s, p, q, lane, r);
-    dot_panel<2>(A, P, s, p, q, lane, r);
-    dot_panel<3>(A, P, s, p, q, lane, r);
-    dot_panel<4>(A, P, s, p, q, lane, r);
-    dot_panel<5>(A, P, s, p, q, lane, r);
+    if constexpr (ROWP > 1) dot_panel<1>(A, P, s, p, q, lane, r); else ldl_panel<1>(A, s, p, q, r);
+    if constexpr (ROWP > 2) dot_panel<2>(A, P, s, p, q, lane, r); else ldl_panel<2>(A, s, p, q, r);
+    if constexpr (ROWP > 3) dot_panel<3>(A, P, s, p, q, lane, r); else ldl_panel<3>(A, s, p, q, r);
+    if constexpr (ROWP > 4) dot_panel<4>(A, P, s, p, q, lane, r); else ldl_panel<4>(A, s, p, q, r);
+    if constexpr (ROWP > 5) dot_panel<5>(A, P, s, p, q, lane, r); else ldl_panel<5>(A, s, p, q, r);
     ldl_panel<6>(A, s, p, q, r);
     // the last step (pivot 52) updates no trailing element: apply its rank-1
     // term to (54, 53) here.  Lanes of register block (6, 6): (54, 53) = 53,
@@ -534,9 +544,9 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     const double2 e = readlane_c(A[RB - 1][RB - 1], R54 + C52 + 1);
     const double2 l54 = readlane_c(A[RB - 1][RB - 1], R54 + C52);
     const double2 l53 = readlane_c(A[RB - 1][RB - 1], R53 + C52);
-    double2 t = e;
-    cmsub_conj(t, cscale(l54, r), l53);
-    return make_double2(-t.x, -t.y);   // s = -S(54, 53)
+    double2 sc = e;
+    cmsub_conj(sc, cscale(l54, r), l53);
+    return make_double2(-sc.x, -sc.y);   // s = -S(54, 53)
 }
 
 template <bool FC, bool DOT = false>
