@@ -256,6 +256,17 @@ __device__ __forceinline__ double rcp_nr(double d)
     return fma(r, e, r);
 }
 
+// 1/sqrt(d): v_rsq_f64 + 2 Newton steps y += y (1/2 - d y^2 / 2)
+__device__ __forceinline__ double rsq_nr(double d)
+{
+    double y = __builtin_amdgcn_rsq(d);
+    const double hd = 0.5 * d;
+    double e = fma(-hd * y, y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-hd * y, y, 0.5);
+    return fma(y, e, y);
+}
+
 // A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
 template <int BB>
 __device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v)
@@ -469,6 +480,87 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 // the Schur complement -w^T X Ryy^-1 rx in element (54, 53), so H = u s with
 // s = w^T X z needs neither the back-substitution nor the C W product; the
 // function returns s (wave-uniform) instead of x_lane z_lane.
+// ---------------------------------------------------------------------
+// Cholesky form of the row panels (default).  Publishing c_k = u_k / sqrt(d_k)
+// instead of u_k makes the rank-1 term symmetric, A -= c c^H: both operands
+// are read from the one published column as they are -- no per-block scaling
+// of the column operand (2 (6 - KB) MULs per step) and no r_k u_k for the
+// panel.  The price is 1/sqrt instead of 1/d (3 more VALU per step).
+// ---------------------------------------------------------------------
+template <int BB>
+__device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col, int q)
+{
+    if constexpr (BB < RB) {
+        upd_col<BB>(A, Ur, col[q + 8 * BB]);
+        upd_cols_chol<BB + 1>(A, Ur, col, q);
+    }
+}
+
+// Panel KB in row form.  Entering: P = block column KB with P[0] = c_{8KB}
+// (scaled), c_{8KB} published.
+template <int KB>
+__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q, int lane)
+{
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) {
+        const int k = 8 * KB + kq;
+        const double2 *col = s.u[k & 1];
+        double2 *next = s.u[(k + 1) & 1];
+        double2 Ur[RB];
+#pragma unroll
+        for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
+        if (kq < 7) {
+            cmsub_conj(P[kq + 1], P[kq], col[8 * KB + kq + 1]);   // lookahead: column k+1
+            const double rs = rsq_nr(readlane_f64(P[kq + 1].x, k + 1));
+            P[kq + 1] = cscale(P[kq + 1], rs);
+            next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
+#pragma unroll
+            for (int c = kq + 2; c < 8; ++c) cmsub_conj(P[c], P[kq], col[8 * KB + c]);
+            upd_cols_chol<KB + 1>(A, Ur, col, q);
+        } else {
+            upd_col<KB + 1>(A, Ur, col[q + 8 * (KB + 1)]);
+            if constexpr (KB + 2 < RB) {
+                to_rows<KB + 1>(A, P, s, p, q, lane);
+                const double rs = rsq_nr(readlane_f64(P[0].x, k + 1));
+                P[0] = cscale(P[0], rs);
+                next[lane] = P[0];
+            } else {   // block column 6 stays block-cyclic: the 8 owners of column 48 publish
+                const double rs = rsq_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
+                const double2 cs = cscale(A[KB + 1][KB + 1], rs);
+                if (q == 0) next[p + 8 * (KB + 1)] = cs;
+            }
+            upd_cols_chol<KB + 2>(A, Ur, col, q);
+        }
+        wave_lds_sync();
+    }
+}
+
+// Pivots 48..52 on register block (6, 6) and the read-out.  Eliminated
+// columns take unmasked updates (never read again); (54, 53) receives every
+// step, the last (pivot 52) straight from the published c_52.
+__device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, int p, int q)
+{
+    constexpr int B6 = 8 * (RB - 1);
+#pragma unroll
+    for (int kq = 0; kq < NSC - 1 - B6; ++kq) {
+        const int k = B6 + kq;
+        const double2 *col = s.u[k & 1];
+        double2 *next = s.u[(k + 1) & 1];
+        cmsub_conj(A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
+        const double rs = rsq_nr(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
+        const double2 cs = cscale(A[RB - 1][RB - 1], rs);
+        if (q == kq + 1) next[p + B6] = cs;
+        wave_lds_sync();
+    }
+    const double2 *col = s.u[(NSC - 1) & 1];   // c_52
+    double2 sc = readlane_c(A[RB - 1][RB - 1], 8 * (NSC + 1 - B6) + (NSC - B6));   // (54, 53)
+    cmsub_conj(sc, col[NSC + 1], col[NSC]);
+    return make_double2(-sc.x, -sc.y);   // s = -S(54, 53)
+}
+
+#ifndef WCE_DOT_CHOL   // A/B: 0 = square-root-free LDL^H row panels (dot_panel)
+#define WCE_DOT_CHOL 1
+#endif
 #ifndef WCE_DOT_CYCLIC   // A/B: the rank-1 read-out on the all-block-cyclic factorisation
 #define WCE_DOT_CYCLIC 0
 #endif
@@ -527,6 +619,19 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
         for (int bb = 1; bb < RB; ++bb) A[RB - 1][bb] = s.blk[q + 8 * bb];
     }
     wave_lds_sync();   // s.u[0] is reused by the first publish
+    if constexpr (WCE_DOT_CHOL) {
+        static_assert(!WCE_DOT_CHOL || ROWP == RB - 1, "Cholesky panels: 0..5 in row form");
+        P[0] = cscale(P[0], rsq_nr(readlane_f64(P[0].x, 0)));
+        s.u[0][lane] = P[0];
+        wave_lds_sync();
+        chol_panel<0>(A, P, s, p, q, lane);
+        chol_panel<1>(A, P, s, p, q, lane);
+        chol_panel<2>(A, P, s, p, q, lane);
+        chol_panel<3>(A, P, s, p, q, lane);
+        chol_panel<4>(A, P, s, p, q, lane);
+        chol_panel<5>(A, P, s, p, q, lane);
+        return chol_last(A, s, p, q);
+    }
     double r = rcp_nr(readlane_f64(P[0].x, 0));
     s.u[0][lane] = P[0];
     wave_lds_sync();
