@@ -256,15 +256,24 @@ __device__ __forceinline__ double rcp_nr(double d)
     return fma(r, e, r);
 }
 
-// 1/sqrt(d): v_rsq_f64 + 2 Newton steps y += y (1/2 - d y^2 / 2)
+#ifndef WCE_RSQ_NEWTON2   // A/B: two Newton steps instead of one third-order step
+#define WCE_RSQ_NEWTON2 0
+#endif
+// 1/sqrt(d) from v_rsq_f64 (relative error ~2^-24).  One third-order
+// (Householder) step y += y e (1/2 + 3e/8), e = 1 - d y^2: error ~2^-72
+// before rounding, 5 VALU on a 4-deep chain (two Newton steps: 7 on 6).
 __device__ __forceinline__ double rsq_nr(double d)
 {
     double y = __builtin_amdgcn_rsq(d);
-    const double hd = 0.5 * d;
-    double e = fma(-hd * y, y, 0.5);
-    y = fma(y, e, y);
-    e = fma(-hd * y, y, 0.5);
-    return fma(y, e, y);
+    if (WCE_RSQ_NEWTON2) {
+        const double hd = 0.5 * d;
+        double e = fma(-hd * y, y, 0.5);
+        y = fma(y, e, y);
+        e = fma(-hd * y, y, 0.5);
+        return fma(y, e, y);
+    }
+    const double e = fma(-d * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
 // A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
