@@ -14,6 +14,7 @@ ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--frames", type=int, default=1 << 20)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--mask", type=int, default=3)
+ap.add_argument("--ostride", type=int, default=53, help="output row stride (complex); 64 = 1 KiB-aligned rows")
 args = ap.parse_args()
 N = 53
 inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
@@ -37,8 +38,8 @@ for d in args.dirs:
         k = min(chunk, n - off)
         for dst, h in ((tx, txh), (rx, rxh), (pre, preh)):
             lib.wce_memcpy_htod(dst.addr + off * N * 16, h[:k].ctypes.data, k * N * 16)
-    outs = [m.DeviceArray((n, N)) for _ in range(4)]
-    o = m.Outputs(*(x.addr for x in outs), None, None, N, 0, 0, 0, 0)
+    outs = [m.DeviceArray((n, args.ostride)) for _ in range(4)]
+    o = m.Outputs(*(x.addr for x in outs), None, None, args.ostride, 0, 0, 0, 0)
     fr = ctx.frames(tx, rx, n, frame_stride=N, block_stride=N, rx_pre=pre, pre_stride=N)
     state.append((os.path.basename(d.rstrip("/")), m, ctx, fr, o, m.Stream(), (tx, rx, pre, outs)))
 res = {s[0]: [] for s in state}
