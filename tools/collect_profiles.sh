@@ -1,0 +1,13 @@
+#!/bin/bash
+# Copy what tools/refresh_profiles.sh left in gpurun_out/ into profiles/ under
+# this round's names.  usage: tools/collect_profiles.sh [r01]
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+RND=${1:-r01}
+G=$R/gpurun_out
+cp "$G/bench_full.json" "$R/profiles/${RND}_bench.json"
+cp "$G/stats/run_kernel_stats.csv" "$R/profiles/${RND}_kernel_stats.csv"
+[ -f "$G/stats_head/run_kernel_stats.csv" ] && cp "$G/stats_head/run_kernel_stats.csv" "$R/profiles/${RND}_kernel_stats_headline.csv"
+cp "$G/pmc_summary.json" "$R/profiles/${RND}_pmc_summary.json"
+cp "$G/pmc_headline.json" "$R/profiles/${RND}_pmc_headline.json"
+echo "collected into profiles/ as ${RND}_*"

@@ -5,7 +5,8 @@
 #      the same kernel) and over all bench legs (-> pmc_summary.json)
 #   2. the full bench line (reads the fresh PMC summary for "traffic")
 #   3. rocprofv3 --kernel-trace --stats of the same bench (kernel durations)
-# Results land in gpurun_out/; copy them into profiles/ with the round prefix.
+# Results land in gpurun_out/; copy them into profiles/ with the round prefix
+# (tools/collect_profiles.sh).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out"
@@ -20,4 +21,8 @@ timeout -k 10 400 python3 "$R/bench.py" > "$R/gpurun_out/bench_full.json" 2> "$R
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/stats" -o run \
     -- python3 "$R/bench.py" --no-cpu-baseline > "$R/gpurun_out/stats.log" 2>&1 || exit $?
+# headline only: the per-launch average of the headline kernel, undiluted by
+# the other modes' launches of the same kernel (REF mode, FRAME_COV)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/stats_head" -o run \
+    -- python3 "$R/bench.py" --no-extras --no-cpu-baseline > "$R/gpurun_out/stats_head.log" 2>&1 || exit $?
 echo "refresh done"
