@@ -216,21 +216,23 @@ def main():
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "prewarm_s": args.prewarm_s,
-           "config": {"workload": f"PS_MMSE {args.mode} (53x53 per-frame solve + MFMA C*W), BASELINE configs[2]",
+           "config": {"workload": f"PS_MMSE {args.mode} (53x53 per-frame Hermitian solve of Ryy = X C X' + ow2 I, bordered read-out H = u s), BASELINE configs[2]",
                       "frames_per_gpu": B, "global_frames": B * dist.world, "subcarriers": N, "ofdm_blocks": NBLK,
                       "parallelism": f"dp{dist.world} (frames sharded, 1 RCCL state broadcast)"}}
 
     if not args.no_extras:
         # Dominant kernel = the whole step: for the rank-1 covariances (TEXTBOOK,
-        # REF) one launch of mmse_solve_fc_kernel does the MMSE (LDL^H with two
-        # bordered rows, H = u s).  HIP events on the launch stream.
+        # REF) one launch of mmse_solve_fc_kernel does the MMSE (Cholesky with two
+        # bordered rows, H = u s).  HIP events on the launch stream.  "bound":
+        # "mfma" = the FP64 compute roofline (MI355X FP64 vector = matrix peak);
+        # this kernel runs on the FP64 VALU, the MFMA GEMM is the COV leg below.
         reps = max(5, args.steps)
         t_step = time_events(wce, stream, step, reps)
         fl_alg = FLOP_SOLVE_TXT + FLOP_APPLY if mode == wce.MMSE_TEXTBOOK else FLOP_SOLVE_REF + FLOP_APPLY
         ach = fl_alg * B / (t_step * 1e-3) / 1e12
         kname = "mmse_solve_fc_kernel"
         traffic, tsrc = pmc_traffic(kname, B, "pmc_headline")
-        res["roofline"] = {"bound": "mfma", "kernel": f"{kname} (fp64 VALU LDL^H, bordered by conj(rx) and (w o x)^T)",
+        res["roofline"] = {"bound": "mfma", "kernel": f"{kname} (fp64 VALU Cholesky, row-per-lane panels, bordered by conj(rx) and (w o x)^T)",
                            "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                            "frac": ach / PEAK_FP64_TFLOPS, "traffic": traffic,
                            "traffic_unit": "bytes/launch (FETCH_SIZEx2 + WRITE_SIZE)",
