@@ -14,9 +14,19 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b)
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 __device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+// 1/d: v_rcp_f64 (2^28 ulp) + 2 Newton steps -> correctly rounded in the
+// probe (profiles/r01_ubench_rcp.txt); 5 VALU against 11 for an IEEE divide
+__device__ __forceinline__ double rcp_nr(double d)
+{
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
 __device__ __forceinline__ double2 cdiv(double2 a, double2 b)
 {
-    const double inv = 1.0 / (b.x * b.x + b.y * b.y);
+    const double inv = rcp_nr(b.x * b.x + b.y * b.y);
     return make_double2((a.x * b.x + a.y * b.y) * inv, (a.y * b.x - a.x * b.y) * inv);
 }
 // acc -= l * conj(c)   (4 DFMA)

@@ -247,14 +247,6 @@ struct SolveLds {
 // an unpadded buffer measured 1% slower: address VALU).
 __device__ __forceinline__ int conv_idx(int row, int c) { return row * CVS + c; }
 
-__device__ __forceinline__ double rcp_nr(double d)
-{
-    double r = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    return fma(r, e, r);
-}
 
 #ifndef WCE_RSQ_NEWTON2   // A/B: two Newton steps instead of one third-order step
 #define WCE_RSQ_NEWTON2 0
@@ -858,8 +850,11 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     const double2 rp = l.rx_pre ? ld2(l.rx_pre, f * l.ps + k) : make_double2(0, 0);
     const LsLane c = ls_lane(st, l.tx_pre, k);
     // pilot LS from the frame data the solve staged in LDS (pilots are in X in both modes)
-    const double2 h0 = cdiv(s.rx[WCE_P0], s.x[WCE_P0]), h1 = cdiv(s.rx[WCE_P1], s.x[WCE_P1]);
-    const double2 h2 = cdiv(s.rx[WCE_P2], s.x[WCE_P2]), h3 = cdiv(s.rx[WCE_P3], s.x[WCE_P3]);
+    // lane j < 4 divides pilot j once; the four values are broadcast by readlane
+    const int pj = lane & 3;
+    const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
+    const double2 hp = cdiv(s.rx[pil], s.x[pil]);
+    const double2 h0 = readlane_c(hp, 0), h1 = readlane_c(hp, 1), h2 = readlane_c(hp, 2), h3 = readlane_c(hp, 3);
     const double2 hlt = lt_ls_lane<false>(c, l.rx_pre != nullptr, rp, k);
     double2 hlin, hcub, hsnc;
     ps_lane<false>(c, mask, h0, h1, h2, h3, hlin, hcub, hsnc);
