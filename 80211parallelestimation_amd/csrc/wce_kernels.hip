@@ -154,9 +154,17 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
 // LIGHT: the request is a subset of LT_LS | PS_Linear (BASELINE configs[1]);
 // the Cubic/Sinc constants and paths compile out, which keeps the kernel under
 // 128 VGPRs (4 waves/SIMD: twice the loads in flight of the generic kernel).
+#ifndef WCE_LS_PIPE   // LIGHT: loads of the next frame group issued before this group's math
+#define WCE_LS_PIPE 1
+#endif
+#ifndef WCE_LS_PIPE_FRAMES
+#define WCE_LS_PIPE_FRAMES 4
+#endif
 template <bool EQ, bool ML, bool LIGHT = false>
 __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
 {
+    constexpr bool PIPE = LIGHT && WCE_LS_PIPE;
+    constexpr int F = PIPE ? WCE_LS_PIPE_FRAMES : LS_FRAMES;   // frames per wave iteration
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * LS_WAVES;
     const bool act = lane < NSC;
@@ -172,12 +180,10 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
     const int64_t pil_off = ML ? (int64_t)(lane >> 2) * a.bs + pil : (int64_t)a.blk * a.bs + pil;
     const bool rx_pre = need_lt && a.rx_pre;
 
-    for (int64_t f0 = ((int64_t)blockIdx.x * LS_WAVES + (threadIdx.x >> 6)) * LS_FRAMES; f0 < a.n;
-         f0 += nw * LS_FRAMES) {
-        // ---- issue every load of LS_FRAMES frames before any use
-        double2 ptx[LS_FRAMES], prx[LS_FRAMES], rp[LS_FRAMES];
+    // every load of F frames, issued before any use
+    auto load = [&](int64_t f0, double2 (&ptx)[F], double2 (&prx)[F], double2 (&rp)[F]) {
 #pragma unroll
-        for (int u = 0; u < LS_FRAMES; ++u) {
+        for (int u = 0; u < F; ++u) {
             const int64_t f = f0 + u < a.n ? f0 + u : a.n - 1;
             ptx[u] = make_double2(1, 0);
             prx[u] = make_double2(0, 0);
@@ -187,8 +193,16 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
             }
             rp[u] = rx_pre ? ld2(a.rx_pre, f * a.ps + k) : make_double2(0, 0);
         }
+    };
+    const int64_t step = nw * F;
+    int64_t f0 = ((int64_t)blockIdx.x * LS_WAVES + (threadIdx.x >> 6)) * F;
+    double2 ptx[F], prx[F], rp[F];
+    if (f0 < a.n) load(f0, ptx, prx, rp);
+    for (; f0 < a.n; f0 += step) {
+        double2 ntx[F], nrx[F], nrp[F];
+        if (PIPE && f0 + step < a.n) load(f0 + step, ntx, nrx, nrp);   // in flight during this group's math
 #pragma unroll
-        for (int u = 0; u < LS_FRAMES; ++u) {
+        for (int u = 0; u < F; ++u) {
             const int64_t f = f0 + u;
             if (f >= a.n) break;
             double2 h0 = make_double2(0, 0), h1 = h0, h2 = h0, h3 = h0;
@@ -205,6 +219,12 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
             double2 hlin, hcub, hsnc;
             ps_lane<ML>(c, mask, h0, h1, h2, h3, hlin, hcub, hsnc);
             if (act) ls_store<EQ>(a, f, k, mask, hlt, hlin, hcub, hsnc);
+        }
+        if (PIPE) {
+#pragma unroll
+            for (int u = 0; u < F; ++u) { ptx[u] = ntx[u]; prx[u] = nrx[u]; rp[u] = nrp[u]; }
+        } else if (f0 + step < a.n) {
+            load(f0 + step, ptx, prx, rp);
         }
     }
 }
@@ -1042,7 +1062,7 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 int launch_ls(const State *st, const LsArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
-    const int64_t groups = (a.n + LS_FRAMES - 1) / LS_FRAMES;     // one wave per LS_FRAMES frames
+    const int64_t groups = (a.n + LS_FRAMES - 1) / LS_FRAMES;     // one wave per LS_FRAMES frames (grid-stride)
     int64_t blocks = (groups + LS_WAVES - 1) / LS_WAVES;
     if (blocks > 256 * 8) blocks = 256 * 8;      // grid-stride the rest
     const bool eq = (a.mask & WCE_EQUALIZE) && a.eq;
