@@ -420,3 +420,46 @@ def test_border_dot_matches_backsolve_path(gpu_wce, golden, mode, sem):
     assert normrel(res[0]["ps_mmse"], res[1]["ps_mmse"]).max() < 1e-11
     for name in ("lt_ls", "ps_linear", "ps_cubic", "ps_sinc"):
         assert np.array_equal(res[0][name], res[1][name]), name
+
+
+@pytest.mark.parametrize("sem", ["c", "matlab"])
+def test_ls_light_pipeline_batch_edges(gpu_wce, golden, sem):
+    """BASELINE configs[1] requests (LT_LS + PS_Linear) run the LIGHT,
+    software-pipelined ls_kernel (next frame group's loads in flight during
+    this group's math).  Batch sizes around the group (4 frames), the wave and
+    the grid-stride sweep (2,048 x 4 waves x 4 frames = 32,768 frames) must give
+    exactly what the generic kernel gives for the same two outputs (bit-identical:
+    same per-lane arithmetic), and match the oracle on sampled frames."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    Bmax = 2 * 32768 + 4 * 5 + 3
+    tx, rx, pre = _synth(ctx, gpu_wce, Bmax, seed=11, rx_pre=True)
+    txh, rxh, preh = tx.numpy(), rx.numpy(), pre.numpy()
+    semantics = gpu_wce.SEM_MATLAB if sem == "matlab" else gpu_wce.SEM_C
+    for B in (1, 3, 4, 5, 63, 4097, 32768, 32769, Bmax):
+        lt, lin = gpu_wce.DeviceArray((B, N), zero=True), gpu_wce.DeviceArray((B, N), zero=True)
+        lt2, lin2 = gpu_wce.DeviceArray((B, N), zero=True), gpu_wce.DeviceArray((B, N), zero=True)
+        cub = gpu_wce.DeviceArray((B, N), zero=True)
+        fr = ctx.frames(tx, rx, B, rx_pre=pre, semantics=semantics)
+        ctx.estimate(fr, gpu_wce.Outputs(lt.addr, lin.addr, None, None, None, None, N, 0, 0, 0, 0),
+                     gpu_wce.LT_LS | gpu_wce.PS_LINEAR)
+        ctx.estimate(fr, gpu_wce.Outputs(lt2.addr, lin2.addr, cub.addr, None, None, None, N, 0, 0, 0, 0),
+                     gpu_wce.LT_LS | gpu_wce.PS_LINEAR | gpu_wce.PS_CUBIC)   # generic kernel
+        gpu_wce.synchronize()
+        a, b = lt.numpy(), lin.numpy()
+        assert np.array_equal(a, lt2.numpy()) and np.array_equal(b, lin2.numpy()), B
+        for f in sorted({0, B - 1, B // 2}):
+            assert normrel(a[f], oracle_lt(inp, preh[f], sem)) < TOL_LS, (B, f)
+            if sem == "c":
+                from oracle_py import ps_linear
+                assert normrel(b[f], ps_linear(txh[f, 0], rxh[f, 0])) < TOL_LS, (B, f)
+
+
+def oracle_lt(inp, rp, sem):
+    from oracle_py import lt_ls
+    if sem == "c":
+        return lt_ls(inp["tx_pre"], rp)
+    t = inp["tx_pre"]   # WiFi_channel_estimation_LT_LS.m: conj(tx) rx / |tx|^2, DC = 0
+    h = np.conj(t) * rp / np.where(np.abs(t) > 0, np.abs(t) ** 2, 1.0)
+    h[26] = 0
+    return h
