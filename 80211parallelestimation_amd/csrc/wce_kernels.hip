@@ -230,6 +230,100 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 }
 
 // =====================================================================
+// LT_LS + PS_Linear, C semantics (BASELINE configs[1]) over the flat element
+// index e = f * 53 + k of a frame range.  Every lane of every load and store
+// instruction carries one (frame, subcarrier) element, so that 64-lane
+// instructions stream 1 KiB with no idle lanes 53..63.  The kernel is
+// latency-bound (its two input streams do not overlap, r01_ab_ls.txt):
+// what it needs is bytes in flight, and ~60 VGPRs give 8 waves/SIMD where
+// the per-frame kernel holds 2.  A wave-chunk is 512 elements (<= 11 frames).
+// Its pilot LS values (4 per frame, one division each on lanes 4j+p) go
+// through a per-wave LDS table.  The arithmetic is ls_kernel's: outputs are
+// bit-identical.
+// =====================================================================
+#ifndef WCE_LS_FLAT   // A/B: 0 = configs[1] requests run the per-frame LIGHT kernel
+#define WCE_LS_FLAT 1
+#endif
+#ifndef WCE_FLAT_U
+#define WCE_FLAT_U 8
+#endif
+constexpr int FLAT_U = WCE_FLAT_U;                      // elements per lane per chunk
+constexpr int FLAT_CHUNK = 64 * FLAT_U;                 // 512
+constexpr int FLAT_FR = (FLAT_CHUNK - 1) / NSC + 2;     // frames one chunk can touch: 11
+static_assert(4 * FLAT_FR <= 64, "one pilot per lane");
+constexpr int64_t FLAT_MAX_FRAMES = 1ll << 26;          // per launch: e < 2^32
+
+__global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ st, LsArgs a, int64_t f_begin,
+                                                      uint32_t nfr)
+{
+    __shared__ double2 s_txp[64], s_hlt[64];
+    __shared__ double2 s_hp[LS_WAVES][4 * FLAT_FR];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool do_lt = (a.mask & WCE_EST_LT_LS) && a.lt, do_lin = (a.mask & WCE_EST_PS_LINEAR) && a.lin;
+    const bool f32 = a.f32 != 0;
+    if (threadIdx.x < NSC) {
+        s_txp[threadIdx.x] = ld2(a.tx_pre ? a.tx_pre : st->tx_pre, threadIdx.x);
+        s_hlt[threadIdx.x] = ld2(st->h_lt, threadIdx.x);
+    }
+    __syncthreads();
+    const uint32_t E = nfr * (uint32_t)NSC;
+    const uint32_t nchunks = (E + FLAT_CHUNK - 1) / FLAT_CHUNK;
+    const int pj = lane & 3;
+    const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
+    double2 *hp_tab = s_hp[w];
+    for (uint32_t c = blockIdx.x * LS_WAVES + w; c < nchunks; c += gridDim.x * LS_WAVES) {
+        const uint32_t e0 = c * FLAT_CHUNK;
+        const uint32_t ff = e0 / NSC;                       // first frame of the chunk
+        // ---- every load of the chunk issued before any use
+        double2 ptx = make_double2(1, 0), prx = make_double2(0, 0);
+        if (do_lin && lane < 4 * FLAT_FR) {
+            const uint32_t fr = min(ff + (uint32_t)(lane >> 2), nfr - 1);
+            const int64_t o = (f_begin + fr) * a.fs + (int64_t)a.blk * a.bs + pil;
+            ptx = ld2(a.tx, o);
+            prx = ld2(a.rx, o);
+        }
+        double2 rp[FLAT_U];
+#pragma unroll
+        for (int i = 0; i < FLAT_U; ++i) {
+            const uint32_t e = min(e0 + 64u * i + lane, E - 1);
+            const uint32_t f = e / NSC, k = e - f * NSC;
+            rp[i] = (do_lt && a.rx_pre) ? ld2(a.rx_pre, (f_begin + f) * a.ps + k) : make_double2(0, 0);
+        }
+        if (do_lin) {
+            const double2 hp = cdiv(prx, ptx);              // main.c:82-84
+            if (lane < 4 * FLAT_FR) hp_tab[lane] = hp;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < FLAT_U; ++i) {
+            const uint32_t e = e0 + 64u * i + lane;
+            const uint32_t f = e / NSC, k = e - f * NSC;
+            const int64_t o = (f_begin + f) * a.os + k;
+            if (do_lt) {                                    // main.c:66-75
+                double2 h = s_hlt[k];
+                if (a.rx_pre) {
+                    const double2 t = s_txp[k];
+                    const double cq = t.x - t.y;
+                    h = cdiv(make_double2(cq * rp[i].x, cq * rp[i].y), make_double2(cq * t.x, cq * t.y));
+                }
+                if (k == WCE_DC) h = make_double2(0, 0);
+                if (e < E) st_out(a.lt, o, h, f32);
+            }
+            if (do_lin) {                                   // main.c:86-99
+                const int seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
+                const double alpha = (double)((int)k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) *
+                                     (1.0 / 14.0);
+                const int fl = (int)(f - ff) * 4 + seg;
+                const double2 lo = hp_tab[fl < 4 * FLAT_FR - 1 ? fl : 4 * FLAT_FR - 2];
+                const double2 hi = hp_tab[fl < 4 * FLAT_FR - 1 ? fl + 1 : 4 * FLAT_FR - 1];
+                if (e < E) st_out(a.lin, o, cadd(lo, cscale(csub(hi, lo), alpha)), f32);
+            }
+        }
+        wave_lds_sync();                                    // hp_tab is rewritten by the next chunk
+    }
+}
+
+// =====================================================================
 // MMSE solve.  One wave per frame, lane = 8p + q holds A[p+8a][q+8b] for the
 // 28 register blocks a >= b (a, b < 7): the block-cyclic 8x8 grid spreads the
 // shrinking trailing matrix evenly over lanes.  Row 53 holds conj(rx), so the
@@ -1067,6 +1161,18 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
     if (blocks > 256 * 8) blocks = 256 * 8;      // grid-stride the rest
     const bool eq = (a.mask & WCE_EQUALIZE) && a.eq;
     const dim3 g((unsigned)blocks), b(256);
+    if (WCE_LS_FLAT && !a.matlab && !eq &&
+        (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0) {
+        for (int64_t f0 = 0; f0 < a.n; f0 += FLAT_MAX_FRAMES) {
+            const int64_t nf = a.n - f0 < FLAT_MAX_FRAMES ? a.n - f0 : FLAT_MAX_FRAMES;
+            const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
+            int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
+            if (fb > 256 * 8) fb = 256 * 8;      // grid-stride the rest
+            hipLaunchKernelGGL(ls_flat_kernel, dim3((unsigned)fb), dim3(256), 0, (hipStream_t)stream, st, a, f0,
+                               (uint32_t)nf);
+        }
+        return hip_status(hipGetLastError());
+    }
     const bool light = !WCE_LS_NO_LIGHT && !eq && (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0;
     hipStream_t s = (hipStream_t)stream;
     if (a.matlab) {
