@@ -335,6 +335,24 @@ def bench_ls(wce, ctx, stream, n, reps):
         gbs = BYTES_LS_CFG2 * nb / (t * 1e-3) / 1e9
         out[label] = {"frames": nb, "avg_launch_ms": t, "frames_per_s": nb / (t * 1e-3), "achieved_GBs": gbs,
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
+    # HBM bytes from the LS-only PMC pass (tools/pmc_ls.sh: 1,048,576 frames per
+    # dispatch).  Reads: rx_pre streams (FETCH_SIZE half-counts 16-B/lane
+    # streaming reads on gfx950) plus 8 pilot loads per frame, each a full 64-B
+    # sector (counted in full); writes exact.
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_ls.json")))
+    if files:
+        k = json.load(open(files[-1])).get("wce::ls_flat_kernel")
+        if k:
+            per = 1024.0 / 1048576
+            out["pmc_bytes_per_frame"] = {"FETCH_SIZE": k["FETCH_SIZE"] * per, "WRITE_SIZE": k["WRITE_SIZE"] * per,
+                                          "expected_FETCH_SIZE": N * 16 / 2 + 8 * 64,
+                                          "real_traffic": N * 16 + 8 * 64 + k["WRITE_SIZE"] * per,
+                                          "source": os.path.basename(files[-1])}
+            key = "b%d" % n
+            rt = out["pmc_bytes_per_frame"]["real_traffic"]
+            out[key]["traffic"] = rt * n
+            out[key]["real_GBs"] = rt * n / (out[key]["avg_launch_ms"] * 1e-3) / 1e9
     return out
 
 

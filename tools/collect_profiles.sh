@@ -10,4 +10,5 @@ cp "$G/stats/run_kernel_stats.csv" "$R/profiles/${RND}_kernel_stats.csv"
 [ -f "$G/stats_head/run_kernel_stats.csv" ] && cp "$G/stats_head/run_kernel_stats.csv" "$R/profiles/${RND}_kernel_stats_headline.csv"
 cp "$G/pmc_summary.json" "$R/profiles/${RND}_pmc_summary.json"
 cp "$G/pmc_headline.json" "$R/profiles/${RND}_pmc_headline.json"
+[ -f "$G/pmc_ls.json" ] && cp "$G/pmc_ls.json" "$R/profiles/${RND}_pmc_ls.json"
 echo "collected into profiles/ as ${RND}_*"

@@ -14,7 +14,9 @@ cd "$R" && PMC_DIR=pmc_head bash tools/pmc_passes.sh > "$R/gpurun_out/pmc_head_p
 python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc_head" "$R/gpurun_out/pmc_headline.json" > /dev/null || exit $?
 cd "$R" && PMC_EXTRAS=1 bash tools/pmc_passes.sh > "$R/gpurun_out/pmc_passes.log" 2>&1 || exit $?
 python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc" "$R/gpurun_out/pmc_summary.json" > /dev/null || exit $?
+cd "$R" && bash tools/pmc_ls.sh > "$R/gpurun_out/pmc_ls_passes.log" 2>&1 || exit $?
 RND=${ROUND:-r01}   # the bench reads the newest profiles/*_pmc_*.json: overwrite this round's
+cp "$R/gpurun_out/pmc_ls.json" "$R/profiles/${RND}_pmc_ls.json"
 cp "$R/gpurun_out/pmc_summary.json" "$R/profiles/${RND}_pmc_summary.json"
 cp "$R/gpurun_out/pmc_headline.json" "$R/profiles/${RND}_pmc_headline.json"
 timeout -k 10 400 python3 "$R/bench.py" > "$R/gpurun_out/bench_full.json" 2> "$R/gpurun_out/bench_full.err" || exit $?
