@@ -268,6 +268,7 @@ static wce::SolveArgs solve_args(const wce_ctx *c, const wce_frames *in, wce_com
         a.cw = c->d_state->cwvec;
         a.cs = 0;
         a.hout = 1;
+        a.ref_pilots = 1;   // Ryy = 2 ow2 I, X = pilots: s = w^T X rx / b from 4 subcarriers
     }
     a.tx = reinterpret_cast<const double *>(in->tx);
     a.rx = reinterpret_cast<const double *>(in->rx);

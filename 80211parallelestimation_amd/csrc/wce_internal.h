@@ -90,6 +90,8 @@ struct SolveArgs {
     int32_t split;            // MATLAB averaging: nblk waves per frame, wave g = f*nblk + b
                               // writes W_b to w[g*ws] (or, with hout, cw . W_b to dots[g])
     double *dots;
+    int32_t ref_pilots;       // REF (main.c): a = 0 and X = the 4 pilots -> mmse_ref_flat_kernel
+    int32_t pad;
 };
 struct SynthArgs {
     double *tx, *rx, *rx_pre;

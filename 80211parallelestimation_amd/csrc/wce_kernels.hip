@@ -324,6 +324,85 @@ __global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ 
 }
 
 // =====================================================================
+// PS_MMSE in REF (main.c) semantics: a = 0, so Ryy = 2 ow2 I is diagonal and
+// X keeps the 4 pilots only (main.c:148-212, repaired as in DESIGN.md s2):
+// H_f = u_f s_f with s_f = sum_p w_f[P_p] tx_f[P_p] rx_f[P_p] / b.  Per frame
+// that is 4 pilot pairs in (64-B sectors, as the LS path) and 53 outputs:
+// HBM-bound, so it runs like ls_flat_kernel over e = 53 f + k -- lanes 4j+p
+// form frame j's pilot terms, a quad DPP sum gives s_j into a per-wave LDS
+// table, and every element lane writes u[k] s.  cs == 0: one shared (u, w)
+// (the ctx's C_ref); cs != 0: per-frame factors (WCE_MMSE_FRAME_COV).
+// =====================================================================
+#ifndef WCE_REF_FLAT   // A/B: 0 = REF runs inside mmse_solve_fc_kernel (one wave per frame)
+#define WCE_REF_FLAT 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ double dpp_quad(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+// sum over the 4 lanes of each quad, ((t0 + t1) + (t2 + t3)) in every lane
+__device__ __forceinline__ double2 quad_sum_c(double2 t)
+{
+    t = cadd(t, make_double2(dpp_quad<0xB1>(t.x), dpp_quad<0xB1>(t.y)));   // quad_perm [1,0,3,2]
+    return cadd(t, make_double2(dpp_quad<0x4E>(t.x), dpp_quad<0x4E>(t.y)));  // quad_perm [2,3,0,1]
+}
+
+__global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
+                                                            uint32_t nfr)
+{
+    __shared__ double2 s_u[64];
+    __shared__ double2 s_s[LS_WAVES][FLAT_FR];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool shared = a.cs == 0;
+    if (shared && threadIdx.x < NSC) s_u[threadIdx.x] = ld2(a.cu, threadIdx.x);
+    __syncthreads();
+    const double rb = 1.0 / st->bcoef;
+    const uint32_t E = nfr * (uint32_t)NSC;
+    const uint32_t nchunks = (E + FLAT_CHUNK - 1) / FLAT_CHUNK;
+    const int pj = lane & 3;
+    const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
+    double2 *s_tab = s_s[w];
+    for (uint32_t c = blockIdx.x * LS_WAVES + w; c < nchunks; c += gridDim.x * LS_WAVES) {
+        const uint32_t e0 = c * FLAT_CHUNK;
+        const uint32_t ff = e0 / NSC;
+        // ---- loads: pilot terms (lanes 4j+p) and, per frame, the u rows
+        double2 xt = make_double2(0, 0), xr = xt, wp = xt;
+        const uint32_t fr = min(ff + (uint32_t)(lane >> 2), nfr - 1);
+        if (lane < 4 * FLAT_FR) {
+            const int64_t o = (f_begin + fr) * a.fs + (int64_t)a.blk * a.bs + pil;
+            xt = ld2(a.tx, o);
+            xr = ld2(a.rx, o);
+            const int64_t wo = shared ? pil : (f_begin + fr) * a.cs + pil;
+            wp = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
+        }
+        double2 uf[FLAT_U];
+        if (!shared) {
+#pragma unroll
+            for (int i = 0; i < FLAT_U; ++i) {
+                const uint32_t e = min(e0 + 64u * i + lane, E - 1);
+                const uint32_t f = e / NSC, k = e - f * NSC;
+                uf[i] = ld2(a.cu, (f_begin + f) * a.cs + k);
+            }
+        }
+        const double2 sj = quad_sum_c(cmul(cmul(wp, xt), xr));   // w^T X rx over frame j's pilots
+        if (lane < 4 * FLAT_FR && pj == 0) s_tab[lane >> 2] = cscale(sj, rb);
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < FLAT_U; ++i) {
+            const uint32_t e = e0 + 64u * i + lane;
+            const uint32_t f = e / NSC, k = e - f * NSC;
+            const int jl = (int)(f - ff) < FLAT_FR ? (int)(f - ff) : FLAT_FR - 1;
+            const double2 u = shared ? s_u[k] : uf[i];
+            if (e < E) st2(a.w, (f_begin + f) * a.ws + k, cmul(u, s_tab[jl]));
+        }
+        wave_lds_sync();   // s_tab is rewritten by the next chunk
+    }
+}
+
+// =====================================================================
 // MMSE solve.  One wave per frame, lane = 8p + q holds A[p+8a][q+8b] for the
 // 28 register blocks a >= b (a, b < 7): the block-cyclic 8x8 grid spreads the
 // shrinking trailing matrix evenly over lanes.  Row 53 holds conj(rx), so the
@@ -1196,6 +1275,16 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     if (a.nblk > 1 && !a.split) return WCE_EINVAL;   // block averaging runs split
     const dim3 g((unsigned)waves), b(64);
     hipStream_t s = (hipStream_t)stream;
+    if (WCE_REF_FLAT && a.hout && a.ref_pilots && !a.split) {
+        for (int64_t f0 = 0; f0 < a.n; f0 += FLAT_MAX_FRAMES) {
+            const int64_t nf = a.n - f0 < FLAT_MAX_FRAMES ? a.n - f0 : FLAT_MAX_FRAMES;
+            const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
+            int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
+            if (fb > 256 * 8) fb = 256 * 8;
+            hipLaunchKernelGGL(mmse_ref_flat_kernel, dim3((unsigned)fb), dim3(256), 0, s, st, a, f0, (uint32_t)nf);
+        }
+        return hip_status(hipGetLastError());
+    }
     if (a.hout) hipLaunchKernelGGL(mmse_solve_fc_kernel, g, b, 0, s, st, a);
     else if (a.cu) hipLaunchKernelGGL(mmse_solve_kernel<true>, g, b, 0, s, st, a);
     else hipLaunchKernelGGL(mmse_solve_kernel<false>, g, b, 0, s, st, a);
