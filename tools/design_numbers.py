@@ -49,7 +49,7 @@ a = s.index("| Quantity | Value |")
 b = s.index("The bench brings the GPU to its steady clock")
 s = s[:a] + table + "\n" + s[b:]
 a = s.index("**PMC**, `mmse_solve")
-b = s.index("**What limits it now:**")
+b = s.index("**What limits it now**")
 s = s[:a] + pmc + "\n" + s[b:]
 open(p, "w").write(s)
 print(table)
