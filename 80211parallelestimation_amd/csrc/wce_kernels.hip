@@ -484,22 +484,9 @@ __device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double
 
 // Publish column k (unscaled) from the lanes that own it (q == kq).  Only
 // stores sit under the branch: no register is redefined in it.
-__device__ __forceinline__ int lane_id() { return threadIdx.x; }
-#ifndef WCE_ABLATE_PUBLISH   // timing-only build: no pivot-column stores after pivot 0
-#define WCE_ABLATE_PUBLISH 0
-#endif
 template <int KB>
 __device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 *buf, int p, int q, int kq)
 {
-    if (WCE_ABLATE_PUBLISH == 1 && KB + kq > 0) return;
-    if (WCE_ABLATE_PUBLISH == 2 && KB + kq > 0) {   // one masked store per step
-        if (q == kq) buf[p + 8 * KB] = A[KB][KB];
-        return;
-    }
-    if (WCE_ABLATE_PUBLISH == 3 && KB + kq > 0) {   // one full-wave store per step
-        buf[lane_id() & 63] = A[KB][KB];
-        return;
-    }
     if (q == kq) {
 #pragma unroll
         for (int aa = KB; aa < RB; ++aa) buf[p + 8 * aa] = A[aa][KB];
