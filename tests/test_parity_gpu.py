@@ -463,3 +463,29 @@ def oracle_lt(inp, rp, sem):
     h = np.conj(t) * rp / np.where(np.abs(t) > 0, np.abs(t) ** 2, 1.0)
     h[26] = 0
     return h
+
+
+def test_ref_flat_batch_edges(gpu_wce, golden, oracle):
+    """REF-mode PS_MMSE runs mmse_ref_flat_kernel (flat (frame, subcarrier)
+    elements, 512 per wave-chunk, <= 11 frames per chunk): batch sizes around
+    the chunk and the grid-stride sweep, sampled frames vs the bit-exact REF
+    oracle, output rows padded to 60 with the padding left untouched."""
+    r = golden["ref"]
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    Bmax = 32768 * 2 + 11
+    tx, rx, _ = _synth(ctx, gpu_wce, Bmax, seed=13)
+    txh, rxh = tx.numpy(), rx.numpy()
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    hls = oracle.lt_ls(inp["tx_pre"], inp["rx_pre"])
+    os_ = 60
+    for B in (1, 3, 10, 11, 12, 97, 4096, Bmax):
+        H = gpu_wce.DeviceArray((B, os_), zero=True)
+        ctx.estimate(ctx.frames(tx, rx, B), gpu_wce.Outputs(None, None, None, None, H.addr, None, os_, 0, 0, 0, 0),
+                     gpu_wce.PS_MMSE)
+        gpu_wce.synchronize()
+        h = H.numpy()
+        assert np.all(h[:, N:] == 0), B
+        for f in sorted({0, B - 1, B // 2, min(B - 1, 10), min(B - 1, 11)}):
+            exp = oracle.mmse_ref_repaired(txh[f, 0], rxh[f, 0], F, inp["ow2"], hls, invF)
+            assert normrel(h[f, :N], exp) < TOL, (B, f)
