@@ -4,16 +4,23 @@
 //   ls_kernel             LT_LS + PS_Linear/Cubic/Sinc + equalization, one
 //                         wave per frame, HBM streaming (main.c:66-146,
 //                         WiFi_Equalization.m); C or MATLAB semantics.
+//   ls_flat_kernel        LT_LS + PS_Linear only (BASELINE configs[1]), C
+//                         semantics, over flat (frame, subcarrier) elements.
+//   mmse_ref_flat_kernel  PS_MMSE in main.c semantics (diagonal Ryy: 4 pilot
+//                         terms per frame, H = u s), flat elements, HBM-bound.
 //   solve_block           the per-frame MMSE core: Ryy = a X C X' + b I built
-//                         in registers (8x8 lane grid, block-cyclic 28 blocks),
-//                         square-root-free LDL' with conj(rx) bordered on as
-//                         row 53 (forward solve for free), LDS only for the
-//                         pivot-column broadcast (main.c:148-212 /
-//                         WiFi_channel_estimation_PS_MMSE.m).  Two read-outs:
-//   mmse_solve_fc_kernel    rank-1 C = u w^T (REF, TEXTBOOK, per-frame C): a
-//                           second bordered row (w o x)^T leaves s = w^T X z in
-//                           the Schur complement; H = u s, one launch.
-//   mmse_solve_kernel       dense C (COV): blocked back-substitution, W = X z;
+//                         in registers (8x8 lane grid, block-cyclic 28 blocks)
+//                         with conj(rx) bordered on as row 53 (forward solve
+//                         for free), LDS for the pivot-column broadcast
+//                         (main.c:148-212 / WiFi_channel_estimation_PS_MMSE.m).
+//                         Two read-outs:
+//   mmse_solve_fc_kernel    rank-1 C = u w^T (TEXTBOOK, per-frame C; the
+//                           headline): Cholesky with row-per-lane panels (one
+//                           full-wave publish per pivot, dot_factor); a second
+//                           bordered row (w o x)^T leaves s = w^T X z in the
+//                           Schur complement; H = u s, one launch.
+//   mmse_solve_kernel       dense C (COV): block-cyclic square-root-free LDL',
+//                           blocked back-substitution, W = X z;
 //   matvec_kernel           then H = C W on v_mfma_f64_16x16x4_f64 (also the
 //                           per-frame covariance factors, MATLAB block mean).
 //   mmse_solve_ls_kernel  config 5: either solve with the LS family and
