@@ -1,0 +1,62 @@
+"""The committed bench line (profiles/<round>_bench.json) keeps the driver's
+contract and agrees with the committed rocprofv3 summary of the same command
+(CPU-only: reads the evidence files, runs nothing on a GPU)."""
+import csv
+import glob
+import json
+import os
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BASELINE = json.load(open(os.path.join(REPO, "BASELINE.json")))
+
+
+def _latest(pattern):
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    if not files:
+        pytest.skip(f"no profiles/{pattern}")
+    return files[-1]
+
+
+@pytest.fixture(scope="module")
+def line():
+    return json.load(open(_latest("r*_bench.json")))
+
+
+def test_contract_keys(line):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["metric"] == BASELINE["metric"]
+    assert line["n_gpus"] == 1 and line["scaling"] == "weak" and line["higher_is_better"] is True
+    assert line["vs_baseline"] is None          # BASELINE.md publishes no number for this metric
+    assert "workload" in line["config"] and "model" not in line["config"]
+    # value = frames of all ranks / timed wall
+    B = line["config"]["frames_per_gpu"] * line["n_gpus"]
+    assert abs(line["value"] - B / (line["ms_per_step"] * 1e-3)) / line["value"] < 1e-6
+
+
+def test_roofline_consistent(line):
+    r = line["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "TFLOP/s"
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    ach = r["flop_per_frame"] * r["frames_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12
+    assert abs(ach - r["achieved"]) / ach < 1e-9
+    assert r["traffic"] is None or r["traffic"] > 0.9 * r["algorithmic_bytes"]
+
+
+def test_cpu_baseline_fields(line):
+    c = line["cpu_baseline"]
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+
+
+def test_rocprof_headline_average_agrees(line):
+    """The headline kernel's average duration in the committed headline-only
+    rocprofv3 --stats summary is the bench's event-timed launch (within 10%:
+    the profiled run includes the clock ramp)."""
+    rows = list(csv.DictReader(open(_latest("r*_kernel_stats_headline.csv"))))
+    k = [r for r in rows if "mmse_solve_fc_kernel" in r["Name"]]
+    assert k, "headline kernel missing from the rocprof summary"
+    avg_ms = float(k[0]["AverageNs"]) * 1e-6
+    assert abs(avg_ms - line["roofline"]["avg_launch_ms"]) / avg_ms < 0.10, (avg_ms, line["roofline"]["avg_launch_ms"])
