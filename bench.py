@@ -145,6 +145,22 @@ def pmc_traffic(kernel: str, launches_frames: int, which: str = "pmc_summary"):
     return b * launches_frames / 65536.0, os.path.basename(files[-1])
 
 
+def pmc_mfma_busy(kernel: str, simds: int = 256 * 4):
+    """MFMA pipe utilisation of `kernel` from the committed PMC summary:
+    SQ_VALU_MFMA_BUSY_CYCLES (summed over SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs x
+    SIMDs) -- the busy share of the dispatch's wall cycles."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    keys = [k for k in d if kernel in k and "SQ_VALU_MFMA_BUSY_CYCLES" in d[k] and "GRBM_GUI_ACTIVE" in d[k]]
+    if not keys:
+        return None
+    k = d[sorted(keys, key=len)[0]]
+    return k["SQ_VALU_MFMA_BUSY_CYCLES"] / (k["GRBM_GUI_ACTIVE"] / 8.0 * simds)
+
+
 def time_events(wce, stream, fn, reps):
     e0, e1 = wce.Event(), wce.Event()
     e0.record(stream)
@@ -270,7 +286,8 @@ def main():
         res["apply_kernel"] = {"kernel": "matvec_kernel<false,false> = H = C W (v_mfma_f64_16x16x4), COV mode",
                                "avg_launch_ms": t_apply, "achieved_tflops": ach_apply,
                                "frac_fp64_peak": ach_apply / PEAK_FP64_TFLOPS,
-                               "mfma_traffic": pmc_traffic("matvec_kernel<false, false>", B)[0]}
+                               "mfma_traffic": pmc_traffic("matvec_kernel<false, false, 1>", B)[0],
+                               "mfma_busy_frac_pmc": pmc_mfma_busy("matvec_kernel<false, false, 1>")}
         del ctx3
 
     if not args.no_extras:
