@@ -20,7 +20,7 @@ table = f"""| Quantity | Value |
 | `matvec_kernel` as `H = C·W` (MFMA, COV mode) | {d['apply_kernel']['achieved_tflops']:.0f} TFLOP/s = {100 * d['apply_kernel']['frac_fp64_peak']:.0f}% of FP64 peak |
 | per-frame covariance MMSE (`FRAME_COV`) | {d['frame_cov']['textbook']['frames_per_s']:.3g} frames/s TEXTBOOK, {d['frame_cov']['ref']['frames_per_s']:.3g} REF |
 | config 5 (131,072 frames, all 5 + equalization, fused) | {d['config5']['fp64']['frames_per_s']:.3g} frames/s fp64; {d['config5']['mixed_fp64_solve_fp32_ls']['frames_per_s']:.3g} with fp32 LS outputs |
-| LS config 2 (LT_LS + PS_Linear), 1,048,576 frames | {d['ls_config2']['b1048576']['achieved_GBs'] / 1000:.2f} TB/s algorithmic = {100 * d['ls_config2']['b1048576']['frac']:.0f}% of 8 TB/s; {d['ls_config2']['b1048576']['frames_per_s']:.2g} frames/s |
+| LS config 2 (LT_LS + PS_Linear), 1,048,576 frames | {d['ls_config2']['b1048576']['achieved_GBs'] / 1000:.2f} TB/s algorithmic = {100 * d['ls_config2']['b1048576']['frac']:.0f}% of 8 TB/s; {d['ls_config2']['b1048576'].get('real_GBs', 0) / 1000:.2f} TB/s of PMC-measured HBM traffic (pilot sectors counted); {d['ls_config2']['b1048576']['frames_per_s']:.2g} frames/s |
 | LS config 2, 65,536 frames (MALL-resident) | {d['ls_config2']['b65536']['achieved_GBs'] / 1000:.2f} TB/s, {d['ls_config2']['b65536']['frames_per_s']:.2g} frames/s |
 | front end, 65,536 frames × 15 blocks | {d['front_end']['blocks']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['front_end']['blocks']['frac']:.1f}% of 8 TB/s (PMC traffic = algorithmic bytes to 1e-4); LTF {d['front_end']['preamble']['achieved_GBs'] / 1000:.2f} TB/s |
 | small batches (1,024 frames, all 5 + eq) | {d['small_batch']['direct']['us_per_call']:.0f} µs per call direct, {d['small_batch']['plan']['us_per_call']:.0f} µs as a replayed HIP-graph plan |
