@@ -40,24 +40,50 @@ def broadcast_state_host(dist, blob, nbytes: int, src: int = 0, group=None):
     return t.numpy().copy()
 
 
+def state_to_buffer(wce, ctx, buf=None):
+    """Copy ctx's device-resident state into a torch uint8 CUDA tensor (the
+    buffer RCCL sends).  Device to device."""
+    import torch
+
+    ptr, nbytes = ctx.state()
+    if buf is None:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if buf.numel() != nbytes or not buf.is_cuda:
+        raise ValueError("broadcast buffer must be a CUDA uint8 tensor of wce_state_size() bytes")
+    torch.cuda.synchronize()
+    if wce.load().wce_memcpy_dtod(buf.data_ptr(), ptr, nbytes, None) != 0:
+        raise wce.WceError(-2, "state -> broadcast buffer")
+    return buf
+
+
+def buffer_to_state(wce, buf, ctx):
+    """Install a received state buffer into ctx (an empty context is fine)
+    and mark it ready.  Device to device."""
+    import torch
+
+    ptr, nbytes = ctx.state()
+    if buf.numel() != nbytes or not buf.is_cuda:
+        raise ValueError("broadcast buffer must be a CUDA uint8 tensor of wce_state_size() bytes")
+    torch.cuda.synchronize()
+    if wce.load().wce_memcpy_dtod(ptr, buf.data_ptr(), nbytes, None) != 0:
+        raise wce.WceError(-2, "broadcast buffer -> state")
+    ctx.mark_ready()
+
+
 def broadcast_state_device(dist, wce, ctx, src: int = 0, group=None):
     """ONE RCCL broadcast of ctx's device-resident state from src into every
     other rank's context (which may be an empty context).  Device to device:
     the state never goes back through the host."""
     import torch
 
-    ptr, nbytes = ctx.state()
-    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    lib = wce.load()
     rank = dist.get_rank(group)
     if rank == src:
-        if lib.wce_memcpy_dtod(buf.data_ptr(), ptr, nbytes, None) != 0:
-            raise wce.WceError(-2, "state -> broadcast buffer")
+        buf = state_to_buffer(wce, ctx)
+    else:
+        buf = torch.empty(ctx.state()[1], dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     dist.broadcast(buf, src=src, group=group)
     torch.cuda.synchronize()
     if rank != src:
-        if lib.wce_memcpy_dtod(ptr, buf.data_ptr(), nbytes, None) != 0:
-            raise wce.WceError(-2, "broadcast buffer -> state")
-        ctx.mark_ready()
-    return nbytes
+        buffer_to_state(wce, buf, ctx)
+    return buf.numel()

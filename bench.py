@@ -76,7 +76,10 @@ class Dist:
         self.backend = os.environ.get("WCE_DIST_BACKEND", "nccl")
         self.torch = None
         self.device = self.local
-        if self.world > 1:
+        # WCE_FORCE_DIST=1: run the distributed path at world size 1 too (a
+        # one-rank RCCL group), so a one-GPU box exercises exactly the code the
+        # N>1 runs take: device broadcast, device barrier, max all-reduce.
+        if self.world > 1 or os.environ.get("WCE_FORCE_DIST") == "1":
             import torch
             import torch.distributed as dist
             self.torch, self.dist = torch, dist
