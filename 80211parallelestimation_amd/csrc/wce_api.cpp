@@ -636,3 +636,10 @@ int wce_event_elapsed_ms(float *ms, void *a, void *b)
 }
 
 }  // extern "C"
+
+// ---- internal hooks for wce_multi.cpp (wce_internal.h)
+namespace wce {
+int api_fail(int code, const char *what) { return fail(code, what); }
+int ctx_device(const wce_ctx *c) { return c ? c->device : -1; }
+bool ctx_ready(const wce_ctx *c) { return c && c->ready; }
+}  // namespace wce

@@ -128,4 +128,10 @@ int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, doub
 int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 
+// wce_api.cpp hooks used by wce_multi.cpp: set wce_last_error() and return
+// `code`; a context's device and whether its state is valid.
+int api_fail(int code, const char *what);
+int ctx_device(const wce_ctx *c);
+bool ctx_ready(const wce_ctx *c);
+
 }  // namespace wce

@@ -111,6 +111,16 @@ ABI = {
     "wce_front_end_blocks": [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_void_p],
     "wce_front_end_preamble": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p,
                                c_void_p],
+    "wce_comm_unique_id": [c_void_p],
+    "wce_comm_init_rank": [POINTER(c_void_p), c_void_p, c_int, c_int, c_int],
+    "wce_comm_init_all": [POINTER(c_void_p), c_int, POINTER(c_int)],
+    "wce_comm_destroy": [c_void_p],
+    "wce_comm_info": [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)],
+    "wce_ctx_broadcast_state": [c_void_p, c_void_p, c_int, c_void_p],
+    "wce_ctx_broadcast_state_all": [POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, POINTER(c_void_p)],
+    "wce_comm_max_f64": [c_void_p, POINTER(c_double), c_void_p],
+    "wce_comm_max_f64_all": [POINTER(c_void_p), c_int, POINTER(c_double), POINTER(c_void_p)],
+    "wce_shard": [ctypes.c_int64, c_int, c_int, POINTER(ctypes.c_int64), POINTER(ctypes.c_int64)],
     "wce_device_count": [POINTER(c_int)],
     "wce_set_device": [c_int],
     "wce_malloc": [POINTER(c_void_p), c_size_t],

@@ -230,6 +230,43 @@ int wce_front_end_preamble(wce_ctx *ctx, const wce_complex *lptot, int64_t lptot
                            int64_t n_frames, wce_complex *pre_fft, int64_t pre_stride, double *ow2,
                            void *stream);
 
+/* ---- multi-GPU: frames are independent, so a batch is sharded
+ * over GPUs with no data-path collective; the only exchange is ONE RCCL
+ * broadcast of the packed shared state (wce_ctx_state) over xGMI, the
+ * analogue of the reference's MPI_Bcast of F / Ryy (main_mpi.c:687-688,
+ * 727-728).  RCCL (librccl.so.1) is loaded on first use, so hosts that never
+ * call these need no RCCL.  Two launch models:
+ *   - one process per GPU (the MPI model of main_mpi.c): rank 0 calls
+ *     wce_comm_unique_id, the host distributes the WCE_COMM_ID_BYTES bytes
+ *     (MPI_Bcast, a file, a socket), every rank calls wce_comm_init_rank;
+ *   - one process driving several GPUs: wce_comm_init_all. */
+#define WCE_COMM_ID_BYTES 128
+typedef struct wce_comm wce_comm;
+int wce_comm_unique_id(void *id);
+int wce_comm_init_rank(wce_comm **comm, const void *id, int nranks, int rank, int device);
+int wce_comm_init_all(wce_comm **comms, int ndev, const int *devices);
+int wce_comm_destroy(wce_comm *comm);
+int wce_comm_info(const wce_comm *comm, int *rank, int *nranks, int *device);
+
+/* ONE in-place ncclBroadcast of ctx's shared state from `root` (whose ctx
+ * must hold a valid state) into every rank's ctx (which may be empty, see
+ * wce_ctx_create_empty); ctx and comm must be on the same device.  Returns
+ * once the state has arrived and been validated (a once-per-process setup
+ * call, not a per-batch one).  The _all form does the same for n contexts of
+ * one process (comms from wce_comm_init_all), as one RCCL group. */
+int wce_ctx_broadcast_state(wce_ctx *ctx, wce_comm *comm, int root, void *stream);
+int wce_ctx_broadcast_state_all(wce_ctx **ctxs, wce_comm **comms, int n, int root, void **streams);
+
+/* max over ranks of one double (e.g. each shard's parity error, or its time):
+ * an 8-byte ncclAllReduce, synchronous.  _all: one value per context of one
+ * process, every entry replaced by the maximum. */
+int wce_comm_max_f64(wce_comm *comm, double *value, void *stream);
+int wce_comm_max_f64_all(wce_comm **comms, int n, double *values, void **streams);
+
+/* Contiguous frame range [first, first + count) of `rank` out of `total`
+ * (the first total % nranks ranks take one extra frame). */
+int wce_shard(int64_t total, int nranks, int rank, int64_t *first, int64_t *count);
+
 /* ---- thin runtime helpers (so C hosts and tests need no other HIP binding) ---- */
 int wce_device_count(int *count);
 int wce_set_device(int device);

@@ -70,3 +70,29 @@ def test_state_broadcast_gloo_world2():
         assert same
         assert magic == 0x80211
         assert (first, count) == (rank * 65536, 65536)
+
+
+@pytest.mark.parametrize("total,world", [(0, 2), (1, 2), (65536, 8), (1000003, 7), (5, 8)])
+def test_native_shard_matches_host(wce, total, world):
+    """wce_shard (C ABI) partitions exactly like multi.shard."""
+    multi = importlib.import_module("80211parallelestimation_amd.multi")
+    for r in range(world):
+        assert multi.native_shard(wce, total, world, r) == multi.shard(total, world, r)
+
+
+def test_native_comm_fails_loudly_without_device(wce):
+    """Bad arguments are rejected and, with no gfx950 device, a communicator
+    cannot be created (an error code, never a silent CPU path)."""
+    import ctypes
+
+    multi = importlib.import_module("80211parallelestimation_amd.multi")
+    lib = wce.load()
+    f, c = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.wce_shard(10, 0, 0, ctypes.byref(f), ctypes.byref(c)) != 0
+    assert lib.wce_shard(10, 2, 2, ctypes.byref(f), ctypes.byref(c)) != 0
+    assert lib.wce_comm_info(None, None, None, None) != 0
+    assert lib.wce_ctx_broadcast_state(None, None, 0, None) != 0
+    assert lib.wce_comm_destroy(None) == 0
+    if wce.device_count() == 0:
+        with pytest.raises(wce.WceError):
+            multi.NativeComm(wce, b"\0" * multi.COMM_ID_BYTES, 1, 0, 0)

@@ -51,6 +51,24 @@ def test_rccl_state_broadcast_roundtrip(gpu_wce):
     assert res["allreduce_max"] == 3.5
 
 
+def test_native_rccl_path(gpu_wce):
+    """libwce's own RCCL path (wce_comm_*, no torch in the process): both
+    launch models in their one-rank form, bit-identical estimates after the
+    in-place state broadcast, the root's bytes untouched, the max all-reduce,
+    and a root without state refused."""
+    p = subprocess.run([sys.executable, os.path.join(REPO, "tests", "native_comm_worker.py")], env=_env(),
+                       capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = _last_json(p.stdout)
+    assert res["info"] == [0, 1, 0] and res["all_info"] == [0, 1, 0]
+    for case in ("rank_textbook", "rank_ref", "all_ref"):
+        r = res[case]
+        assert r["bit_identical"] and r["finite"] and r["root_unchanged"], res
+        assert r["bytes"] == gpu_wce.load().wce_state_size()
+    assert res["max"] == 3.5
+    assert res["empty_root_refused"]
+
+
 def test_bench_distributed_path_one_rank(gpu_wce):
     env = _env()
     env["WCE_FORCE_DIST"] = "1"
