@@ -314,6 +314,20 @@ int wce_mmse_apply(wce_ctx *c, const wce_complex *W, wce_complex *H, int64_t str
     return rc ? fail(rc, "mmse_apply launch") : WCE_OK;
 }
 
+int wce_nonfinite_scan(wce_ctx *c, const void *H, int64_t stride, int64_t n, uint32_t flags, uint32_t *bitmap,
+                       unsigned long long *n_bad, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (n < 0) return fail(WCE_EINVAL, "n < 0");
+    if (flags & ~(uint32_t)WCE_OUT_LS_F32) return fail(WCE_EINVAL, "unknown flags");
+    if (n == 0) return WCE_OK;
+    if (!H || !bitmap || (n > 1 && stride < wce::NSC)) return fail(WCE_EINVAL, "bad H/bitmap/stride");
+    DeviceGuard g(c->device);
+    int rc = wce::launch_nonfinite_scan(reinterpret_cast<const double *>(H), stride, n, (flags & WCE_OUT_LS_F32) != 0,
+                                        bitmap, n_bad, stream);
+    return rc ? fail(rc, "nonfinite_scan launch") : WCE_OK;
+}
+
 static int ensure_ws(wce_ctx *c, int64_t n)
 {
     if (n <= c->ws_frames) return WCE_OK;

@@ -1223,6 +1223,44 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthArgs a, const double *_
     }
 }
 
+
+// =====================================================================
+// Non-finite guard ("an optional per-frame non-finite bitmap").
+// The reference passes NaN through silently -- its literal PS_MMSE returns
+// NaN x 53 (main.c:148-212) and its divisions by a zero pilot give
+// Inf.  One HBM pass over an output array on the flat element index
+// e = 53 f + k (like ls_flat_kernel: every lane of a load carries one entry);
+// only the rare non-finite lanes touch the bitmap, and the lane whose
+// atomicOr sets a frame's bit is the one that counts that frame.
+// =====================================================================
+template <bool F32>
+__global__ __launch_bounds__(256) void nonfinite_scan_kernel(const double *__restrict__ H, int64_t stride,
+                                                             int64_t f_begin, uint32_t nfr, uint32_t *bits,
+                                                             unsigned long long *n_bad)
+{
+    const uint32_t E = nfr * (uint32_t)NSC;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < E; e += gridDim.x * 256u) {
+        const uint32_t f = e / NSC, k = e - f * NSC;
+        const int64_t idx = (f_begin + f) * stride + k;
+        double re, im;
+        if constexpr (F32) {
+            const v2f t = reinterpret_cast<const v2f *>(H)[idx];
+            re = t.x;
+            im = t.y;
+        } else {
+            const double2 t = ld2(H, idx);
+            re = t.x;
+            im = t.y;
+        }
+        if (!(__builtin_isfinite(re) && __builtin_isfinite(im))) {
+            const int64_t fg = f_begin + f;
+            const uint32_t bit = 1u << (fg & 31);
+            const uint32_t old = atomicOr(&bits[fg >> 5], bit);
+            if (!(old & bit) && n_bad) atomicAdd(n_bad, 1ull);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP; }
 
@@ -1347,6 +1385,26 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream)
     if (a.n <= 0) return WCE_OK;
     const int64_t blocks = (a.n + 3) / 4;
     hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, st->tx_pre);
+    return hip_status(hipGetLastError());
+}
+
+int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,
+                          unsigned long long *n_bad, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(bits, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s) != hipSuccess) return WCE_EHIP;
+    if (n_bad && hipMemsetAsync(n_bad, 0, sizeof(*n_bad), s) != hipSuccess) return WCE_EHIP;
+    for (int64_t f0 = 0; f0 < n; f0 += FLAT_MAX_FRAMES) {     // f0 % 32 == 0: words never straddle launches
+        const int64_t nf = n - f0 < FLAT_MAX_FRAMES ? n - f0 : FLAT_MAX_FRAMES;
+        int64_t blocks = (nf * NSC + 255) / 256;
+        if (blocks > 256 * 8) blocks = 256 * 8;
+        if (f32)
+            hipLaunchKernelGGL(nonfinite_scan_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, H, stride, f0,
+                               (uint32_t)nf, bits, n_bad);
+        else
+            hipLaunchKernelGGL(nonfinite_scan_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, H, stride, f0,
+                               (uint32_t)nf, bits, n_bad);
+    }
     return hip_status(hipGetLastError());
 }
 

@@ -111,6 +111,8 @@ ABI = {
     "wce_front_end_blocks": [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_void_p],
     "wce_front_end_preamble": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p,
                                c_void_p],
+    "wce_nonfinite_scan": [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, c_uint32, c_void_p, c_void_p,
+                           c_void_p],
     "wce_comm_unique_id": [c_void_p],
     "wce_comm_init_rank": [POINTER(c_void_p), c_void_p, c_int, c_int, c_int],
     "wce_comm_init_all": [POINTER(c_void_p), c_int, POINTER(c_int)],
@@ -313,6 +315,23 @@ class Context:
                tx_pre=None, block=0, semantics=SEM_C) -> Frames:
         return Frames(_addr(tx), _addr(rx), _addr(rx_pre), _addr(tx_pre), frame_stride, block_stride, pre_stride,
                       n_frames, block, semantics)
+
+    def nonfinite_scan(self, H, n_frames, stride=NSC, f32=False, bitmap=None, n_bad=None, stream=None):
+        """wce_nonfinite_scan on a device output array.  With bitmap/n_bad
+        None, allocates them, waits, and returns (bitmap as numpy uint32,
+        number of non-finite frames); otherwise enqueues into the given
+        device buffers and returns None."""
+        own = bitmap is None
+        if own:
+            bitmap = DeviceArray(((n_frames + 31) // 32,), dtype=np.uint32)
+            n_bad = DeviceArray((1,), dtype=np.uint64)
+        _check(_lib.wce_nonfinite_scan(self.handle, _addr(H), stride, n_frames, OUT_LS_F32 if f32 else 0, _addr(bitmap),
+                                       _addr(n_bad), stream), "wce_nonfinite_scan")
+        if not own:
+            return None
+        if stream is not None:
+            _check(_lib.wce_stream_synchronize(stream), "wce_stream_synchronize")
+        return bitmap.numpy(), int(n_bad.numpy()[0])
 
     def estimate(self, frames: Frames, outputs: Outputs, mask: int, stream=None):
         _check(_lib.wce_estimate(self.handle, byref(frames), byref(outputs), mask, stream), "wce_estimate")

@@ -230,6 +230,18 @@ int wce_front_end_preamble(wce_ctx *ctx, const wce_complex *lptot, int64_t lptot
                            int64_t n_frames, wce_complex *pre_fft, int64_t pre_stride, double *ow2,
                            void *stream);
 
+/* Non-finite guard.  The reference passes NaN/Inf through
+ * silently: main.c's PS_MMSE returns NaN x 53 (main.c:148-212), a zero pilot
+ * makes PS_* divide by zero (main.c:82-84), and its dimension checks only
+ * print (utils.c:18-19).  One HBM pass over an output array H[f*stride + k]
+ * (k < 53; complex double, or complex float with flags = WCE_OUT_LS_F32):
+ * bit f % 32 of bitmap[f / 32] (device, ceil(n/32) words, zeroed here) is set
+ * iff any of frame f's 53 entries has a NaN or Inf part; *n_bad (device,
+ * optional) receives the number of such frames.  Any ctx selects the device
+ * (its state need not be loaded).  Asynchronous on `stream`. */
+int wce_nonfinite_scan(wce_ctx *ctx, const void *H, int64_t stride, int64_t n_frames, uint32_t flags,
+                       uint32_t *bitmap, unsigned long long *n_bad, void *stream);
+
 /* ---- multi-GPU: frames are independent, so a batch is sharded
  * over GPUs with no data-path collective; the only exchange is ONE RCCL
  * broadcast of the packed shared state (wce_ctx_state) over xGMI, the
