@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -20,8 +23,13 @@ struct wce_ctx {
     int32_t mode = -1;          // State::mode, cached when the state becomes valid
     bool fuse = true;           // config-5 fusion (wce_debug_set_fusion turns it off for A/B)
     bool bdot = true;           // rank-1 C: second bordered row, no back-solve / GEMM (A/B switch)
-    double *ws = nullptr;       // WCE_MMSE_FRAME_COV workspace: h | g | u | w, [ws_frames][64] complex each
-    int64_t ws_frames = 0;
+    // Workspaces (FRAME_COV factors, MATLAB per-block rows), one per stream:
+    // calls on different streams never share scratch, so they may run
+    // concurrently (SURVEY 8(b) threading).  A call holds its stream's entry
+    // locked from sizing to the last launch; plans own their workspace.
+    std::mutex ws_mu;
+    std::map<void *, std::unique_ptr<wce::Workspace>> ws_by_stream;
+    int64_t ws_hint = 0;        // wce_ctx_reserve: minimum size of new entries
 };
 
 static constexpr int64_t WS_LD = 64;   // row stride (complex) of the workspace vectors
@@ -150,10 +158,11 @@ int wce_ctx_create_cov(wce_ctx **out, int device, const wce_complex *tx_pre, con
 int wce_ctx_destroy(wce_ctx *c)
 {
     if (!c) return WCE_OK;
-    if (c->d_state || c->ws) {
+    {
         DeviceGuard g(c->device);
         if (c->d_state) (void)hipFree(c->d_state);
-        if (c->ws) (void)hipFree(c->ws);
+        for (auto &kv : c->ws_by_stream)
+            if (kv.second->p) (void)hipFree(kv.second->p);
     }
     delete c;
     return WCE_OK;
@@ -328,38 +337,67 @@ int wce_nonfinite_scan(wce_ctx *c, const void *H, int64_t stride, int64_t n, uin
     return rc ? fail(rc, "nonfinite_scan launch") : WCE_OK;
 }
 
-static int ensure_ws(wce_ctx *c, int64_t n)
+// grow `w` to n frames; the old buffer may still be read by work queued on
+// `stream`, so that stream drains first (hipFree would wait for it anyway)
+static int grow_ws(wce_ctx *c, wce::Workspace &w, int64_t n, void *stream)
 {
-    if (n <= c->ws_frames) return WCE_OK;
+    if (n <= w.frames) return WCE_OK;
     DeviceGuard g(c->device);
-    if (c->ws) {
-        HIPCHECK(hipDeviceSynchronize(), "sync before workspace growth");
-        (void)hipFree(c->ws);
-        c->ws = nullptr;
-        c->ws_frames = 0;
+    if (w.p) {
+        HIPCHECK(hipStreamSynchronize((hipStream_t)stream), "sync before workspace growth");
+        (void)hipFree(w.p);
+        w.p = nullptr;
+        w.frames = 0;
     }
-    HIPCHECK(hipMalloc(&c->ws, (size_t)n * WS_ARRAYS * WS_LD * 2 * sizeof(double)), "hipMalloc(workspace)");
-    c->ws_frames = n;
+    HIPCHECK(hipMalloc(&w.p, (size_t)n * WS_ARRAYS * WS_LD * 2 * sizeof(double)), "hipMalloc(workspace)");
+    w.frames = n;
     return WCE_OK;
+}
+
+// stream's workspace entry (created on first use), returned LOCKED
+static wce::Workspace *stream_ws(wce_ctx *c, void *stream, std::unique_lock<std::mutex> &lk)
+{
+    wce::Workspace *w;
+    {
+        std::lock_guard<std::mutex> g(c->ws_mu);
+        auto &slot = c->ws_by_stream[stream];
+        if (!slot) slot.reset(new (std::nothrow) wce::Workspace);
+        w = slot.get();
+    }
+    if (w) lk = std::unique_lock<std::mutex>(w->mu);
+    return w;
+}
+
+int wce_ctx_reserve_stream(wce_ctx *c, int64_t n, void *stream)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (n < 0) return fail(WCE_EINVAL, "n_frames < 0");
+    std::unique_lock<std::mutex> lk;
+    wce::Workspace *w = stream_ws(c, stream, lk);
+    if (!w) return fail(WCE_ENOMEM, "workspace entry");
+    return grow_ws(c, *w, n, stream);
 }
 
 int wce_ctx_reserve(wce_ctx *c, int64_t n)
 {
     if (!c) return fail(WCE_EINVAL, "null ctx");
     if (n < 0) return fail(WCE_EINVAL, "n_frames < 0");
-    return ensure_ws(c, n);
+    {
+        std::lock_guard<std::mutex> g(c->ws_mu);
+        if (n > c->ws_hint) c->ws_hint = n;
+    }
+    return wce_ctx_reserve_stream(c, n, nullptr);
 }
 
 // WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvecs), into
 // the solve arguments.  lt_ready: the caller's LT_LS output already holds H_LT.
 static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready,
-                          wce::SolveArgs &sa, void *stream)
+                          wce::SolveArgs &sa, double *ws, void *stream)
 {
     const int64_t n = in->n_frames;
     if (!in->rx_pre) return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
-    int rc = ensure_ws(c, n);
-    if (rc) return rc;
-    double *hw = c->ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
+    int rc = WCE_OK;
+    double *hw = ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
     const double *h = hw;
     int64_t hs = WS_LD;
     if (lt_ready) {
@@ -394,7 +432,10 @@ static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
     return WCE_OK;
 }
 
-int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
+// fixed != nullptr: a plan's own workspace (capture time); otherwise the
+// stream's entry, held locked until the last launch is queued
+static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream,
+                         wce::Workspace *fixed)
 {
     if (!c || !out) return fail(WCE_EINVAL, "null argument");
     if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
@@ -440,22 +481,37 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     const bool fc = (mask & WCE_MMSE_FRAME_COV) != 0;
     const bool split = sa.nblk > 1;   // MATLAB: one wave per (frame, block), averaged after
     if (split && n * sa.nblk > INT32_MAX) return fail(WCE_EINVAL, "n_frames * 4 > 2^31 - 1 (MATLAB semantics)");
+    std::unique_lock<std::mutex> lk;
+    double *ws = nullptr;
     if (fc || split) {
-        rc = ensure_ws(c, n);
-        if (rc) return rc;
+        wce::Workspace *w = fixed;
+        if (!w) {
+            w = stream_ws(c, stream, lk);
+            if (!w) return fail(WCE_ENOMEM, "workspace entry");
+            int64_t want = n;
+            {
+                std::lock_guard<std::mutex> hg(c->ws_mu);
+                if (c->ws_hint > want) want = c->ws_hint;
+            }
+            rc = grow_ws(c, *w, want, stream);
+            if (rc) return rc;
+        } else if (w->frames < n) {
+            return fail(WCE_EINVAL, "plan workspace too small");
+        }
+        ws = w->p;
     }
     if (fc) {
         const bool lt_ready = !fuse && (mask & WCE_EST_LT_LS) && !(out->flags & WCE_OUT_LS_F32);
-        rc = prep_frame_cov(c, in, out, lt_ready, sa, stream);
+        rc = prep_frame_cov(c, in, out, lt_ready, sa, ws, stream);
         if (rc) return rc;
     }
-    double *aux = c->ws ? c->ws + (WS_ARRAYS - 1) * n * WS_LD * 2 : nullptr;
+    double *aux = ws ? ws + (WS_ARRAYS - 1) * n * WS_LD * 2 : nullptr;
     if (split) {
         sa.split = 1;
         if (sa.hout) {
             sa.dots = aux;
         } else {
-            sa.w = c->ws;
+            sa.w = ws;
             sa.ws = WS_LD;
         }
     }
@@ -463,14 +519,23 @@ int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint3
     if (rc) return fail(rc, "mmse_solve launch");
     double *H = reinterpret_cast<double *>(out->ps_mmse);
     if (sa.hout && split) rc = wce::launch_fc_finish(sa, aux, H, out->out_stride, stream);
-    else if (split) rc = wce::launch_matvec_avg(c->d_state->C, c->ws, WS_LD, sa.nblk, H, out->out_stride, n, stream);
+    else if (split) rc = wce::launch_matvec_avg(c->d_state->C, ws, WS_LD, sa.nblk, H, out->out_stride, n, stream);
     else if (!sa.hout) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream);   // H = C W in place
     if (rc) return fail(rc, "mmse apply launch");
     return WCE_OK;
 }
 
+int wce_estimate(wce_ctx *c, const wce_frames *in, const wce_outputs *out, uint32_t mask, void *stream)
+{
+    return estimate_impl(c, in, out, mask, stream, nullptr);
+}
+
 struct wce_plan {
+    wce_plan() = default;
+    wce_plan(const wce_plan &) = delete;
+    wce_plan &operator=(const wce_plan &) = delete;
     int device = 0;
+    wce::Workspace ws;   // the plan's own scratch: replays never share a stream's
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
 };
@@ -480,27 +545,42 @@ int wce_plan_create(wce_plan **out_plan, wce_ctx *c, const wce_frames *in, const
     if (!out_plan || !c || !in || !out) return fail(WCE_EINVAL, "null argument");
     if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
     DeviceGuard g(c->device);
-    // size the workspace now: nothing may allocate while the stream is captured
+    wce_plan *p = new (std::nothrow) wce_plan;
+    if (!p) return fail(WCE_ENOMEM, "alloc");
+    p->device = c->device;
+    // size the plan's workspace now: nothing may allocate while the stream is captured
     if ((mask & WCE_MMSE_FRAME_COV) || (in->semantics == WCE_SEM_MATLAB && (mask & WCE_EST_PS_MMSE))) {
-        int rc = ensure_ws(c, in->n_frames);
-        if (rc) return rc;
+        int rc = grow_ws(c, p->ws, in->n_frames > 0 ? in->n_frames : 1, nullptr);
+        if (rc) { delete p; return rc; }
     }
+    auto fail_plan = [&](int code) {
+        if (p->ws.p) (void)hipFree(p->ws.p);
+        delete p;
+        return code;
+    };
     hipStream_t cs = nullptr;
-    HIPCHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan capture stream");
-    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-    if (e != hipSuccess) { (void)hipStreamDestroy(cs); return hipfail(e, "hipStreamBeginCapture"); }
-    const int rc = wce_estimate(c, in, out, mask, cs);   // validates, then records the launches
+    hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    if (e != hipSuccess) return fail_plan(hipfail(e, "plan capture stream"));
+    e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(cs);
+        return fail_plan(hipfail(e, "hipStreamBeginCapture"));
+    }
+    const int rc = estimate_impl(c, in, out, mask, cs, &p->ws);   // validates, then records the launches
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(cs, &graph);
     (void)hipStreamDestroy(cs);
-    if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
-    if (e != hipSuccess) return hipfail(e, "hipStreamEndCapture");
-    wce_plan *p = new (std::nothrow) wce_plan;
-    if (!p) { (void)hipGraphDestroy(graph); return fail(WCE_ENOMEM, "alloc"); }
-    p->device = c->device;
+    if (rc) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return fail_plan(rc);
+    }
+    if (e != hipSuccess) return fail_plan(hipfail(e, "hipStreamEndCapture"));
     p->graph = graph;
     e = hipGraphInstantiate(&p->exec, graph, nullptr, nullptr, 0);
-    if (e != hipSuccess) { (void)hipGraphDestroy(graph); delete p; return hipfail(e, "hipGraphInstantiate"); }
+    if (e != hipSuccess) {
+        (void)hipGraphDestroy(graph);
+        return fail_plan(hipfail(e, "hipGraphInstantiate"));
+    }
     *out_plan = p;
     return WCE_OK;
 }
@@ -519,6 +599,7 @@ int wce_plan_destroy(wce_plan *p)
     DeviceGuard g(p->device);
     if (p->exec) (void)hipGraphExecDestroy(p->exec);
     if (p->graph) (void)hipGraphDestroy(p->graph);
+    if (p->ws.p) (void)hipFree(p->ws.p);
     delete p;
     return WCE_OK;
 }

@@ -1,6 +1,7 @@
 // wce_internal.h -- layout shared by the host code (g++ / hipcc) and the
 // gfx950 kernels.  Not part of the public ABI (include/wce.h is).
 #pragma once
+#include <mutex>
 #include <stdint.h>
 #include <stddef.h>
 #include "../../include/wce.h"
@@ -129,6 +130,14 @@ int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t 
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,
                           unsigned long long *n_bad, void *stream);
+
+// per-stream (or per-plan) scratch of wce_estimate: [frames] x 5 arrays of
+// 64 complex (wce_api.cpp WS_ARRAYS / WS_LD); mu serialises the calls of one stream
+struct Workspace {
+    std::mutex mu;
+    double *p = nullptr;
+    int64_t frames = 0;
+};
 
 // wce_api.cpp hooks used by wce_multi.cpp: set wce_last_error() and return
 // `code`; a context's device and whether its state is valid.

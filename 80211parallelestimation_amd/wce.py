@@ -90,6 +90,7 @@ ABI = {
     "wce_ctx_create_empty": [POINTER(c_void_p), c_int],
     "wce_ctx_destroy": [c_void_p],
     "wce_ctx_reserve": [c_void_p, c_int64],
+    "wce_ctx_reserve_stream": [c_void_p, c_int64, c_void_p],
     "wce_plan_create": [POINTER(c_void_p), c_void_p, c_void_p, c_void_p, c_uint32],
     "wce_plan_launch": [c_void_p, c_void_p],
     "wce_plan_destroy": [c_void_p],

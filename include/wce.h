@@ -162,11 +162,20 @@ typedef struct {
  * count elements of each buffer's own type. */
 #define WCE_OUT_LS_F32 (1u << 0)
 
-/* Pre-size the context's device workspace (WCE_MMSE_FRAME_COV and MATLAB-
- * semantics PS_MMSE) for batches of up to n_frames (5 KB per frame), so that
- * wce_estimate never allocates.  Without
- * it the first larger batch allocates (synchronously) and keeps the buffer. */
+/* Threading: one ctx may serve calls on several streams at once, from one
+ * host thread or several.  The shared state is read-only after creation, and
+ * the scratch that WCE_MMSE_FRAME_COV and MATLAB-semantics PS_MMSE need
+ * (5 KB per frame) is kept per stream, so calls on different streams never
+ * share it; calls on the same stream are serialised (as the stream would).
+ * Plans own their scratch.  wce_last_error() is per thread.
+ *
+ * Pre-size that scratch for batches of up to n_frames so that wce_estimate
+ * never allocates: _stream for one stream; wce_ctx_reserve for the NULL
+ * stream, and as the minimum size of every stream's scratch created later.
+ * Without it the first larger batch on a stream allocates (synchronously on
+ * that stream) and keeps the buffer until wce_ctx_destroy. */
 int wce_ctx_reserve(wce_ctx *ctx, int64_t n_frames);
+int wce_ctx_reserve_stream(wce_ctx *ctx, int64_t n_frames, void *stream);
 
 /* Run the estimators selected in `mask` over all frames, asynchronously on
  * `stream`.  Replaces the per-frame calls of main.c:37-54 (and the frame
