@@ -150,3 +150,19 @@ def test_c_host_cli_runs():
     r = subprocess.run([cli, "4096", "textbook", "2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "frames/s" in r.stdout and "front end" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [("65536", "textbook", "5"), ("1001", "ref", "3")])
+def test_c_host_multi_device_runs(args):
+    """tools/wce_multi.c, one C process over every visible GPU through the C
+    ABI (RCCL state broadcast, wce_shard, nonfinite guard, shard-boundary
+    frames recomputed on device 0): exits 0."""
+    import subprocess
+    exe = os.path.join(REPO, "tools", "wce_multi")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", os.path.join(REPO, "80211parallelestimation_amd", "csrc"), "multi"])
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "frames/s aggregate" in r.stdout and "non-finite frames (max over devices): 0;" in r.stdout
+    assert "mismatching device 0: 0" in r.stdout
