@@ -23,6 +23,7 @@ table = f"""| Quantity | Value |
 | LS config 2 (LT_LS + PS_Linear), 1,048,576 frames | {d['ls_config2']['b1048576']['achieved_GBs'] / 1000:.2f} TB/s algorithmic = {100 * d['ls_config2']['b1048576']['frac']:.0f}% of 8 TB/s; {d['ls_config2']['b1048576'].get('real_GBs', 0) / 1000:.2f} TB/s of PMC-measured HBM traffic (pilot sectors counted); {d['ls_config2']['b1048576']['frames_per_s']:.2g} frames/s |
 | LS config 2, 65,536 frames (MALL-resident) | {d['ls_config2']['b65536']['achieved_GBs'] / 1000:.2f} TB/s, {d['ls_config2']['b65536']['frames_per_s']:.2g} frames/s |
 | front end, 65,536 frames × 15 blocks | {d['front_end']['blocks']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['front_end']['blocks']['frac']:.1f}% of 8 TB/s (PMC traffic = algorithmic bytes to 1e-4); LTF {d['front_end']['preamble']['achieved_GBs'] / 1000:.2f} TB/s |
+| non-finite guard (`wce_nonfinite_scan`), 1,048,576 LT_LS outputs | {d['ls_config2']['nonfinite_scan']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['ls_config2']['nonfinite_scan']['frac']:.1f}% of 8 TB/s; headline output non-finite frames: {d['nonfinite_frames']} |
 | small batches (1,024 frames, all 5 + eq) | {d['small_batch']['direct']['us_per_call']:.0f} µs per call direct, {d['small_batch']['plan']['us_per_call']:.0f} µs as a replayed HIP-graph plan |
 | CPU baseline (oracle fp64 port, 16 host cores, dense path) | {d['cpu_baseline']['value']:.2g} MMSE frames/s (4–6e5, host-load dependent) |
 """
