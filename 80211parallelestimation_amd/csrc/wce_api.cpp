@@ -732,6 +732,12 @@ int wce_event_elapsed_ms(float *ms, void *a, void *b)
 
 }  // extern "C"
 
+extern "C" int wce_debug_set_flat_chunk(long long frames)
+{
+    const int rc = wce::set_flat_chunk(frames);
+    return rc ? fail(rc, "flat chunk: 0, or a multiple of 32 in [32, 2^26]") : WCE_OK;
+}
+
 // ---- internal hooks for wce_multi.cpp (wce_internal.h)
 namespace wce {
 int api_fail(int code, const char *what) { return fail(code, what); }

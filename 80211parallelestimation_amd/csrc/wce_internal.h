@@ -128,6 +128,7 @@ int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, doub
 // H[f] = cu_f * mean_b dots[f*nb + b]  (per-frame covariance, MATLAB averaging)
 int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
+int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
 int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,
                           unsigned long long *n_bad, void *stream);
 

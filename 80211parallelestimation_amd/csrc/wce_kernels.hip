@@ -259,6 +259,18 @@ constexpr int FLAT_CHUNK = 64 * FLAT_U;                 // 512
 constexpr int FLAT_FR = (FLAT_CHUNK - 1) / NSC + 2;     // frames one chunk can touch: 11
 static_assert(4 * FLAT_FR <= 64, "one pilot per lane");
 constexpr int64_t FLAT_MAX_FRAMES = 1ll << 26;          // per launch: e < 2^32
+// frames per launch of the flat kernels: FLAT_MAX_FRAMES, or a smaller
+// multiple of 32 set by wce_debug_set_flat_chunk so that tests reach the
+// multi-launch path (f_begin > 0) at sizes a test can afford
+static int64_t g_flat_chunk = FLAT_MAX_FRAMES;
+static inline int64_t flat_chunk() { return __atomic_load_n(&g_flat_chunk, __ATOMIC_RELAXED); }
+int set_flat_chunk(int64_t frames)
+{
+    if (frames == 0) frames = FLAT_MAX_FRAMES;
+    if (frames < 32 || frames > FLAT_MAX_FRAMES || frames % 32) return WCE_EINVAL;
+    __atomic_store_n(&g_flat_chunk, frames, __ATOMIC_RELAXED);
+    return WCE_OK;
+}
 
 __global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ st, LsArgs a, int64_t f_begin,
                                                       uint32_t nfr)
@@ -1274,8 +1286,8 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
     const dim3 g((unsigned)blocks), b(256);
     if (WCE_LS_FLAT && !a.matlab && !eq &&
         (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0) {
-        for (int64_t f0 = 0; f0 < a.n; f0 += FLAT_MAX_FRAMES) {
-            const int64_t nf = a.n - f0 < FLAT_MAX_FRAMES ? a.n - f0 : FLAT_MAX_FRAMES;
+        for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
+            const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
             if (fb > 256 * 8) fb = 256 * 8;      // grid-stride the rest
@@ -1308,8 +1320,8 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     const dim3 g((unsigned)waves), b(64);
     hipStream_t s = (hipStream_t)stream;
     if (WCE_REF_FLAT && a.hout && a.ref_pilots && !a.split) {
-        for (int64_t f0 = 0; f0 < a.n; f0 += FLAT_MAX_FRAMES) {
-            const int64_t nf = a.n - f0 < FLAT_MAX_FRAMES ? a.n - f0 : FLAT_MAX_FRAMES;
+        for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
+            const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
             if (fb > 256 * 8) fb = 256 * 8;
@@ -1394,8 +1406,8 @@ int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, 
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(bits, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s) != hipSuccess) return WCE_EHIP;
     if (n_bad && hipMemsetAsync(n_bad, 0, sizeof(*n_bad), s) != hipSuccess) return WCE_EHIP;
-    for (int64_t f0 = 0; f0 < n; f0 += FLAT_MAX_FRAMES) {     // f0 % 32 == 0: words never straddle launches
-        const int64_t nf = n - f0 < FLAT_MAX_FRAMES ? n - f0 : FLAT_MAX_FRAMES;
+    for (int64_t f0 = 0, fc = flat_chunk(); f0 < n; f0 += fc) {   // fc % 32 == 0: words never straddle launches
+        const int64_t nf = n - f0 < fc ? n - f0 : fc;
         int64_t blocks = (nf * NSC + 255) / 256;
         if (blocks > 256 * 8) blocks = 256 * 8;
         if (f32)

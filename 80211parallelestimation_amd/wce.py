@@ -98,6 +98,7 @@ ABI = {
     "wce_state_build_cov": [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_double],
     "wce_debug_set_fusion": [c_void_p, c_int],
     "wce_debug_set_border_dot": [c_void_p, c_int],
+    "wce_debug_set_flat_chunk": [ctypes.c_int64],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],

@@ -19,6 +19,11 @@ int wce_debug_set_fusion(struct wce_ctx *ctx, int on);
  * bordered row replaces the back-substitution and the C W product; on by
  * default.  Off: back-substitution + MFMA apply (shared modes). */
 int wce_debug_set_border_dot(struct wce_ctx *ctx, int on);
+/* Frames per launch of the flat-index kernels (LT_LS + PS_Linear, REF
+ * PS_MMSE, the non-finite scan): 2^26 by default, so that 53 * frames < 2^32;
+ * a smaller multiple of 32 makes tests reach the multi-launch path at small
+ * sizes.  0 restores the default.  Process-wide. */
+int wce_debug_set_flat_chunk(long long frames);
 #ifdef __cplusplus
 }
 #endif
