@@ -705,6 +705,23 @@ int wce_memcpy_dtod(void *d, const void *s, size_t b, void *st)
     return WCE_OK;
 }
 int wce_memset(void *d, int v, size_t b) { HIPCHECK(hipMemset(d, v, b), "hipMemset"); return WCE_OK; }
+int wce_host_alloc(void **p, size_t b)
+{
+    if (!p) return fail(WCE_EINVAL, "null pointer");
+    HIPCHECK(hipHostMalloc(p, b, hipHostMallocDefault), "hipHostMalloc");
+    return WCE_OK;
+}
+int wce_host_free(void *p) { HIPCHECK(hipHostFree(p), "hipHostFree"); return WCE_OK; }
+int wce_memcpy_htod_async(void *d, const void *s, size_t b, void *st)
+{
+    HIPCHECK(hipMemcpyAsync(d, s, b, hipMemcpyHostToDevice, (hipStream_t)st), "htod async");
+    return WCE_OK;
+}
+int wce_memcpy_dtoh_async(void *d, const void *s, size_t b, void *st)
+{
+    HIPCHECK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToHost, (hipStream_t)st), "dtoh async");
+    return WCE_OK;
+}
 int wce_stream_create(void **s)
 {
     hipStream_t st;

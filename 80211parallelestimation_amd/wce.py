@@ -133,6 +133,10 @@ ABI = {
     "wce_memcpy_dtoh": [c_void_p, c_void_p, c_size_t],
     "wce_memcpy_dtod": [c_void_p, c_void_p, c_size_t, c_void_p],
     "wce_memset": [c_void_p, c_int, c_size_t],
+    "wce_host_alloc": [POINTER(c_void_p), c_size_t],
+    "wce_host_free": [c_void_p],
+    "wce_memcpy_htod_async": [c_void_p, c_void_p, c_size_t, c_void_p],
+    "wce_memcpy_dtoh_async": [c_void_p, c_void_p, c_size_t, c_void_p],
     "wce_stream_create": [POINTER(c_void_p)],
     "wce_stream_destroy": [c_void_p],
     "wce_stream_synchronize": [c_void_p],
@@ -186,6 +190,36 @@ def device_count() -> int:
 
 def _as_c128(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.complex128))
+
+
+class PinnedArray:
+    """Page-locked host memory (wce_host_alloc) with a numpy view, for
+    stream-ordered copies that overlap estimation."""
+
+    def __init__(self, shape, dtype=np.complex128):
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        self.ptr = c_void_p()
+        _check(load().wce_host_alloc(byref(self.ptr), max(self.nbytes, 16)), "wce_host_alloc")
+        buf = (ctypes.c_char * max(self.nbytes, 16)).from_address(self.ptr.value)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=int(np.prod(self.shape))).reshape(self.shape)
+
+    @property
+    def addr(self) -> int:
+        return self.ptr.value
+
+    def free(self):
+        if self.ptr is not None and self.ptr.value:
+            self.array = None
+            _lib.wce_host_free(self.ptr)
+            self.ptr = c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # pragma: no cover
+            pass
 
 
 class DeviceArray:

@@ -297,6 +297,12 @@ int wce_memcpy_htod(void *dst, const void *src, size_t bytes);
 int wce_memcpy_dtoh(void *dst, const void *src, size_t bytes);
 int wce_memcpy_dtod(void *dst, const void *src, size_t bytes, void *stream);
 int wce_memset(void *dst, int value, size_t bytes);
+/* pinned (page-locked) host memory and stream-ordered copies, for hosts that
+ * keep frames in host memory and overlap PCIe transfers with estimation */
+int wce_host_alloc(void **ptr, size_t bytes);
+int wce_host_free(void *ptr);
+int wce_memcpy_htod_async(void *dst, const void *src, size_t bytes, void *stream);
+int wce_memcpy_dtoh_async(void *dst, const void *src, size_t bytes, void *stream);
 int wce_stream_create(void **stream);
 int wce_stream_destroy(void *stream);
 int wce_stream_synchronize(void *stream);

@@ -137,3 +137,37 @@ def test_reserve_stream(gpu_wce, golden):
     _call(wce, ctx, b, 4096, wce.PS_MMSE | wce.FRAME_COV, 0, s.handle)
     s.synchronize()
     assert np.isfinite(b[3].numpy().view(np.float64)).all()
+
+
+def test_pinned_host_pipeline(gpu_wce, golden):
+    """Frames in pinned host memory, chunks round-robin over 2 streams
+    (wce_memcpy_htod_async -> estimate -> wce_memcpy_dtoh_async): the host
+    result equals the device-resident call bit for bit."""
+    wce = gpu_wce
+    inp = golden["inputs"]
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK, device=0)
+    n, c = 4096, 1024
+    tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+    ctx.synth(tx, rx, None, n, seed=3)
+    Hd = wce.DeviceArray((n, N), zero=True)
+    ctx.estimate(ctx.frames(tx, rx, n), wce.Outputs(None, None, None, None, Hd.addr, None, N, 0, 0, 0, 0),
+                 wce.PS_MMSE)
+    wce.synchronize()
+    txh, rxh, hh = wce.PinnedArray((n, N)), wce.PinnedArray((n, N)), wce.PinnedArray((n, N))
+    txh.array[:] = tx.numpy()[:, 0]
+    rxh.array[:] = rx.numpy()[:, 0]
+    hh.array[:] = np.nan
+    lib = wce.load()
+    streams = [wce.Stream(), wce.Stream()]
+    bufs = [[wce.DeviceArray((c, N)) for _ in range(3)] for _ in streams]
+    nb = c * N * 16
+    for i in range(n // c):
+        s, (dt, dr, dh) = streams[i % 2].handle, bufs[i % 2]
+        assert lib.wce_memcpy_htod_async(dt.addr, txh.addr + i * nb, nb, s) == 0
+        assert lib.wce_memcpy_htod_async(dr.addr, rxh.addr + i * nb, nb, s) == 0
+        ctx.estimate(ctx.frames(dt, dr, c, frame_stride=N, block_stride=N),
+                     wce.Outputs(None, None, None, None, dh.addr, None, N, 0, 0, 0, 0), wce.PS_MMSE, s)
+        assert lib.wce_memcpy_dtoh_async(hh.addr + i * nb, dh.addr, nb, s) == 0
+    for st in streams:
+        st.synchronize()
+    assert np.array_equal(hh.array, Hd.numpy())

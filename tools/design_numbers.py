@@ -11,6 +11,11 @@ d = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_bench.json")))
 pm = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_pmc_headline.json")))
 r = d["roofline"]
 refc = d["cpu_baseline"].get("reference_code", {})
+hp = d.get("host_pipeline")
+host_row = (f"| headline from pinned HOST memory (PCIe-inclusive; never `value`) | {hp['frames_per_s']:.3g} frames/s, "
+            f"{hp['pcie_GBs']:.0f} GB/s over PCIe ({hp['pcie_bytes_per_frame']} B per frame: tx, rx block 0 in, H out), "
+            f"{hp['ms_per_batch']:.2f} ms per 65,536 frames; bit-identical to the device-resident path: {hp['bit_identical_to_device_path']} |"
+            if hp else "| headline from pinned host memory | not measured in this bench line |")
 table = f"""| Quantity | Value |
 |---|---|
 | MMSE frames/s, TEXTBOOK (headline) | **{d['value']:.3g}** (target ≥1e7) |
@@ -25,6 +30,7 @@ table = f"""| Quantity | Value |
 | front end, 65,536 frames × 15 blocks | {d['front_end']['blocks']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['front_end']['blocks']['frac']:.1f}% of 8 TB/s (PMC traffic = algorithmic bytes to 1e-4); LTF {d['front_end']['preamble']['achieved_GBs'] / 1000:.2f} TB/s |
 | non-finite guard (`wce_nonfinite_scan`), 1,048,576 LT_LS outputs | {d['ls_config2']['nonfinite_scan']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['ls_config2']['nonfinite_scan']['frac']:.1f}% of 8 TB/s; headline output non-finite frames: {d['nonfinite_frames']} |
 | small batches (1,024 frames, all 5 + eq) | {d['small_batch']['direct']['us_per_call']:.0f} µs per call direct, {d['small_batch']['plan']['us_per_call']:.0f} µs as a replayed HIP-graph plan |
+{host_row}
 | CPU baseline (oracle fp64 port, 16 host cores, dense path) | {d['cpu_baseline']['value']:.2g} MMSE frames/s (4–6e5, host-load dependent) |
 """
 if refc:
