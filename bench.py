@@ -570,6 +570,16 @@ def cpu_reference(budget_s):
     lib.refh_bench_ls.argtypes = [ctypes.c_int] + [P] * 6
     lib.refh_bench_mmse.restype = ctypes.c_double
     lib.refh_bench_mmse.argtypes = [ctypes.c_int, P, P, P, ctypes.c_double, P, P, P]
+    has_omp = hasattr(lib, "refh_bench_ls_omp")
+    if has_omp:
+        lib.refh_bench_ls_omp.restype = ctypes.c_double
+        lib.refh_bench_ls_omp.argtypes = [ctypes.c_int, ctypes.c_int] + [P] * 6
+        lib.refh_bench_mmse_omp.restype = ctypes.c_double
+        lib.refh_bench_mmse_omp.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_double, P, P, P]
+    try:
+        cores = max(1, min(len(os.sched_getaffinity(0)), 16))
+    except AttributeError:  # pragma: no cover
+        cores = max(1, min(os.cpu_count() or 1, 16))
     LD = np.clongdouble
     inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
     ref = dict(np.load(os.path.join(REPO, "tests", "golden", "ref_vectors.npz")))
@@ -587,13 +597,24 @@ def cpu_reference(budget_s):
     h1, h2 = np.zeros((n, N), LD), np.zeros((n, N), LD)
     t = lib.refh_bench_ls(n, p(tpre), p(pre), p(tx), p(rx), p(h1), p(h2))
     out["ls_config2"] = {"value": n / t, "unit": "frames/s", "sample": f"{n} frames, {t:.2f} s"}
+    if has_omp:
+        t = lib.refh_bench_ls_omp(n, cores, p(tpre), p(pre), p(tx), p(rx), p(h1), p(h2))
+        out["ls_config2_omp"] = {"value": n / t, "unit": "frames/s", "cores": cores,
+                                 "sample": f"{n} frames, {t:.3f} s, the reference's functions in a "
+                                           f"frames-parallel OpenMP loop (its own OpenMP driver crashes)"}
     F = np.ascontiguousarray(oracle_py.from_split(ref["F"]))
     invF = np.ascontiguousarray(oracle_py.from_split(ref["invF"]))
     hls = np.ascontiguousarray(oracle_py.lt_ls(inp["tx_pre"], inp["rx_pre"]).astype(LD))
     H = np.zeros((n, N), LD)
     t1 = lib.refh_bench_mmse(1, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(invF), p(H))
-    m = int(max(1, min(n, budget_s / max(t1, 1e-6))))
+    m = int(max(1, min(n, 0.5 * budget_s / max(t1, 1e-6))))
     t = lib.refh_bench_mmse(m, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(invF), p(H))
+    if has_omp:
+        mo = int(max(cores, min(n, 0.5 * budget_s * cores / max(t1, 1e-6))))
+        to = lib.refh_bench_mmse_omp(mo, cores, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(invF), p(H))
+        out["mmse_ref_mode_omp"] = {"value": mo / to, "unit": "frames/s", "cores": cores,
+                                    "sample": f"{mo} frames, {to:.2f} s, frames-parallel OpenMP loop over the "
+                                              f"reference's per-frame MMSE"}
     out["mmse_ref_mode"] = {"value": m / t, "unit": "frames/s", "sample": f"{m} frames, {t:.2f} s",
                             "note": "the reference's literal PS_MMSE also spends ~4 s per frame inverting F "
                                     "and returns NaN; both are removed here"}

@@ -135,4 +135,31 @@ double refh_bench_mmse(int n, ldc *tx, ldc *rx, ldc *F, double ow2, ldc *H_ls, l
     return omp_get_wtime() - t0;
 }
 
+// The same two loops with the frames split over `threads` OpenMP threads:
+// the reference's per-frame functions touch only their own arguments (and
+// malloc), so a frames-parallel loop over them is race-free -- unlike the
+// reference's own OpenMP driver (main_openmp.c), which crashes.
+double refh_bench_ls_omp(int n, int threads, ldc *tx_pre, ldc *rx_pre, ldc *tx, ldc *rx, ldc *H_lt, ldc *H_lin)
+{
+    const double t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int f = 0; f < n; f++) {
+        const size_t o = (size_t)f * SAMPUTIL;
+        WiFi_channel_estimation_LT_LS(tx_pre, rx_pre + o, H_lt + o);
+        WiFi_channel_estimation_PS_Linear(tx + o, rx + o, H_lin + o);
+    }
+    return omp_get_wtime() - t0;
+}
+
+double refh_bench_mmse_omp(int n, int threads, ldc *tx, ldc *rx, ldc *F, double ow2, ldc *H_ls, ldc *invF, ldc *H)
+{
+    const double t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+    for (int f = 0; f < n; f++) {
+        const size_t o = (size_t)f * SAMPUTIL;
+        refh_mmse_repaired(tx + o, rx + o, F, ow2, H_ls, invF, H + o, NULL);
+    }
+    return omp_get_wtime() - t0;
+}
+
 }  // extern "C"

@@ -37,6 +37,10 @@ if refc:
     table += (f"| the reference's own code (`oracle/_ref`, 1 core) | LT_LS + PS_Linear {refc['ls_config2']['value']:.2g} frames/s; "
               f"REF-mode PS_MMSE through its matrix routines {refc['mmse_ref_mode']['value']:.0f} frames/s "
               f"(NaN inverse repaired, per-frame 4-s `inverse(F)` hoisted) |\n")
+    if "ls_config2_omp" in refc:
+        table += (f"| the reference's own functions, frames-parallel OpenMP loop ({refc['ls_config2_omp']['cores']} host cores; "
+                  f"its own OpenMP driver crashes) | LT_LS + PS_Linear {refc['ls_config2_omp']['value']:.2g} frames/s; "
+                  f"REF-mode PS_MMSE {refc['mmse_ref_mode_omp']['value']:.0f} frames/s |\n")
 table += "| reference `main.c` MMSE as written | ~0.004 frames/s, 1 core, NaN output; best published number 0.18 frames/s over 20 MPI ranks |\n"
 k = [x for x in pm if x.endswith("mmse_solve_fc_kernel")]
 pmc = ""
