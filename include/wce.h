@@ -189,9 +189,12 @@ int wce_estimate(wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
  * captured into a HIP graph once and replayed with a single graph launch --
  * for serving loops that re-run small batches into the same buffers, where
  * per-call host checks and kernel launch latency dominate.  Arguments are
- * validated and the workspace sized at creation; the plan keeps raw
- * pointers, so the buffers must outlive it.  NULL stream: the plan uses a
- * private stream for capture; launches go to the stream given. */
+ * validated and the plan's own workspace sized at creation; the plan keeps
+ * raw pointers, so the buffers and the ctx (its device state) must outlive
+ * it.  Capture runs on a private stream; launches go to the stream given, and
+ * replays may run beside direct calls on other streams.  A replay is one
+ * graph launch: it pays off where a call chains several kernels (MATLAB
+ * semantics, FRAME_COV); a single-kernel call is as fast direct. */
 typedef struct wce_plan wce_plan;
 int wce_plan_create(wce_plan **plan, wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
                     uint32_t mask);
