@@ -435,9 +435,20 @@ def bench_small_batch(wce, ctx, stream, n=1024, calls=200):
     eq = wce.DeviceArray((n, NBLK, N))
     o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, 0)
     fr = ctx.frames(tx, rx, n, rx_pre=pre)
-    plan = ctx.plan(fr, o, wce.ALL)
-    res = {"workload": f"{n} frames per call, all 5 estimators + equalization, per-frame preamble", "calls": calls}
-    for label, f in (("direct", lambda: ctx.estimate(fr, o, wce.ALL, s)), ("plan", lambda: plan.launch(s))):
+    # a multi-kernel call: MATLAB semantics + per-frame covariance (LT_LS,
+    # the factor matvec, 4 solve waves per frame, the block average)
+    frm = ctx.frames(tx, rx, n, rx_pre=pre, semantics=wce.SEM_MATLAB)
+    om = wce.Outputs(None, None, None, None, outs[4].addr, None, N, 0, 0, 0, 0)
+    mm = wce.PS_MMSE | wce.FRAME_COV
+    ctx.reserve(n)
+    plan, planm = ctx.plan(fr, o, wce.ALL), ctx.plan(frm, om, mm)
+    res = {"workload": f"{n} frames per call, all 5 estimators + equalization, per-frame preamble (one fused "
+                       f"kernel); matlab_frame_cov: PS_MMSE with MATLAB semantics and per-frame covariance "
+                       f"(several kernels per call)", "calls": calls}
+    cases = (("direct", lambda: ctx.estimate(fr, o, wce.ALL, s)), ("plan", lambda: plan.launch(s)),
+             ("matlab_frame_cov_direct", lambda: ctx.estimate(frm, om, mm, s)),
+             ("matlab_frame_cov_plan", lambda: planm.launch(s)))
+    for label, f in cases:
         for _ in range(20):
             f()
         stream.synchronize()
@@ -448,6 +459,7 @@ def bench_small_batch(wce, ctx, stream, n=1024, calls=200):
         dt = (time.perf_counter() - t0) / calls
         res[label] = {"us_per_call": dt * 1e6, "frames_per_s": n / dt}
     plan.close()
+    planm.close()
     return res
 
 

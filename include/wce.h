@@ -193,8 +193,9 @@ int wce_estimate(wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
  * raw pointers, so the buffers and the ctx (its device state) must outlive
  * it.  Capture runs on a private stream; launches go to the stream given, and
  * replays may run beside direct calls on other streams.  A replay is one
- * graph launch: it pays off where a call chains several kernels (MATLAB
- * semantics, FRAME_COV); a single-kernel call is as fast direct. */
+ * graph launch; on ROCm 7 that measured slightly SLOWER than the direct
+ * call's launches (bench small_batch), so a plan buys validation once and a
+ * fixed argument set, not speed. */
 typedef struct wce_plan wce_plan;
 int wce_plan_create(wce_plan **plan, wce_ctx *ctx, const wce_frames *in, const wce_outputs *out,
                     uint32_t mask);

@@ -16,6 +16,9 @@ host_row = (f"| headline from pinned HOST memory (PCIe-inclusive; never `value`)
             f"{hp['pcie_GBs']:.0f} GB/s over PCIe ({hp['pcie_bytes_per_frame']} B per frame: tx, rx block 0 in, H out), "
             f"{hp['ms_per_batch']:.2f} ms per 65,536 frames; bit-identical to the device-resident path: {hp['bit_identical_to_device_path']} |"
             if hp else "| headline from pinned host memory | not measured in this bench line |")
+sb = d["small_batch"]
+mlsb = (f"; MATLAB + FRAME_COV (several kernels): {sb['matlab_frame_cov_direct']['us_per_call']:.0f} µs direct, "
+        f"{sb['matlab_frame_cov_plan']['us_per_call']:.0f} µs as a plan" if "matlab_frame_cov_plan" in sb else "")
 table = f"""| Quantity | Value |
 |---|---|
 | MMSE frames/s, TEXTBOOK (headline) | **{d['value']:.3g}** (target ≥1e7) |
@@ -29,7 +32,7 @@ table = f"""| Quantity | Value |
 | LS config 2, 65,536 frames (MALL-resident) | {d['ls_config2']['b65536']['achieved_GBs'] / 1000:.2f} TB/s, {d['ls_config2']['b65536']['frames_per_s']:.2g} frames/s |
 | front end, 65,536 frames × 15 blocks | {d['front_end']['blocks']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['front_end']['blocks']['frac']:.1f}% of 8 TB/s (PMC traffic = algorithmic bytes to 1e-4); LTF {d['front_end']['preamble']['achieved_GBs'] / 1000:.2f} TB/s |
 | non-finite guard (`wce_nonfinite_scan`), 1,048,576 LT_LS outputs | {d['ls_config2']['nonfinite_scan']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['ls_config2']['nonfinite_scan']['frac']:.1f}% of 8 TB/s; headline output non-finite frames: {d['nonfinite_frames']} |
-| small batches (1,024 frames, all 5 + eq) | {d['small_batch']['direct']['us_per_call']:.0f} µs per call direct, {d['small_batch']['plan']['us_per_call']:.0f} µs as a replayed HIP-graph plan |
+| small batches (1,024 frames, all 5 + eq) | {d['small_batch']['direct']['us_per_call']:.0f} µs per call direct, {d['small_batch']['plan']['us_per_call']:.0f} µs as a replayed HIP-graph plan{mlsb} |
 {host_row}
 | CPU baseline (oracle fp64 port, 16 host cores, dense path) | {d['cpu_baseline']['value']:.2g} MMSE frames/s (4–6e5, host-load dependent) |
 """
