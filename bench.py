@@ -309,6 +309,10 @@ def main():
             "frames_per_s_per_gpu": B / (t_other * 1e-3), "ms_per_step": t_other}
         del ctx2
 
+        # BASELINE configs[3]: 1,048,576 frames in total, sharded over the
+        # ranks (strong scaling), same kernel; all ranks, barrier + max
+        res["config4"] = bench_config4(wce, ctx, dist, stream, hs, max(5, args.steps // 5))
+
         # LS path (config 2: LT_LS + PS_Linear), HBM-bound
         if dist.rank == 0:
             res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
@@ -329,6 +333,34 @@ def main():
     if dist.rank == 0:
         print(json.dumps(res), flush=True)
     dist.close()
+
+
+def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20):
+    """BASELINE configs[3]: `total` frames sharded contiguously over the
+    ranks (wce_shard's partition), each rank generating its shard from the
+    global frame index; timed like the headline (barrier + device sync on
+    both sides, max over ranks).  Strong scaling: total work fixed."""
+    import importlib
+    multi = importlib.import_module("80211parallelestimation_amd.multi")
+    first, count = multi.shard(total, dist.world, dist.rank)
+    tx, rx = wce.DeviceArray((count, NBLK, N)), wce.DeviceArray((count, NBLK, N))
+    ctx.synth(tx, rx, None, count, first_frame=first, seed=0x80211, h_shared=hs, stream=stream.handle)
+    H = wce.DeviceArray((count, N))
+    fr = ctx.frames(tx, rx, count)
+    o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+    for _ in range(3):
+        ctx.estimate(fr, o, wce.PS_MMSE, stream.handle)
+    stream.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.estimate(fr, o, wce.PS_MMSE, stream.handle)
+    stream.synchronize()
+    dist.barrier()
+    dt = dist.max(time.perf_counter() - t0) / steps
+    return {"workload": "BASELINE configs[3]: PS_MMSE over 1,048,576 frames sharded over the ranks",
+            "global_frames": total, "frames_per_gpu": count, "n_gpus": dist.world, "steps": steps,
+            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong"}
 
 
 def bench_ls(wce, ctx, stream, n, reps):
