@@ -60,3 +60,19 @@ def test_rocprof_headline_average_agrees(line):
     assert k, "headline kernel missing from the rocprof summary"
     avg_ms = float(k[0]["AverageNs"]) * 1e-6
     assert abs(avg_ms - line["roofline"]["avg_launch_ms"]) / avg_ms < 0.10, (avg_ms, line["roofline"]["avg_launch_ms"])
+
+
+def test_extra_legs_consistent(line):
+    """The extra legs that carry their own arithmetic agree with it: configs[3]
+    (strong scaling over 1,048,576 frames), the PCIe-inclusive host pipeline,
+    and the non-finite check of the headline output."""
+    c4 = line.get("config4")
+    if c4:
+        assert c4["global_frames"] == 1 << 20 and c4["scaling"] == "strong"
+        assert abs(c4["frames_per_s"] - c4["global_frames"] / (c4["ms_per_step"] * 1e-3)) / c4["frames_per_s"] < 1e-6
+    hp = line.get("host_pipeline")
+    if hp:
+        assert hp["bit_identical_to_device_path"] is True
+        assert hp["frames_per_s"] < line["value"]          # PCIe-bound, never the headline
+    if "nonfinite_frames" in line:
+        assert line["nonfinite_frames"] == 0
