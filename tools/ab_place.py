@@ -36,7 +36,7 @@ layouts = {
     "rnd1": list(np.random.default_rng(1).integers(0, 64, 5) * 4096),
     "rnd2": list(np.random.default_rng(2).integers(0, 64, 5) * 4096),
 }
-total = 5 * A + max(sum(v) for v in layouts.values()) + 4 * MiB
+total = 5 * A + max(sum(v) for v in layouts.values()) + 5 * 32 * MiB + 4 * MiB
 buf = wce.DeviceArray((total,), dtype=np.uint8)
 base = (buf.addr + 2 * MiB - 1) // (2 * MiB) * (2 * MiB)
 rng = np.random.default_rng(1)
@@ -54,6 +54,17 @@ for name, gaps in layouts.items():
         p += A + int(g)
     plans[name] = addrs
     res[name] = []
+# every stream start rounded up to an alignment (inside the same allocation)
+for al in (64 * 1024, 2 * MiB, 32 * MiB):
+    addrs, p = [], base
+    for _ in range(5):
+        p = (p + al - 1) // al * al
+        addrs.append(p)
+        p += A
+    name = f"align{al // 1024}K"
+    plans[name] = addrs
+    res[name] = []
+    assert p <= buf.addr + total
 for rnd in range(args.rounds + 1):
     for name, (tx, rx, pre, lt, lin) in plans.items():
         if rnd == 0:
