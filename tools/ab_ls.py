@@ -15,6 +15,7 @@ ap.add_argument("--frames", type=int, default=1 << 20)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--mask", type=int, default=3)
 ap.add_argument("--ostride", type=int, default=53, help="output row stride (complex); 64 = 1 KiB-aligned rows")
+ap.add_argument("--sets", type=int, default=1, help="independently allocated buffer sets, each timed with every variant")
 args = ap.parse_args()
 N = 53
 inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
@@ -34,19 +35,21 @@ for d in args.dirs:
     ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_REF)
     n = args.frames
     if not state:
-        # one set of device buffers for every variant: HBM placement moves the
-        # timing by ~10% between buffer sets, more than most variants differ
-        tx, rx, pre = m.DeviceArray((n, N)), m.DeviceArray((n, N)), m.DeviceArray((n, N))
-        for off in range(0, n, chunk):
-            k = min(chunk, n - off)
-            for dst, h in ((tx, txh), (rx, rxh), (pre, preh)):
-                lib.wce_memcpy_htod(dst.addr + off * N * 16, h[:k].ctypes.data, k * N * 16)
-        outs = [m.DeviceArray((n, args.ostride)) for _ in range(4)]
-    else:
-        tx, rx, pre, outs = state[0][6]
-    o = m.Outputs(*(x.addr for x in outs), None, None, args.ostride, 0, 0, 0, 0)
-    fr = ctx.frames(tx.addr, rx.addr, n, frame_stride=N, block_stride=N, rx_pre=pre.addr, pre_stride=N)
-    state.append((os.path.basename(d.rstrip("/")), m, ctx, fr, o, m.Stream(), (tx, rx, pre, outs)))
+        # buffer sets shared by every variant: HBM placement moves the timing by
+        # up to ~15% between allocations, more than most variants differ
+        bsets = []
+        for _ in range(args.sets):
+            tx, rx, pre = m.DeviceArray((n, N)), m.DeviceArray((n, N)), m.DeviceArray((n, N))
+            for off in range(0, n, chunk):
+                k = min(chunk, n - off)
+                for dst, h in ((tx, txh), (rx, rxh), (pre, preh)):
+                    lib.wce_memcpy_htod(dst.addr + off * N * 16, h[:k].ctypes.data, k * N * 16)
+            bsets.append((tx, rx, pre, [m.DeviceArray((n, args.ostride)) for _ in range(4)]))
+    for si, (tx, rx, pre, outs) in enumerate(bsets):
+        o = m.Outputs(*(x.addr for x in outs), None, None, args.ostride, 0, 0, 0, 0)
+        fr = ctx.frames(tx.addr, rx.addr, n, frame_stride=N, block_stride=N, rx_pre=pre.addr, pre_stride=N)
+        name = os.path.basename(d.rstrip("/")) + (f"@set{si}" if args.sets > 1 else "")
+        state.append((name, m, ctx, fr, o, m.Stream(), bsets))
 res = {s[0]: [] for s in state}
 for rnd in range(args.rounds + 1):
     for name, m, ctx, fr, o, st, _ in state:
