@@ -318,6 +318,7 @@ def main():
         # BASELINE configs[3]: 1,048,576 frames in total, sharded over the
         # ranks (strong scaling), same kernel; all ranks, barrier + max
         res["config4"] = bench_config4(wce, ctx, dist, stream, hs, max(5, args.steps // 5))
+        res["config5_sharded"] = bench_config5_sharded(wce, ctx, dist, stream, max(3, args.steps // 20))
 
         # LS path (config 2: LT_LS + PS_Linear), HBM-bound
         if dist.rank == 0:
@@ -339,6 +340,37 @@ def main():
     if dist.rank == 0:
         print(json.dumps(res), flush=True)
     dist.close()
+
+
+def bench_config5_sharded(wce, ctx, dist, stream, steps, total=1 << 20):
+    """BASELINE configs[4] as the config names it: all 5 estimators +
+    per-symbol equalization, fused, mixed precision (fp64 solve, LS family and
+    equalized symbols stored fp32), per-frame preambles, `total` frames
+    sharded over the ranks (strong scaling).  Timed like config4."""
+    import importlib
+    multi = importlib.import_module("80211parallelestimation_amd.multi")
+    first, count = multi.shard(total, dist.world, dist.rank)
+    s = stream.handle
+    tx, rx, pre = wce.DeviceArray((count, NBLK, N)), wce.DeviceArray((count, NBLK, N)), wce.DeviceArray((count, N))
+    ctx.synth(tx, rx, pre, count, first_frame=first, seed=0x80211, stream=s)
+    outs = [wce.DeviceArray((count, N), np.complex64) for _ in range(4)] + [wce.DeviceArray((count, N))]
+    eq = wce.DeviceArray((count, NBLK, N), np.complex64)
+    o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32)
+    fr = ctx.frames(tx, rx, count, rx_pre=pre)
+    for _ in range(3):
+        ctx.estimate(fr, o, wce.ALL, s)
+    stream.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.estimate(fr, o, wce.ALL, s)
+    stream.synchronize()
+    dist.barrier()
+    dt = dist.max(time.perf_counter() - t0) / steps
+    return {"workload": "BASELINE configs[4]: all 5 estimators + equalization fused, fp64 solve / fp32 LS and eq "
+                        "outputs, per-frame preambles, 1,048,576 frames sharded over the ranks",
+            "global_frames": total, "frames_per_gpu": count, "n_gpus": dist.world, "steps": steps,
+            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong"}
 
 
 def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20):

@@ -76,3 +76,10 @@ def test_extra_legs_consistent(line):
         assert hp["frames_per_s"] < line["value"]          # PCIe-bound, never the headline
     if "nonfinite_frames" in line:
         assert line["nonfinite_frames"] == 0
+
+
+def test_config5_sharded_consistent(line):
+    c5 = line.get("config5_sharded")
+    if c5:
+        assert c5["global_frames"] == 1 << 20 and c5["scaling"] == "strong"
+        assert abs(c5["frames_per_s"] - c5["global_frames"] / (c5["ms_per_step"] * 1e-3)) / c5["frames_per_s"] < 1e-6
