@@ -16,6 +16,14 @@ host_row = (f"| headline from pinned HOST memory (PCIe-inclusive; never `value`)
             f"{hp['pcie_GBs']:.0f} GB/s over PCIe ({hp['pcie_bytes_per_frame']} B per frame: tx, rx block 0 in, H out), "
             f"{hp['ms_per_batch']:.2f} ms per 65,536 frames; bit-identical to the device-resident path: {hp['bit_identical_to_device_path']} |"
             if hp else "| headline from pinned host memory | not measured in this bench line |")
+c4, c5s = d.get("config4"), d.get("config5_sharded")
+c4_row = ""
+if c4:
+    c4_row += (f"| BASELINE configs[3] batch (1,048,576 frames, sharded over {c4['n_gpus']} GPU(s), strong scaling) | "
+               f"{c4['frames_per_s']:.3g} frames/s |")
+if c5s:
+    c4_row += ("\n" if c4_row else "") + (f"| BASELINE configs[4] as named (1,048,576 frames, all 5 + eq fused, fp64 solve / fp32 LS, "
+               f"sharded over {c5s['n_gpus']} GPU(s)) | {c5s['frames_per_s']:.3g} frames/s |")
 sb = d["small_batch"]
 mlsb = (f"; MATLAB + FRAME_COV (several kernels): {sb['matlab_frame_cov_direct']['us_per_call']:.0f} µs direct, "
         f"{sb['matlab_frame_cov_plan']['us_per_call']:.0f} µs as a plan" if "matlab_frame_cov_plan" in sb else "")
@@ -23,6 +31,7 @@ table = f"""| Quantity | Value |
 |---|---|
 | MMSE frames/s, TEXTBOOK (headline) | **{d['value']:.3g}** (target ≥1e7) |
 | `mmse_solve_fc_kernel` (the whole step: one launch) | {r['avg_launch_ms']:.3f} ms per 65,536 frames. **{r['achieved']:.1f} TFLOP/s = {100 * r['frac']:.1f}%** of FP64 spec peak by SURVEY's F_alg. Executed flops: {r['achieved_executed']:.1f} TFLOP/s = {100 * r['achieved_executed'] / 78.6:.1f}% |
+{c4_row}
 | MMSE frames/s, REF (diagonal Ryy: no factorisation) | {d['ref_mode']['frames_per_s_per_gpu']:.3g} |
 | MMSE with a dense model covariance (COV: back-substitution + MFMA GEMM) | {d['cov_mode']['frames_per_s_per_gpu']:.3g} frames/s; solve {d['cov_mode']['solve_tflops']:.1f} TFLOP/s |
 | `matvec_kernel` as `H = C·W` (MFMA, COV mode) | {d['apply_kernel']['achieved_tflops']:.0f} TFLOP/s = {100 * d['apply_kernel']['frac_fp64_peak']:.0f}% of FP64 peak |
