@@ -698,11 +698,12 @@ __device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double
 
 // Panel KB in row form.  Entering: P = block column KB with P[0] = c_{8KB}
 // (scaled), c_{8KB} published.
-template <int KB>
+// K0 = 1: pivot 8KB is already eliminated (exact_first_step), c_{8KB+1} published.
+template <int KB, int K0 = 0>
 __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q, int lane)
 {
 #pragma unroll
-    for (int kq = 0; kq < 8; ++kq) {
+    for (int kq = K0; kq < 8; ++kq) {
         const int k = 8 * KB + kq;
         const double2 *col = s.u[k & 1];
         double2 *next = s.u[(k + 1) & 1];
@@ -758,6 +759,77 @@ __device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, 
     return make_double2(-sc.x, -sc.y);   // s = -S(54, 53)
 }
 
+// ---------------------------------------------------------------------
+// Exact first elimination step (the rank-1 read-out path).  Ryy = al be^T + b I
+// with al = a x o u, be = w o conj(x) = conj(al) / a (w = conj(u) whenever
+// a != 0).  Its cond is 1 + |al|^2 / b ~ 4e6 on the synthetic frames: rounding
+// the entries al_i be_j to fp64 alone perturbs s = (w o x)^T Ryy^-1 rx by up to
+// ~1e-10 norm-relative, and a plain fp64 factorisation reaches 1.7e-9 on frames
+// whose channel is unrelated to the preamble's (profiles/r01_accuracy_probe.txt).
+// All of that ill-conditioning is consumed by the first pivot: eliminating
+// pivot m leaves
+//     S_ij = al_i be_j (b / d0) + b [i == j],   d0 = al_m be_m + b,
+// whose rank-1 part is at most 52 b when m is the largest |al_m| (cond <= 53).
+// So S is formed directly from the factors -- never as the fp64 difference
+// al_i be_j - (al_i be_m)(al_m be_j) / d0 -- and so are the two bordered rows:
+//     row 53: conj(rx_j) - conj(rx_m) al_m be_j / d0
+//     row 54: rho_j - rho_m al_m be_j / d0 = w_j [x_j b/d0 + kap/d0 x_m (conj(x_m) x_j - x_m conj(x_j))]
+//             (rho = w o x, kap = a w_m u_m; the bracket has no cancellation)
+//     (54, 53): -rho_m rx_m / d0.
+// Pivot m is swapped with index 0 (s is invariant under a symmetric
+// permutation); index 0 then holds b on the diagonal and zeros elsewhere, so
+// the factorisation proper runs over pivots 1..52 of the 53 x 53 matrix.
+// LDS out: u[0] = al' (scaled by b/d0), u[1] = be', z = rx', blk = rho' and
+// blk[53] = the (54, 53) entry; all permuted, index 0 zero.
+// ---------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, 64));
+    return v;
+}
+
+__device__ __forceinline__ void exact_first_step(const SolveArgs &a, SolveLds &s, int64_t f, double ac, double bc)
+{
+    const int lane = threadIdx.x;
+    const bool act = lane < NSC;
+    const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
+    const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
+    const double2 xl = s.x[lane];
+    const double2 rxl = s.rx[lane];
+    const double2 al = cscale(cmul(xl, uf), ac);
+    const double2 be = cmul(wf, cconj(xl));
+    // pivot: the largest |al_l|^2 (float key, lane in the low 6 bits; ties and
+    // the last few mantissa bits do not matter for the choice)
+    const float mag = (float)(al.x * al.x + al.y * al.y);
+    const uint32_t key = act ? ((__float_as_uint(mag) & ~63u) | (uint32_t)lane) : 0u;
+    const int m = __builtin_amdgcn_readfirstlane((int)(wave_max_u32(key) & 63u));
+    const double2 alm = readlane_c(al, m), bem = readlane_c(be, m);
+    const double2 xm = readlane_c(xl, m), rxm = readlane_c(rxl, m);
+    const double2 um = readlane_c(uf, m), wm = readlane_c(wf, m);
+    const double d0 = (alm.x * bem.x - alm.y * bem.y) + bc;
+    const double r0 = rcp_nr(d0);
+    const double sc = bc * r0;
+    // row 53: rx'_l = rx_l - rx_m conj(al_m be_l) / d0
+    const double2 rxp = csub(rxl, cscale(cmul(rxm, cconj(cmul(alm, be))), r0));
+    // row 54: w_l [x_l b/d0 + (kap/d0) x_m 2i Im(conj(x_m) x_l)]
+    const double ti = 2.0 * (xm.x * xl.y - xm.y * xl.x);
+    const double2 kr = cscale(cmul(make_double2(ac * wm.x, ac * wm.y), um), r0);
+    const double2 ixm = make_double2(-xm.y * ti, xm.x * ti);   // x_m 2i Im(.)
+    double2 rhop = cmul(wf, cadd(cscale(xl, sc), cmul(kr, ixm)));
+    double2 alp = cscale(al, sc), bep = be, rxo = rxp;
+    if (lane == m) alp = bep = rxo = rhop = make_double2(0, 0);
+    if (lane == NSC) {   // the (54, 53) entry: -rho_m rx_m / d0
+        const double2 rhom = cmul(wm, xm);
+        rhop = cscale(cmul(rhom, rxm), -r0);
+    }
+    const int dst = lane == m ? 0 : (lane == 0 ? m : lane);
+    s.u[0][dst] = alp;
+    s.u[1][dst] = bep;
+    s.z[dst] = rxo;
+    s.blk[dst] = rhop;
+}
+
 #ifndef WCE_DOT_CHOL   // A/B: 0 = square-root-free LDL^H row panels (dot_panel)
 #define WCE_DOT_CHOL 1
 #endif
@@ -773,15 +845,7 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
-    {
-        const bool act = lane < NSC;
-        const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
-        const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
-        const double2 xl = s.x[lane];
-        s.u[0][lane] = cscale(cmul(xl, uf), ac);
-        s.u[1][lane] = cmul(wf, cconj(xl));
-        s.blk[lane] = cmul(wf, xl);
-    }
+    exact_first_step(a, s, f, ac, bc);
     wave_lds_sync();
     double2 A[RB][RB];
     double2 P[8];
@@ -794,7 +858,7 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
         }
         if (lane == NSC) {
 #pragma unroll
-            for (int c = 0; c < 8; ++c) P[c] = cconj(s.rx[c]);
+            for (int c = 0; c < 8; ++c) P[c] = cconj(s.z[c]);
         }
         if (lane == NSC + 1) {
 #pragma unroll
@@ -810,9 +874,9 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
 #pragma unroll
     for (int aa = 1; aa < RB - 1; ++aa) A[aa][aa].x += bdiag;
     A[RB - 1][RB - 1].x += (p == q && p < NSC - 8 * (RB - 1)) ? bc : 0.0;
-    if (p == NSC - 8 * (RB - 1)) {   // row 53 = conj(rx)
+    if (p == NSC - 8 * (RB - 1)) {   // row 53 = conj(rx'), rx after the exact first step
 #pragma unroll
-        for (int bb = 1; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
+        for (int bb = 1; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.z[q + 8 * bb]);
     }
     if (p == NSC + 1 - 8 * (RB - 1)) {   // row 54 = (w o x)^T
 #pragma unroll
@@ -821,10 +885,12 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     wave_lds_sync();   // s.u[0] is reused by the first publish
     if constexpr (WCE_DOT_CHOL) {
         static_assert(!WCE_DOT_CHOL || ROWP == RB - 1, "Cholesky panels: 0..5 in row form");
-        P[0] = cscale(P[0], rsq_nr(readlane_f64(P[0].x, 0)));
-        s.u[0][lane] = P[0];
+        // pivot 0 was eliminated exactly (column 0 is b e_0): the
+        // factorisation starts at pivot 1, whose column the build left final
+        P[1] = cscale(P[1], rsq_nr(readlane_f64(P[1].x, 1)));
+        s.u[1][lane] = P[1];
         wave_lds_sync();
-        chol_panel<0>(A, P, s, p, q, lane);
+        chol_panel<0, 1>(A, P, s, p, q, lane);
         chol_panel<1>(A, P, s, p, q, lane);
         chol_panel<2>(A, P, s, p, q, lane);
         chol_panel<3>(A, P, s, p, q, lane);
