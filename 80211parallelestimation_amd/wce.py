@@ -248,6 +248,18 @@ class DeviceArray:
             _check(_lib.wce_memcpy_dtoh(out.ctypes.data_as(c_void_p), self.ptr, self.nbytes), "wce_memcpy_dtoh")
         return out
 
+    def rows(self, first, count=1) -> np.ndarray:
+        """rows [first, first + count) of the leading axis, without copying the rest"""
+        first, count = int(first), int(count)
+        if first < 0 or count < 0 or first + count > self.shape[0]:
+            raise IndexError("rows out of range")
+        out = np.empty((count,) + self.shape[1:], self.dtype)
+        row = out.nbytes // max(count, 1)
+        if out.nbytes:
+            _check(_lib.wce_memcpy_dtoh(out.ctypes.data_as(c_void_p), c_void_p(self.addr + first * row), out.nbytes),
+                   "wce_memcpy_dtoh")
+        return out
+
     def free(self):
         if self.ptr is not None and self.ptr.value:
             _lib.wce_free(self.ptr)

@@ -39,10 +39,14 @@ FLOP_SOLVE_REF = FLOP_CHOL + FLOP_TRSV   # REF: a = 0, Ryy is the diagonal 2 ow2
 # what the rank-1 kernel (mmse_solve_fc_kernel) executes per frame: the LDL^H,
 # the rank-1 Ryy build (one complex product per lower-triangle element), the
 # two bordered forward solves; no back-substitution, no C W product
-FLOP_EXEC_R1 = FLOP_CHOL + 6.0 * N * (N + 1) / 2 + FLOP_TRSV
+# (round 2: pivot 0 is eliminated exactly from the rank-1 factors, the
+# Cholesky runs over the 52 x 52 trailing matrix)
+FLOP_EXEC_R1 = 4.0 / 3.0 * (N - 1) ** 3 + 6.0 * N * (N + 1) / 2 + FLOP_TRSV
 BYTES_FE_BLOCK = 64 * 16 + N * 16        # front end: 64 useful samples in (CP skipped) + 53 bins out
 BYTES_FE_PRE = 128 * 16 + N * 16 + 8     # two LTF copies in, preamble FFT + sigma^2 out
 BYTES_LS_CFG2 = 2672                     # LT_LS + PS_Linear: rx_pre 848 + pilots 128 + 2 x 848 out
+BYTES_REF_ALG = 8 * 16 + N * 16          # REF PS_MMSE: 4 tx + 4 rx pilots in, H out = 976
+BYTES_PILOT_SECTORS = 8 * 64             # the 8 pilot reads of a frame each fetch a whole 64-B sector
 PEAK_FP64_TFLOPS = 78.6                  # MI355X FP64 vector = FP64 matrix (spec)
 PEAK_HBM_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "MMSE-estimated 802.11 frames/sec (53 subcarriers) at 1/2/4/8 MI355X; % roofline"
@@ -129,39 +133,42 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def pmc_traffic(kernel: str, launches_frames: int, which: str = "pmc_summary"):
-    """HBM bytes per launch of `kernel` (a substring of the demangled name,
-    e.g. "mmse_solve_kernel<true>") from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_summary.json, tools/pmc_passes.sh): FETCH_SIZE (KiB, x2
-    for gfx950's half-counted 16-B/lane streaming reads, MI355X_MICROARCH.md
-    HBM) + WRITE_SIZE (KiB).  The summary was taken at 65,536 frames per launch."""
+def pmc_leg(leg: str, frames: int, write_bytes: float, tol: float = 0.02, waves: int = None):
+    """Per-dispatch PMC counters of one bench leg's dominant kernel from the
+    committed profiles/*_pmc_legs.json (tools/pmc_legs.sh: rocprofv3 --pmc over
+    tools/prof_leg.py, which launches ONLY that kernel, at exactly the bench's
+    launch size).  Used only if the profiled launches are this launch: the
+    recorded frames must equal `frames`, and either SQ_WAVES must equal
+    `waves` (when the caller knows the launch's wave count) or WRITE_SIZE
+    (exact for 16-B/lane streaming stores, MI355X_MICROARCH.md HBM) must equal
+    the launch's algorithmic output bytes `write_bytes` within `tol`.
+    Returns (counters, source file) or (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{which}.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_legs.json")))
     if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    keys = [k for k in d if kernel in k and "FETCH_SIZE" in d[k] and "WRITE_SIZE" in d[k]]
-    if not keys:
-        return None, None
-    k = d[sorted(keys, key=len)[0]]
-    b = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0
-    return b * launches_frames / 65536.0, os.path.basename(files[-1])
+        return None, "no profiles/*_pmc_legs.json"
+    d = json.load(open(files[-1])).get(leg)
+    if not d:
+        return None, f"leg {leg} not profiled"
+    if d["frames"] != frames:
+        return None, f"profiled at {d['frames']} frames, bench launch is {frames}"
+    k = d["counters"]
+    if waves is not None:
+        if abs(k.get("SQ_WAVES", -1) - waves) > 0.5:
+            return None, f"SQ_WAVES {k.get('SQ_WAVES')} is not this launch's {waves} waves"
+    elif "WRITE_SIZE" not in k or abs(k["WRITE_SIZE"] * 1024.0 - write_bytes) > tol * write_bytes:
+        return None, f"WRITE_SIZE {k.get('WRITE_SIZE')} KiB is not this launch's {write_bytes:.0f} B of outputs"
+    return k, os.path.basename(files[-1])
 
 
-def pmc_mfma_busy(kernel: str, simds: int = 256 * 4):
-    """MFMA pipe utilisation of `kernel` from the committed PMC summary:
-    SQ_VALU_MFMA_BUSY_CYCLES (summed over SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs x
-    SIMDs) -- the busy share of the dispatch's wall cycles."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json")))
-    if not files:
-        return None
-    d = json.load(open(files[-1]))
-    keys = [k for k in d if kernel in k and "SQ_VALU_MFMA_BUSY_CYCLES" in d[k] and "GRBM_GUI_ACTIVE" in d[k]]
-    if not keys:
-        return None
-    k = d[sorted(keys, key=len)[0]]
-    return k["SQ_VALU_MFMA_BUSY_CYCLES"] / (k["GRBM_GUI_ACTIVE"] / 8.0 * simds)
+def hbm_bytes(k, narrow_fetch_kib: float = 0.0):
+    """HBM bytes of one dispatch from its counters: FETCH_SIZE counts a wide
+    coalesced streaming read (16 B/lane) at half its bytes on gfx950 (x2, the
+    guide's correction), but a narrow scattered read's 64-B sectors in full --
+    calibrated by the pilot-only leg (tools/prof_leg.py ls_pilots: 8 sectors
+    = 512 B per frame measured as FETCH_SIZE).  narrow_fetch_kib = the part of
+    FETCH_SIZE that is such sector reads; WRITE_SIZE is exact."""
+    return (2.0 * (k["FETCH_SIZE"] - narrow_fetch_kib) + narrow_fetch_kib + k["WRITE_SIZE"]) * 1024.0
 
 
 def time_events(wce, stream, fn, reps):
@@ -246,29 +253,32 @@ def main():
     if not args.no_extras:
         # Dominant kernel = the whole step: for the rank-1 covariances (TEXTBOOK,
         # REF) one launch of mmse_solve_fc_kernel does the MMSE (Cholesky with two
-        # bordered rows, H = u s).  HIP events on the launch stream.  "bound":
-        # "mfma" = the FP64 compute roofline (MI355X FP64 vector = matrix peak);
-        # this kernel runs on the FP64 VALU, the MFMA GEMM is the COV leg below.
+        # bordered rows, H = u s).  HIP events on the launch stream.  The kernel
+        # runs on the FP64 VALU (no MFMA: DESIGN.md s6), so the bound is the FP64
+        # vector peak, 78.6 TF -- numerically the same as the FP64 MFMA peak.
         reps = max(5, args.steps)
         t_step = time_events(wce, stream, step, reps)
         fl_alg = FLOP_SOLVE_TXT + FLOP_APPLY if mode == wce.MMSE_TEXTBOOK else FLOP_SOLVE_REF + FLOP_APPLY
         ach = fl_alg * B / (t_step * 1e-3) / 1e12
         kname = "mmse_solve_fc_kernel"
-        traffic, tsrc = pmc_traffic(kname, B, "pmc_headline")
-        res["roofline"] = {"bound": "mfma", "kernel": f"{kname} (fp64 VALU Cholesky, row-per-lane panels, bordered by conj(rx) and (w o x)^T)",
+        k, tsrc = pmc_leg("headline", B, N * 16.0 * B, waves=B) if mode == wce.MMSE_TEXTBOOK else (None, "REF headline")
+        ach_x = FLOP_EXEC_R1 * B / (t_step * 1e-3) / 1e12
+        res["roofline"] = {"bound": "fp64-valu", "kernel": f"{kname} (fp64 VALU Cholesky, row-per-lane panels, bordered by conj(rx) and (w o x)^T)",
                            "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": traffic,
-                           "traffic_unit": "bytes/launch (FETCH_SIZEx2 + WRITE_SIZE)",
+                           "frac": ach / PEAK_FP64_TFLOPS, "traffic": hbm_bytes(k) if k else None,
+                           "traffic_unit": "HBM bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, same-size launches)",
                            "traffic_source": tsrc,
                            "algorithmic_bytes": 3 * 848 * B,
                            "flop_per_frame": fl_alg, "frames_per_launch": B, "avg_launch_ms": t_step,
                            "flop_per_frame_executed": FLOP_EXEC_R1 if mode == wce.MMSE_TEXTBOOK else None,
-                           "achieved_executed": (FLOP_EXEC_R1 * B / (t_step * 1e-3) / 1e12
-                                                 if mode == wce.MMSE_TEXTBOOK else None),
-                           "note": "flop_per_frame = SURVEY 8(d) F_alg (4/3 n^3 + 28 n^2, the generic dense MMSE) "
-                                   "per the measurement contract; flop_per_frame_executed = what this kernel runs "
-                                   "(rank-1 Ryy build, two forward solves, no C W product). peak = MI355X FP64 "
-                                   "(vector = matrix, spec)"}
+                           "achieved_executed": ach_x if mode == wce.MMSE_TEXTBOOK else None,
+                           "frac_executed": ach_x / PEAK_FP64_TFLOPS if mode == wce.MMSE_TEXTBOOK else None,
+                           "valu_insts_per_frame": (k["SQ_INSTS_VALU"] / B) if k and "SQ_INSTS_VALU" in k else None,
+                           "note": "frac = SURVEY 8(d) F_alg (4/3 n^3 + 28 n^2, the generic dense MMSE) per the "
+                                   "measurement contract; frac_executed = the flops this kernel runs (exact first "
+                                   "step, Cholesky over pivots 1..52, rank-1 Ryy build, two bordered forward "
+                                   "solves; no back-substitution, no C W product). peak = MI355X FP64 vector "
+                                   "(= FP64 matrix), spec, 2.4 GHz"}
         res["mmse_frac_of_roofline"] = value / dist.world * fl_alg / (PEAK_FP64_TFLOPS * 1e12)
 
     if not args.no_extras and dist.rank == 0:
@@ -289,12 +299,31 @@ def main():
         res["cov_mode"] = {"workload": "WCE_MMSE_COV: full-rank PDP covariance, dense C (BASELINE configs[2] shape)",
                            "frames_per_s_per_gpu": B / (t_cov * 1e-3), "ms_per_step": t_cov,
                            "solve_kernel": "mmse_solve_kernel<false> (dense C, back-substitution)",
-                           "solve_ms": t_cs, "solve_tflops": FLOP_SOLVE_TXT * B / (t_cs * 1e-3) / 1e12}
-        res["apply_kernel"] = {"kernel": "matvec_kernel<false,false> = H = C W (v_mfma_f64_16x16x4), COV mode",
-                               "avg_launch_ms": t_apply, "achieved_tflops": ach_apply,
-                               "frac_fp64_peak": ach_apply / PEAK_FP64_TFLOPS,
-                               "mfma_traffic": pmc_traffic("matvec_kernel<false, false, 1>", B)[0],
-                               "mfma_busy_frac_pmc": pmc_mfma_busy("matvec_kernel<false, false, 1>")}
+                           "solve_ms": t_cs, "solve_tflops": FLOP_SOLVE_TXT * B / (t_cs * 1e-3) / 1e12,
+                           "solve_frac_fp64_peak": FLOP_SOLVE_TXT * B / (t_cs * 1e-3) / 1e12 / PEAK_FP64_TFLOPS}
+        kc, csrc = pmc_leg("cov_solve", B, N * 16.0 * B, waves=B)
+        if kc:
+            res["cov_mode"]["solve_pmc_per_wave"] = {
+                c: kc[c] / B for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS",
+                                       "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES") if c in kc}
+            res["cov_mode"]["solve_pmc_source"] = csrc
+        # MFMA counters of exactly this launch (65,536 frames = 4,096 waves of 16
+        # frames): the 'apply' leg of tools/pmc_legs.sh
+        ka, asrc = pmc_leg("apply", B, N * 16.0 * B, waves=4 * ((B + 63) // 64))
+        app = {"kernel": "matvec_kernel<false,false,1> = H = C W (v_mfma_f64_16x16x4), COV mode",
+               "avg_launch_ms": t_apply, "achieved_tflops": ach_apply,
+               "frac_fp64_peak": ach_apply / PEAK_FP64_TFLOPS, "pmc_source": asrc,
+               "algorithmic_bytes": 2 * N * 16 * B}
+        if ka:
+            waves = 4 * ((B + 63) // 64)
+            mfma = ka["SQ_INSTS_VALU_MFMA_F64"]             # wave-level v_mfma_f64_16x16x4 per launch
+            app.update({"waves": waves, "mfma_insts_per_wave": mfma / waves,
+                        "traffic": hbm_bytes(ka),
+                        "executed_tflops": mfma * 2 * 16 * 16 * 4 / (t_apply * 1e-3) / 1e12,
+                        "mfma_busy_frac_pmc": ka["SQ_VALU_MFMA_BUSY_CYCLES"] / (ka["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4),
+                        "note": "executed = 224 MFMA/wave x 2,048 flop: 56 x 64 zero-padded (53 x 53 useful, "
+                                "x1.276); busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
+        res["apply_kernel"] = app
         del ctx3
 
     if not args.no_extras:
@@ -315,24 +344,32 @@ def main():
         if dist.rank == 0:
             res["host_pipeline"] = bench_host_pipeline(wce, ctx, tx, rx, H, B, max(3, reps // 10))
 
+        # rank-0 single-GPU legs first: the 1,048,576-frame strong-scaling legs
+        # below allocate and free ~37 GB, which moves later legs' placement
+        # (LS spread is physical placement)
+        if dist.rank == 0:
+            # rank 0 only: contexts built locally (make_ctx would broadcast: a collective)
+            local_ctx = lambda m: wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m, device=dev)
+            # LS path (config 2: LT_LS + PS_Linear), HBM-bound
+            res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
+            res["front_end"] = bench_front(wce, ctx, stream, B, reps)
+            res["frame_cov"] = bench_frame_cov(wce, local_ctx, stream, B, reps)
+            res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
+            res["small_batch"] = bench_small_batch(wce, ctx, stream)
+            # REF past the MALL: 1,048,576 full frames (27 GB), last of the rank-0 legs
+            ctx_ref = local_ctx(wce.MMSE_REF)
+            res.setdefault("ref_mode", {})["b%d" % args.ls_frames] = bench_ref_large(wce, ctx_ref, stream,
+                                                                                   args.ls_frames, reps)
+            del ctx_ref
+
         # BASELINE configs[3]: 1,048,576 frames in total, sharded over the
         # ranks (strong scaling), same kernel; all ranks, barrier + max
         res["config4"] = bench_config4(wce, ctx, dist, stream, hs, max(5, args.steps // 5))
         res["config5_sharded"] = bench_config5_sharded(wce, ctx, dist, stream, max(3, args.steps // 20))
 
-        # LS path (config 2: LT_LS + PS_Linear), HBM-bound
-        if dist.rank == 0:
-            res["ls_config2"] = bench_ls(wce, ctx, stream, args.ls_frames, reps)
-            res["front_end"] = bench_front(wce, ctx, stream, B, reps)
-            # rank 0 only: contexts built locally (make_ctx would broadcast: a collective)
-            local_ctx = lambda m: wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m, device=dev)
-            res["frame_cov"] = bench_frame_cov(wce, local_ctx, stream, B, reps)
-            res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
-            res["small_batch"] = bench_small_batch(wce, ctx, stream)
-
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
-        res["cpu_baseline"] = cpu_baseline(ctx, tx, rx, B, mode, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(wce, ctx, frames, tx, rx, B, mode, args.cpu_seconds)
         refc = cpu_reference(args.cpu_seconds / 2)
         if refc is not None:
             res["cpu_baseline"]["reference_code"] = refc
@@ -367,10 +404,29 @@ def bench_config5_sharded(wce, ctx, dist, stream, steps, total=1 << 20):
     stream.synchronize()
     dist.barrier()
     dt = dist.max(time.perf_counter() - t0) / steps
+    # untimed: every output of the last step must be finite (the 4 fp32 LS
+    # outputs, the fp64 MMSE, the 15 fp32 equalized blocks); max over ranks
+    bad = sum(ctx.nonfinite_scan(h, count, f32=(i < 4), stream=s)[1] for i, h in enumerate(outs))
+    bad += ctx.nonfinite_scan(eq, count * NBLK, f32=True, stream=s)[1]
     return {"workload": "BASELINE configs[4]: all 5 estimators + equalization fused, fp64 solve / fp32 LS and eq "
                         "outputs, per-frame preambles, 1,048,576 frames sharded over the ranks",
             "global_frames": total, "frames_per_gpu": count, "n_gpus": dist.world, "steps": steps,
-            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong"}
+            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong",
+            "nonfinite_outputs": int(dist.max(float(bad))),
+            **config5_traffic(count, dt)}
+
+
+def config5_traffic(count, dt):
+    """HBM traffic of the fused configs[4] kernel from the 'config5' PMC leg
+    (1,048,576 frames: only the N=1 launch size is profiled)."""
+    wbytes = (4 * N * 8 + N * 16 + NBLK * N * 8) * count
+    k, src = pmc_leg("config5", count, wbytes, waves=count)   # one wave per frame
+    if not k:
+        return {"pmc_source": src}
+    alg = (NBLK * N + N + N) * 16 * count + wbytes     # rx 15 blocks + tx block 0 + rx_pre in
+    return {"algorithmic_bytes": alg, "traffic": hbm_bytes(k), "achieved_GBs": alg / dt / 1e9,
+            "frac_hbm": alg / dt / 1e9 / PEAK_HBM_GBS, "pmc_source": src,
+            "valu_insts_per_frame": k.get("SQ_INSTS_VALU", 0) / count}
 
 
 def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20):
@@ -401,11 +457,10 @@ def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20):
             "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong"}
 
 
-def bench_ls(wce, ctx, stream, n, reps):
-    """LT_LS (per-frame preamble) + PS_Linear over n frames; algorithmic bytes
-    2,672 B/frame.  Frames hold block 0 only (frame_stride = 53): the PS path
-    reads 4 pilots of block 0, LT_LS the frame's own preamble."""
-    s = stream.handle
+def ls_frames(wce, ctx, n, pilots_only=False):
+    """configs[1] input: n frames holding block 0 only (frame_stride = 53: the
+    PS path reads 4 pilots of block 0, LT_LS the frame's own preamble), plus
+    per-frame preambles.  Returns (buffers, wce.Frames)."""
     lib = wce.load()
     tx, rx, pre = wce.DeviceArray((n, N)), wce.DeviceArray((n, N)), wce.DeviceArray((n, N))
     rng = np.random.default_rng(1)
@@ -418,6 +473,16 @@ def bench_ls(wce, ctx, stream, n, reps):
         m = min(chunk, n - off)
         for d, h in ((tx, txh), (rx, rxh), (pre, preh)):
             assert lib.wce_memcpy_htod(d.addr + off * N * 16, h[:m].ctypes.data, m * N * 16) == 0
+    fr = ctx.frames(tx, rx, n, frame_stride=N, block_stride=N, rx_pre=None if pilots_only else pre, pre_stride=N)
+    return (tx, rx, pre), fr
+
+
+def bench_ls(wce, ctx, stream, n, reps):
+    """LT_LS (per-frame preamble) + PS_Linear over n frames; algorithmic bytes
+    2,672 B/frame (ls_frames' layout)."""
+    s = stream.handle
+    bufs, fr_n = ls_frames(wce, ctx, n)
+    tx, rx, pre = bufs
     hlt, hlin = wce.DeviceArray((n, N)), wce.DeviceArray((n, N))
     o = wce.Outputs(hlt.addr, hlin.addr, None, None, None, None, N, 0, 0, 0, 0)
     out = {"workload": "LT_LS + PS_Linear (config 2), per-frame preamble, algorithmic 2672 B/frame"}
@@ -437,32 +502,60 @@ def bench_ls(wce, ctx, stream, n, reps):
     gbs = 848 * n / (t * 1e-3) / 1e9
     out["nonfinite_scan"] = {"kernel": "nonfinite_scan_kernel<false>", "frames": n, "avg_launch_ms": t,
                              "algorithmic_bytes_per_frame": 848, "achieved_GBs": gbs, "frac": gbs / PEAK_HBM_GBS}
-    # HBM bytes from the LS-only PMC pass (tools/pmc_ls.sh: 1,048,576 frames per
-    # dispatch).  Reads: rx_pre streams (FETCH_SIZE half-counts 16-B/lane
-    # streaming reads on gfx950) plus 8 pilot loads per frame, each a full 64-B
-    # sector (counted in full); writes exact.
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_ls.json")))
-    if files:
-        k = json.load(open(files[-1])).get("wce::ls_flat_kernel")
-        if k:
-            per = 1024.0 / 1048576
-            out["pmc_bytes_per_frame"] = {"FETCH_SIZE": k["FETCH_SIZE"] * per, "WRITE_SIZE": k["WRITE_SIZE"] * per,
-                                          "expected_FETCH_SIZE": N * 16 / 2 + 8 * 64,
-                                          "real_traffic": N * 16 + 8 * 64 + k["WRITE_SIZE"] * per,
-                                          "source": os.path.basename(files[-1])}
-            key = "b%d" % n
-            rt = out["pmc_bytes_per_frame"]["real_traffic"]
-            out[key]["traffic"] = rt * n
-            out[key]["real_GBs"] = rt * n / (out[key]["avg_launch_ms"] * 1e-3) / 1e9
+    # HBM bytes from counters of same-size launches (tools/pmc_legs.sh 'ls';
+    # the pilot-sector reads calibrated by the pilot-only leg 'ls_pilots')
+    key = "b%d" % n
+    k, src = pmc_leg("ls", n, 2 * N * 16.0 * n)
+    kp, _ = pmc_leg("ls_pilots", n, N * 16.0 * n)
+    out[key]["pmc_source"] = src
+    if k and kp:
+        traffic = hbm_bytes(k, narrow_fetch_kib=kp["FETCH_SIZE"])
+        out[key].update({"traffic": traffic, "traffic_bytes_per_frame": traffic / n,
+                         "real_GBs": traffic / (out[key]["avg_launch_ms"] * 1e-3) / 1e9,
+                         "pilot_fetch_bytes_per_frame": kp["FETCH_SIZE"] * 1024.0 / n,
+                         "traffic_note": "FETCH_SIZE x2 for the streamed rx_pre reads, pilot sectors counted in "
+                                         "full (the pilot-only leg measures them at ~512 B = 8 x 64-B sectors "
+                                         "per frame), WRITE_SIZE exact"})
     return out
 
 
-def bench_front(wce, ctx, stream, n, reps):
-    """Time-domain front end (SURVEY 8(f)-2) over n frames of 15 x 80-sample
-    blocks + a 160-sample LTF each: HBM-bound, algorithmic bytes per block
-    1,872 (64 samples in, 53 bins out), per LTF 2,904."""
+def ref_frames(wce, ctx, n, stream=None):
+    """REF-mode input: n full frames (15 x 53 blocks, 12,720 B of tx and of rx
+    each), synthesised on the device.  Returns (tx, rx, wce.Frames)."""
+    tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+    ctx.synth(tx, rx, None, n, seed=0x80211, stream=stream)
+    return tx, rx, ctx.frames(tx, rx, n)
+
+
+def bench_ref_large(wce, ctx, stream, n, reps):
+    """PS_MMSE in REF (main.c) semantics past the 256 MiB MALL: n full frames,
+    one mmse_ref_flat_kernel launch.  Algorithmic bytes 976 per frame (4 tx + 4
+    rx pilots in, 53 out); the pilot reads cost a 64-B sector each, so the
+    sector floor is 8 x 64 + 848 = 1,360 B per frame."""
     s = stream.handle
+    tx, rx, fr = ref_frames(wce, ctx, n, s)
+    H = wce.DeviceArray((n, N))
+    o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+    f = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
+    for _ in range(3):
+        f()
+    t = time_events(wce, stream, f, reps)
+    alg = BYTES_REF_ALG * n / (t * 1e-3) / 1e9
+    sec = (BYTES_PILOT_SECTORS + N * 16) * n / (t * 1e-3) / 1e9
+    k, src = pmc_leg("ref", n, N * 16.0 * n)
+    traffic = hbm_bytes(k, narrow_fetch_kib=k["FETCH_SIZE"]) if k else None
+    _, bad = ctx.nonfinite_scan(H, n, stream=s)
+    return {"frames": n, "avg_launch_ms": t, "frames_per_s": n / (t * 1e-3),
+            "roofline": {"bound": "hbm", "kernel": "mmse_ref_flat_kernel", "achieved": alg, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": alg / PEAK_HBM_GBS, "traffic": traffic,
+                         "algorithmic_bytes": BYTES_REF_ALG * n, "sector_floor_bytes": (BYTES_PILOT_SECTORS + N * 16) * n,
+                         "achieved_sector_GBs": sec, "frac_sector": sec / PEAK_HBM_GBS, "pmc_source": src,
+                         "traffic_note": "FETCH_SIZE (pilot sectors, counted in full) + WRITE_SIZE"},
+            "nonfinite_frames": bad}
+
+
+def front_frames(wce, n):
+    """n time-domain packets (15 blocks of 80 samples) and 160-sample LTFs."""
     rng = np.random.default_rng(2)
     chunk = min(n, 8192)
     pk = wce.DeviceArray((n, NBLK * 80))
@@ -474,6 +567,15 @@ def bench_front(wce, ctx, stream, n, reps):
         m = min(chunk, n - off)
         assert lib.wce_memcpy_htod(pk.addr + off * NBLK * 80 * 16, src[:m].ctypes.data, m * NBLK * 80 * 16) == 0
         assert lib.wce_memcpy_htod(lt.addr + off * 160 * 16, srcl[:m].ctypes.data, m * 160 * 16) == 0
+    return pk, lt
+
+
+def bench_front(wce, ctx, stream, n, reps):
+    """Time-domain front end (SURVEY 8(f)-2) over n frames of 15 x 80-sample
+    blocks + a 160-sample LTF each: HBM-bound, algorithmic bytes per block
+    1,872 (64 samples in, 53 bins out), per LTF 2,904."""
+    s = stream.handle
+    pk, lt = front_frames(wce, n)
     sym = wce.DeviceArray((n, NBLK, N))
     pre = wce.DeviceArray((n, N))
     ow2 = wce.DeviceArray((n,), np.float64)
@@ -486,7 +588,9 @@ def bench_front(wce, ctx, stream, n, reps):
         t = time_events(wce, stream, f, reps)
         gbs = per * units / (t * 1e-3) / 1e9
         kn = f"front_kernel<{'true' if label == 'preamble' else 'false'}>"
-        traffic, _ = pmc_traffic(kn, n)
+        k, _ = pmc_leg("front_" + label, n, (N * 16.0 + (8 if label == "preamble" else 0)) * units,
+                       tol=0.1 if label == "preamble" else 0.02)   # sigma^2: one 8-B store per frame
+        traffic = hbm_bytes(k) if k else None
         out[label] = {"kernel": kn, "avg_launch_ms": t,
                       "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_unit": per, "achieved_GBs": gbs,
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS,
@@ -717,9 +821,10 @@ def cpu_reference(budget_s):
     return out
 
 
-def cpu_baseline(ctx, tx, rx, B, mode, budget_s):
+def cpu_baseline(wce, ctx, frames, tx, rx, B, mode, budget_s):
     """The oracle's fp64 OpenMP port of the same unified MMSE (kind "port"),
-    on a bounded sample of the benchmark's own frames."""
+    on a bounded sample of the benchmark's own frames; its H is compared with
+    the GPU's H of the same frames (max norm-relative error)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_py
     try:
@@ -732,8 +837,12 @@ def cpu_baseline(ctx, tx, rx, B, mode, budget_s):
     m = min(B, 4096)
     txh = tx.numpy()[:m, 0].copy()
     rxh = rx.numpy()[:m, 0].copy()
-    _, t = oracle_py.bench_mmse_f64(C, mask, a, b, txh.reshape(-1), rxh.reshape(-1), N, cores)
+    Hc, t = oracle_py.bench_mmse_f64(C, mask, a, b, txh.reshape(-1), rxh.reshape(-1), N, cores)
     rate = m / t
+    Hg = wce.DeviceArray((B, N), zero=True)
+    ctx.estimate(frames, wce.Outputs(None, None, None, None, Hg.addr, None, N, 0, 0, 0, 0), wce.PS_MMSE)
+    wce.synchronize()
+    err = oracle_py.normrel(Hg.rows(0, m), Hc)
     target = int(min(max(rate * budget_s / cores, m), 2_000_000))
     reps = max(1, target // m)
     t_tot = 0.0
@@ -745,6 +854,8 @@ def cpu_baseline(ctx, tx, rx, B, mode, budget_s):
             "sample": f"{frames} frames ({m} distinct bench frames x {reps}): the unified dense MMSE in fp64 "
                       f"(LDL^H + back-substitution + C w, the GPU's dense-C path), OpenMP over frames, "
                       f"{t_tot:.2f} s wall",
+            "max_normrel_err_vs_gpu": float(err.max()), "median_normrel_err_vs_gpu": float(np.median(err)),
+            "err_frames": m,
             "reference_main_c_seconds_per_frame": 232.6,
             "reference_note": "main.c PS_MMSE itself: ~200-233 s/frame on 1 core, output NaN (SURVEY 0-1); "
                               "its OpenMP path segfaults"}

@@ -34,10 +34,17 @@ def oracle():
 
 
 def _ensure_libwce():
-    lib = os.path.join(REPO, "80211parallelestimation_amd", "libwce.so")
-    if not os.path.exists(lib):
-        subprocess.check_call(["make", "-C", os.path.join(REPO, "80211parallelestimation_amd", "csrc"), "-j4"],
-                              stdout=subprocess.DEVNULL)
+    """Build libwce.so unless it exists AND was linked from exactly the
+    current sources (content hash written by the Makefile beside it): a
+    pushed, older library is rebuilt, never tested silently."""
+    pkg = os.path.join(REPO, "80211parallelestimation_amd")
+    lib = os.path.join(pkg, "libwce.so")
+    sys.path.insert(0, pkg)
+    import srchash
+    stamp = lib + ".srchash"
+    fresh = os.path.exists(lib) and os.path.exists(stamp) and open(stamp).read().strip() == srchash.source_hash()
+    if not fresh:
+        subprocess.check_call(["make", "-C", os.path.join(pkg, "csrc"), "-B", "-j8"], stdout=subprocess.DEVNULL)
     return lib
 
 

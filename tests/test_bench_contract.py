@@ -39,7 +39,7 @@ def test_contract_keys(line):
 
 def test_roofline_consistent(line):
     r = line["roofline"]
-    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "TFLOP/s"
+    assert r["bound"] in ("hbm", "mfma", "fp64-valu") and r["unit"] == "TFLOP/s"
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     ach = r["flop_per_frame"] * r["frames_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12
     assert abs(ach - r["achieved"]) / ach < 1e-9
@@ -49,6 +49,25 @@ def test_roofline_consistent(line):
 def test_cpu_baseline_fields(line):
     c = line["cpu_baseline"]
     assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    if "max_normrel_err_vs_gpu" in c:        # the port's H against the GPU's, same frames
+        assert c["max_normrel_err_vs_gpu"] < 1e-10
+
+
+def test_leg_rooflines(line):
+    """Legs that carry a roofline keep its arithmetic; counters come from
+    same-size launches (pmc_source names the legs file, not a refusal)."""
+    ref = line.get("ref_mode", {}).get("b1048576")
+    if ref:
+        r = ref["roofline"]
+        assert r["bound"] == "hbm" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+        assert abs(r["achieved"] - r["algorithmic_bytes"] / (ref["avg_launch_ms"] * 1e-3) / 1e9) / r["achieved"] < 1e-9
+        assert ref["nonfinite_frames"] == 0
+        if r["traffic"] is not None:
+            assert r["traffic"] > 0.95 * r["sector_floor_bytes"]
+    app = line.get("apply_kernel")
+    if app and "waves" in app:
+        assert app["waves"] == 4096 and abs(app["mfma_insts_per_wave"] - 224) < 1e-6
+        assert app["executed_tflops"] > app["achieved_tflops"]
 
 
 def test_rocprof_headline_average_agrees(line):
@@ -81,5 +100,7 @@ def test_extra_legs_consistent(line):
 def test_config5_sharded_consistent(line):
     c5 = line.get("config5_sharded")
     if c5:
+        if "nonfinite_outputs" in c5:
+            assert c5["nonfinite_outputs"] == 0
         assert c5["global_frames"] == 1 << 20 and c5["scaling"] == "strong"
         assert abs(c5["frames_per_s"] - c5["global_frames"] / (c5["ms_per_step"] * 1e-3)) / c5["frames_per_s"] < 1e-6

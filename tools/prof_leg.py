@@ -1,0 +1,116 @@
+"""Run ONE bench leg's dominant kernel at exactly the bench's launch size,
+`--reps` times, and nothing else but its setup (synth / one solve): the
+workload for rocprofv3 --pmc passes (tools/pmc_legs.sh), so that a per-kernel
+average over the dispatches of a pass is an average over same-size launches.
+
+legs (bench.py field -> kernel, frames per launch):
+  headline   roofline            mmse_solve_fc_kernel             65,536 (TEXTBOOK, 1 wave/frame)
+  apply      apply_kernel        matvec_kernel<false,false,1>     65,536 (COV H = C W, 16 frames/wave)
+  cov_solve  cov_mode            mmse_solve_kernel<false>         65,536 (COV dense solve)
+  ref        ref_mode.b1048576   mmse_ref_flat_kernel          1,048,576 (REF, main.c semantics)
+  ls         ls_config2          ls_flat_kernel                1,048,576 (LT_LS + PS_Linear)
+  ls_pilots  (calibration)       ls_flat_kernel                1,048,576 (PS_Linear only: pilot reads)
+  front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
+  config5    config5_sharded     mmse_solve_ls_kernel<true,true,true>  1,048,576 (all 5 + eq, fp32 LS)
+"""
+import argparse
+import importlib
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+N, NBLK = 53, 15
+
+LEGS = {
+    "headline": ("mmse_solve_fc_kernel", 65536),
+    "apply": ("matvec_kernel<false, false, 1>", 65536),
+    "cov_solve": ("mmse_solve_kernel<false>", 65536),
+    "ref": ("mmse_ref_flat_kernel", 1 << 20),
+    "ls": ("ls_flat_kernel", 1 << 20),
+    "ls_pilots": ("ls_flat_kernel", 1 << 20),      # PS_Linear only: calibrates the pilot-sector reads
+    "front_blocks": ("front_kernel<false>", 65536),
+    "front_preamble": ("front_kernel<true>", 65536),
+    "config5": ("mmse_solve_ls_kernel<true, true, true>", 1 << 20),
+}
+
+
+def pdp_rhh():
+    p = np.exp(-0.12 * np.arange(N))
+    return np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--leg", choices=sorted(LEGS), required=True)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    wce = importlib.import_module("80211parallelestimation_amd")
+    import bench
+    inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
+    leg = args.leg
+    n = LEGS[leg][1]
+    if leg in ("headline", "apply", "cov_solve"):
+        if leg == "headline":
+            ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+        else:
+            ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh())
+        hlt = ctx.shared()[0]
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211, h_shared=wce.DeviceArray.from_numpy(hlt))
+        H = wce.DeviceArray((n, N), zero=True)
+        fr = ctx.frames(tx, rx, n)
+        if leg == "headline":
+            run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
+                                       wce.PS_MMSE)
+        elif leg == "cov_solve":
+            run = lambda: ctx.mmse_solve(fr, H, N)
+        else:
+            W = wce.DeviceArray((n, N), zero=True)
+            ctx.mmse_solve(fr, W, N)
+            run = lambda: ctx.mmse_apply(W, H, n, N)
+    elif leg == "ref":
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        tx, rx, fr = bench.ref_frames(wce, ctx, n)
+        H = wce.DeviceArray((n, N), zero=True)
+        run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
+                                   wce.PS_MMSE)
+    elif leg in ("ls", "ls_pilots"):
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        bufs, fr = bench.ls_frames(wce, ctx, n, pilots_only=leg == "ls_pilots")
+        hlt, hlin = wce.DeviceArray((n, N)), wce.DeviceArray((n, N))
+        if leg == "ls":
+            o = wce.Outputs(hlt.addr, hlin.addr, None, None, None, None, N, 0, 0, 0, 0)
+            run = lambda: ctx.estimate(fr, o, wce.LT_LS | wce.PS_LINEAR)
+        else:
+            o = wce.Outputs(None, hlin.addr, None, None, None, None, N, 0, 0, 0, 0)
+            run = lambda: ctx.estimate(fr, o, wce.PS_LINEAR)
+    elif leg.startswith("front_"):
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        pk, lt = bench.front_frames(wce, n)
+        sym, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+        ow2 = wce.DeviceArray((n,), np.float64)
+        if leg == "front_blocks":
+            run = lambda: ctx.front_end_blocks(pk, n, NBLK, sym)
+        else:
+            run = lambda: ctx.front_end_preamble(lt, n, 160, pre, ow2)
+    else:
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+        tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+        ctx.synth(tx, rx, pre, n, seed=0x80211)
+        outs = [wce.DeviceArray((n, N), np.complex64) for _ in range(4)] + [wce.DeviceArray((n, N))]
+        eq = wce.DeviceArray((n, NBLK, N), np.complex64)
+        o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32)
+        fr = ctx.frames(tx, rx, n, rx_pre=pre)
+        run = lambda: ctx.estimate(fr, o, wce.ALL)
+    wce.synchronize()
+    for _ in range(args.reps):
+        run()
+    wce.synchronize()
+    print(f"{leg}: {args.reps} launches of {LEGS[leg][0]} at {n} frames")
+
+
+if __name__ == "__main__":
+    main()
