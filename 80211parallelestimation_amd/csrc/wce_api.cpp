@@ -749,6 +749,12 @@ int wce_event_elapsed_ms(float *ms, void *a, void *b)
 
 }  // extern "C"
 
+extern "C" int wce_debug_set_variant(int which, int value)
+{
+    const int rc = wce::set_variant(which, value);
+    return rc ? fail(rc, "variant: which in [0, 4), value in [0, 16)") : WCE_OK;
+}
+
 extern "C" int wce_debug_set_flat_chunk(long long frames)
 {
     const int rc = wce::set_flat_chunk(frames);

@@ -129,6 +129,11 @@ int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, doub
 int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
+// kernel variants for A/B timing (wce_debug_set_variant)
+constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks, 1 = 64-frame tiles
+constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks, 1 = 64-frame tiles
+constexpr int WCE_VARIANT_COUNT = 4;
+int set_variant(int which, int value);
 int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,
                           unsigned long long *n_bad, void *stream);
 

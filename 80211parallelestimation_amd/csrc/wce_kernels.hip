@@ -355,6 +355,9 @@ __global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ 
 #ifndef WCE_REF_FLAT   // A/B: 0 = REF runs inside mmse_solve_fc_kernel (one wave per frame)
 #define WCE_REF_FLAT 1
 #endif
+#ifndef WCE_REF_TILE_WAVES_PER_CU
+#define WCE_REF_TILE_WAVES_PER_CU 28   // 71 VGPRs: 7 waves/SIMD
+#endif
 template <int CTRL>
 __device__ __forceinline__ double dpp_quad(double v)
 {
@@ -418,6 +421,75 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
             if (e < E) st2(a.w, (f_begin + f) * a.ws + k, cmul(u, s_tab[jl]));
         }
         wave_lds_sync();   // s_tab is rewritten by the next chunk
+    }
+}
+
+// =====================================================================
+// Frame tiles (round 2): a wave owns 64 consecutive frames at a time.  Lane j
+// issues ALL of frame j's pilot loads at once (8 x 16 B: 512 B in flight per
+// lane, against 2 x 16 B on 44 lanes per 512-element chunk above), reduces
+// them lane-locally, and publishes one value per frame through a per-wave LDS
+// table; the wave then streams the tile's 64 x 53 outputs -- one contiguous
+// 54 KB run -- with 53 full-wave nontemporal 16-B stores, element
+// e = 64 i + lane walked incrementally (k += 11, f += 1, wrap at 53: no
+// division).  The grid holds one wave per resident slot (launch_flat_tiles).
+// =====================================================================
+constexpr int TILE_F = 64;                 // frames per wave tile
+
+// element walk of a tile: lane l starts at (f, k) = (l / 53, l % 53)
+struct TileWalk {
+    int f, k;
+    __device__ __forceinline__ explicit TileWalk(int lane) : f(lane >= NSC ? 1 : 0), k(lane >= NSC ? lane - NSC : lane) {}
+    __device__ __forceinline__ void next()
+    {
+        k += 64 - NSC;
+        f += 1;
+        if (k >= NSC) { k -= NSC; f += 1; }
+    }
+};
+
+__global__ __launch_bounds__(256) void mmse_ref_tile_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
+                                                            uint32_t nfr)
+{
+    __shared__ double2 s_u[64];
+    __shared__ double2 s_s[LS_WAVES][TILE_F];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool shared = a.cs == 0;
+    if (shared && threadIdx.x < NSC) s_u[threadIdx.x] = ld2(a.cu, threadIdx.x);
+    __syncthreads();
+    const double rb = 1.0 / st->bcoef;
+    const uint32_t ntiles = (nfr + TILE_F - 1) / TILE_F;
+    double2 *s_tab = s_s[w];
+    for (uint32_t t = blockIdx.x * LS_WAVES + w; t < ntiles; t += gridDim.x * LS_WAVES) {
+        const uint32_t f0 = t * TILE_F;
+        const uint32_t fr = min(f0 + (uint32_t)lane, nfr - 1);
+        const int64_t fo = (f_begin + fr) * a.fs + (int64_t)a.blk * a.bs;
+        double2 xt[4], xr[4], wp[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            xt[p] = ld2(a.tx, fo + PILOT[p]);
+            xr[p] = ld2(a.rx, fo + PILOT[p]);
+            const int64_t wo = shared ? PILOT[p] : (f_begin + fr) * a.cs + PILOT[p];
+            wp[p] = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
+        }
+        // s_j = w^T X rx / b over frame j's pilots, summed in quad_sum_c's
+        // order ((t0 + t1) + (t2 + t3)) so the result matches the chunked kernel
+        double2 tp[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) tp[p] = cmul(cmul(wp[p], xt[p]), xr[p]);
+        s_tab[lane] = cscale(cadd(cadd(tp[0], tp[1]), cadd(tp[2], tp[3])), rb);
+        wave_lds_sync();
+        const uint32_t nf = min((uint32_t)TILE_F, nfr - f0);
+        const uint32_t ne = nf * NSC;
+        TileWalk wk(lane);
+        const int64_t obase = (f_begin + f0) * a.ws;
+#pragma unroll 4
+        for (uint32_t e = lane; e < ne; e += 64) {
+            const double2 u = shared ? s_u[wk.k] : ld2(a.cu, (f_begin + f0 + wk.f) * a.cs + wk.k);
+            st2_nt(a.w, obase + (int64_t)wk.f * a.ws + wk.k, cmul(u, s_tab[wk.f]));
+            wk.next();
+        }
+        wave_lds_sync();   // s_tab is rewritten by the next tile
     }
 }
 
@@ -1342,6 +1414,33 @@ __global__ __launch_bounds__(256) void nonfinite_scan_kernel(const double *__res
 // ---------------------------------------------------------------- launchers
 static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP; }
 
+// A/B kernel variants, process-wide (wce_debug_set_variant): lets one process
+// time two kernels on the same buffers, interleaved.  Defaults = the product.
+static int g_variant[WCE_VARIANT_COUNT] = {0, 0, 0, 0};
+int set_variant(int which, int value)
+{
+    if (which < 0 || which >= WCE_VARIANT_COUNT || value < 0 || value > 15) return WCE_EINVAL;
+    __atomic_store_n(&g_variant[which], value, __ATOMIC_RELAXED);
+    return WCE_OK;
+}
+static inline int variant(int which) { return __atomic_load_n(&g_variant[which], __ATOMIC_RELAXED); }
+
+// blocks of 4 waves for a tile kernel: one wave per tile up to the device's
+// resident-wave budget (CUs x waves per CU), grid-stride past it
+static int64_t tile_blocks(int64_t tiles, int waves_per_cu)
+{
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            cus = n;
+        if (cus <= 0) cus = 256;
+    }
+    const int64_t cap = (int64_t)cus * waves_per_cu / LS_WAVES;
+    const int64_t need = (tiles + LS_WAVES - 1) / LS_WAVES;
+    return need < cap ? need : cap;
+}
+
 int launch_ls(const State *st, const LsArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
@@ -1388,6 +1487,11 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     if (WCE_REF_FLAT && a.hout && a.ref_pilots && !a.split) {
         for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
+            if (variant(WCE_VARIANT_REF) == 1) {
+                const int64_t fb = tile_blocks((nf + TILE_F - 1) / TILE_F, WCE_REF_TILE_WAVES_PER_CU);
+                hipLaunchKernelGGL(mmse_ref_tile_kernel, dim3((unsigned)fb), dim3(256), 0, s, st, a, f0, (uint32_t)nf);
+                continue;
+            }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
             if (fb > 256 * 8) fb = 256 * 8;

@@ -99,6 +99,7 @@ ABI = {
     "wce_debug_set_fusion": [c_void_p, c_int],
     "wce_debug_set_border_dot": [c_void_p, c_int],
     "wce_debug_set_flat_chunk": [ctypes.c_int64],
+    "wce_debug_set_variant": [c_int, c_int],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
