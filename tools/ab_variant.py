@@ -11,6 +11,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
 N, NBLK = 53, 15
 WHICH = {"ref": 0, "ls": 1}
 
@@ -66,7 +67,6 @@ def main():
         t = float(np.median(ts))
         print(f"{args.leg} variant {v}: median {t * 1e3:.1f} us  min {min(ts) * 1e3:.1f}  "
               f"{alg * n / (t * 1e-3) / 1e12:.2f} TB/s {unit}  ({', '.join(f'{x * 1e3:.0f}' for x in ts)})")
-    lib.wce_debug_set_variant(WHICH[args.leg], 0)
 
 
 if __name__ == "__main__":
