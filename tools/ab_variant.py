@@ -1,7 +1,7 @@
 """Interleaved A/B of kernel variants (wce_debug_set_variant) on the same
 buffers in one process: rounds x (variant a, variant b, ...), HIP-event
 timing per launch, outputs compared bit for bit across variants.
-usage: python tools/ab_variant.py {ref,ls} [--variants 0 1] [--rounds 5] [--reps 20]"""
+usage: python tools/ab_variant.py {ref,ls,dense} [--variants 0 1] [--rounds 5] [--reps 20]"""
 import argparse
 import importlib
 import os
@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 N, NBLK = 53, 15
-WHICH = {"ref": 0, "ls": 1}
+WHICH = {"ref": 0, "ls": 1, "dense": 2}
 
 
 def main():
@@ -39,6 +39,17 @@ def main():
         o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
         run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
         alg, unit = bench.BYTES_REF_ALG, "alg"
+    elif args.leg == "dense":
+        # COV mode (full-rank PDP covariance): the dense solve alone (W = X z)
+        import prof_leg
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rhh())
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211)
+        fr = ctx.frames(tx, rx, n)
+        W = wce.DeviceArray((n, N), zero=True)
+        outs = [W]
+        run = lambda: ctx.mmse_solve(fr, W, N, s)
+        alg, unit = bench.FLOP_SOLVE_TXT / 1000.0, "(= PF/s of F_alg solve flops)"
     else:
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
         bufs, fr = bench.ls_frames(wce, ctx, n)
@@ -62,7 +73,10 @@ def main():
                     ref_out = got
                 else:
                     same = all(np.array_equal(a, b) for a, b in zip(got, ref_out))
-                    print(f"variant {v}: outputs bit-identical to variant {args.variants[0]}: {same}")
+                    dif = max(float(np.max(np.abs(a - b), axis=-1).max() / max(np.abs(b).max(), 1e-300))
+                              for a, b in zip(got, ref_out))
+                    print(f"variant {v}: outputs bit-identical to variant {args.variants[0]}: {same} "
+                          f"(max |diff| / max |ref| = {dif:.2e})")
     for v, ts in times.items():
         t = float(np.median(ts))
         print(f"{args.leg} variant {v}: median {t * 1e3:.1f} us  min {min(ts) * 1e3:.1f}  "
