@@ -124,10 +124,10 @@ __device__ __forceinline__ void st_out(double *p, int64_t idx, double2 v, bool f
 }
 
 // store the requested LS-family outputs of frame f, subcarrier k, and run
-// WiFi_Equalization.m:1-9 over the frame's 15 blocks
+// WiFi_Equalization.m:1-9 over the frame's 15 blocks rv (already loaded)
 template <bool EQ>
-__device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
-                                         double2 hcub, double2 hsnc)
+__device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
+                                            double2 hcub, double2 hsnc, const double2 (&rv)[NBLK])
 {
     const int64_t o = f * a.os + k;
     const bool f32 = a.f32 != 0;
@@ -137,10 +137,7 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
     if ((mask & WCE_EST_PS_SINC) && a.snc) st_out(a.snc, o, hsnc, f32);
     if constexpr (EQ) {
         const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
-        const int64_t rb = f * a.fs + k, eb = f * a.eqfs + k;
-        double2 rv[NBLK];
-#pragma unroll
-        for (int b = 0; b < NBLK; b++) rv[b] = ld2(a.rx, rb + b * a.bs);
+        const int64_t eb = f * a.eqfs + k;
 #pragma unroll
         for (int b = 0; b < NBLK; b++) {
             const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
@@ -149,6 +146,17 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
             st_out(a.eq, eb + b * a.eqbs, e, f32);
         }
     }
+}
+template <bool EQ>
+__device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
+                                         double2 hcub, double2 hsnc)
+{
+    double2 rv[NBLK];
+    if constexpr (EQ) {
+#pragma unroll
+        for (int b = 0; b < NBLK; b++) rv[b] = ld2(a.rx, f * a.fs + k + b * a.bs);
+    }
+    ls_store_rv<EQ>(a, f, k, mask, hlt, hlin, hcub, hsnc, rv);
 }
 
 // ML: MATLAB semantics (WiFi_channel_estimation_*.m): pilot LS averaged over
@@ -523,7 +531,7 @@ struct SolveLds {
             double2 z[64];    // solution
             double rd[64];    // r_k = 1 / d_k, 0 past 52
         };
-        double2 conv[56 * CVS];   // row-per-lane panels: block column -> rows (dot_panel)
+        double2 conv[56 * CVS];   // row-per-lane panels: block column -> rows (to_rows)
     };
 };
 // conv element (row, c) at row * 9 + c: the odd row stride keeps both the
@@ -649,51 +657,6 @@ __device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)
     const int l = lane < 56 ? lane : 55;   // lanes 56..63 carry a copy of row 55 (never read)
 #pragma unroll
     for (int c = 0; c < 8; ++c) P[c] = s.conv[conv_idx(l, c)];
-}
-
-#ifndef WCE_ROWP_PANELS   // panels 0 .. WCE_ROWP_PANELS-1 in row form; the rest block-cyclic
-#define WCE_ROWP_PANELS 6
-#endif
-constexpr int ROWP = WCE_ROWP_PANELS;
-static_assert(ROWP >= 1 && ROWP < RB, "the last block column runs ldl_panel");
-
-// Panel KB in row form.  Entering: P = block column KB, u_{8KB} published,
-// r = r_{8KB}.
-template <int KB>
-__device__ __forceinline__ void dot_panel(double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q, int lane,
-                                          double &r)
-{
-#pragma unroll
-    for (int kq = 0; kq < 8; ++kq) {
-        const int k = 8 * KB + kq;
-        const double2 *col = s.u[k & 1];
-        double2 *next = s.u[(k + 1) & 1];
-        const double rk = r;
-        double2 Ur[RB];
-#pragma unroll
-        for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
-        if (kq < 7) {
-            const double2 t = cscale(P[kq], rk);              // r_k u_k at this lane's row
-            cmsub_conj(P[kq + 1], t, col[8 * KB + kq + 1]);   // lookahead: column k+1
-            r = rcp_nr(readlane_f64(P[kq + 1].x, k + 1));
-            next[lane] = P[kq + 1];                           // publish: one store
-#pragma unroll
-            for (int c = kq + 2; c < 8; ++c) cmsub_conj(P[c], t, col[8 * KB + c]);
-            upd_cols_from<KB + 1>(A, Ur, col, q, rk);
-        } else {
-            upd_col<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
-            if constexpr (KB + 1 < ROWP) {
-                to_rows<KB + 1>(A, P, s, p, q, lane);
-                r = rcp_nr(readlane_f64(P[0].x, k + 1));
-                next[lane] = P[0];
-            } else {   // block column KB+1 on runs block-cyclic (ldl_panel)
-                r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
-                publish_col<KB + 1>(A, next, p, q, 0);
-            }
-            upd_cols_from<KB + 2>(A, Ur, col, q, rk);
-        }
-        wave_lds_sync();
-    }
 }
 
 // Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
@@ -902,18 +865,15 @@ __device__ __forceinline__ void exact_first_step(const SolveArgs &a, SolveLds &s
     s.blk[dst] = rhop;
 }
 
-#ifndef WCE_DOT_CHOL   // A/B: 0 = square-root-free LDL^H row panels (dot_panel)
-#define WCE_DOT_CHOL 1
-#endif
-#ifndef WCE_DOT_CYCLIC   // A/B: the rank-1 read-out on the all-block-cyclic factorisation
-#define WCE_DOT_CYCLIC 0
-#endif
 // The rank-1 read-out path (a != 0): Ryy = a (x o u)(w o x')^T + b I bordered
 // by conj(rx) (row 53) and (w o x)^T (row 54), factorised with row-per-lane
-// panels 0..5 (dot_panel) and the block-cyclic last panel; returns
-// s = -S(54, 53) = w^T X Ryy^-1 rx.
+// Cholesky panels 0..5 (chol_panel) and the block-cyclic last panel
+// (chol_last); returns s = -S(54, 53) = w^T X Ryy^-1 rx.  pf() is called
+// before the last panel, when most of the matrix registers are dead: the
+// config-5 kernel issues its epilogue's loads there (LsPrefetch).
+template <class PF>
 __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
-                                              int64_t f, double ac, double bc)
+                                              int64_t f, double ac, double bc, PF &pf)
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
@@ -955,46 +915,29 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
         for (int bb = 1; bb < RB; ++bb) A[RB - 1][bb] = s.blk[q + 8 * bb];
     }
     wave_lds_sync();   // s.u[0] is reused by the first publish
-    if constexpr (WCE_DOT_CHOL) {
-        static_assert(!WCE_DOT_CHOL || ROWP == RB - 1, "Cholesky panels: 0..5 in row form");
-        // pivot 0 was eliminated exactly (column 0 is b e_0): the
-        // factorisation starts at pivot 1, whose column the build left final
-        P[1] = cscale(P[1], rsq_nr(readlane_f64(P[1].x, 1)));
-        s.u[1][lane] = P[1];
-        wave_lds_sync();
-        chol_panel<0, 1>(A, P, s, p, q, lane);
-        chol_panel<1>(A, P, s, p, q, lane);
-        chol_panel<2>(A, P, s, p, q, lane);
-        chol_panel<3>(A, P, s, p, q, lane);
-        chol_panel<4>(A, P, s, p, q, lane);
-        chol_panel<5>(A, P, s, p, q, lane);
-        return chol_last(A, s, p, q);
-    }
-    double r = rcp_nr(readlane_f64(P[0].x, 0));
-    s.u[0][lane] = P[0];
+    // pivot 0 was eliminated exactly (column 0 is b e_0): the
+    // factorisation starts at pivot 1, whose column the build left final
+    P[1] = cscale(P[1], rsq_nr(readlane_f64(P[1].x, 1)));
+    s.u[1][lane] = P[1];
     wave_lds_sync();
-    dot_panel<0>(A, P, s, p, q, lane, r);
-    if constexpr (ROWP > 1) dot_panel<1>(A, P, s, p, q, lane, r); else ldl_panel<1>(A, s, p, q, r);
-    if constexpr (ROWP > 2) dot_panel<2>(A, P, s, p, q, lane, r); else ldl_panel<2>(A, s, p, q, r);
-    if constexpr (ROWP > 3) dot_panel<3>(A, P, s, p, q, lane, r); else ldl_panel<3>(A, s, p, q, r);
-    if constexpr (ROWP > 4) dot_panel<4>(A, P, s, p, q, lane, r); else ldl_panel<4>(A, s, p, q, r);
-    if constexpr (ROWP > 5) dot_panel<5>(A, P, s, p, q, lane, r); else ldl_panel<5>(A, s, p, q, r);
-    ldl_panel<6>(A, s, p, q, r);
-    // the last step (pivot 52) updates no trailing element: apply its rank-1
-    // term to (54, 53) here.  Lanes of register block (6, 6): (54, 53) = 53,
-    // (54, 52) = 52, (53, 52) = 44; r = r_52.
-    constexpr int R54 = 8 * (NSC + 1 - 8 * (RB - 1)), R53 = 8 * (NSC - 8 * (RB - 1)), C52 = NSC - 1 - 8 * (RB - 1);
-    const double2 e = readlane_c(A[RB - 1][RB - 1], R54 + C52 + 1);
-    const double2 l54 = readlane_c(A[RB - 1][RB - 1], R54 + C52);
-    const double2 l53 = readlane_c(A[RB - 1][RB - 1], R53 + C52);
-    double2 sc = e;
-    cmsub_conj(sc, cscale(l54, r), l53);
-    return make_double2(-sc.x, -sc.y);   // s = -S(54, 53)
+    chol_panel<0, 1>(A, P, s, p, q, lane);
+    chol_panel<1>(A, P, s, p, q, lane);
+    chol_panel<2>(A, P, s, p, q, lane);
+    chol_panel<3>(A, P, s, p, q, lane);
+    chol_panel<4>(A, P, s, p, q, lane);
+    chol_panel<5>(A, P, s, p, q, lane);
+    pf();
+    return chol_last(A, s, p, q);
 }
 
-template <bool FC, bool DOT = false>
+// no prefetch (every kernel but the config-5 fusion)
+struct NoPrefetch {
+    __device__ __forceinline__ void operator()() {}
+};
+
+template <bool FC, bool DOT = false, class PF = NoPrefetch>
 __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
-                                               int64_t base, int64_t f)
+                                               int64_t base, int64_t f, PF &&pf = PF())
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
@@ -1031,9 +974,10 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
             double2 t = act ? cmul(cmul(wf, s.x[lane]), s.rx[lane]) : make_double2(0, 0);
 #pragma unroll
             for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
+            pf();
             return cscale(t, 1.0 / bc);   // s = w^T X rx / b
         }
-        if (!WCE_DOT_CYCLIC) return dot_factor(st, a, s, f, ac, bc);
+        return dot_factor(st, a, s, f, ac, bc, pf);
     }
     {
         if (FC && ac != 0.0) {   // a X u w^T X': both factors staged in the pivot buffers
@@ -1082,17 +1026,6 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
             for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
         }
-        if constexpr (DOT) {   // bordered row 54 = (w o x)^T; (54, 53) starts at 0 since x_53 = 0
-            const bool act = lane < NSC;
-            const double2 uf = act ? ld2(a.cu, f * a.cs + lane) : make_double2(0, 0);
-            const double2 wf = !act ? make_double2(0, 0) : a.cw ? ld2(a.cw, f * a.cs + lane) : cconj(uf);
-            s.blk[lane] = cmul(wf, s.x[lane]);
-            wave_lds_sync();
-            if (p == NSC + 1 - 8 * (RB - 1)) {
-#pragma unroll
-                for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = s.blk[q + 8 * bb];
-            }
-        }
     }
     // pivot 0 and its column
     double r = rcp_nr(readlane_f64(A[0][0].x, 0));
@@ -1106,18 +1039,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     ldl_panel<5>(A, s, p, q, r);
     ldl_panel<6>(A, s, p, q, r);
     wave_lds_sync();
-    if constexpr (DOT) {
-        // the last step (pivot 52) updates no trailing element: apply its
-        // rank-1 term to (54, 53) here.  Lanes of register block (6, 6):
-        // (54, 53) = 53, (54, 52) = 52, (53, 52) = 44; r = r_52.
-        constexpr int R54 = 8 * (NSC + 1 - 8 * (RB - 1)), R53 = 8 * (NSC - 8 * (RB - 1)), C52 = NSC - 1 - 8 * (RB - 1);
-        const double2 e = readlane_c(A[RB - 1][RB - 1], R54 + C52 + 1);
-        const double2 l54 = readlane_c(A[RB - 1][RB - 1], R54 + C52);
-        const double2 l53 = readlane_c(A[RB - 1][RB - 1], R53 + C52);
-        double2 t = e;
-        cmsub_conj(t, cscale(l54, r), l53);
-        return make_double2(-t.x, -t.y);   // s = -S(54, 53)
-    }
+    pf();
     // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
     double rq[RB];
 #pragma unroll
@@ -1455,7 +1377,7 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
-            if (fb > 256 * 8) fb = 256 * 8;      // grid-stride the rest
+            if (fb > 256 * 8 && variant(WCE_VARIANT_LS) == 0) fb = 256 * 8;   // grid-stride the rest
             hipLaunchKernelGGL(ls_flat_kernel, dim3((unsigned)fb), dim3(256), 0, (hipStream_t)stream, st, a, f0,
                                (uint32_t)nf);
         }
@@ -1494,7 +1416,7 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
             }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
-            if (fb > 256 * 8) fb = 256 * 8;
+            if (fb > 256 * 8 && variant(WCE_VARIANT_REF) == 0) fb = 256 * 8;
             hipLaunchKernelGGL(mmse_ref_flat_kernel, dim3((unsigned)fb), dim3(256), 0, s, st, a, f0, (uint32_t)nf);
         }
         return hip_status(hipGetLastError());

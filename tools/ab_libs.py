@@ -1,0 +1,78 @@
+"""Interleaved A/B of whole libwce.so builds (tools/variants.sh) on one leg,
+one process: rounds x libraries, HIP-event timing per launch.
+legs: config5 (all 5 estimators + equalization fused, fp32 LS/eq outputs,
+per-frame preambles), headline (PS_MMSE TEXTBOOK), dense (COV mmse_solve).
+usage: python tools/ab_libs.py build_variants/A build_variants/B [--leg config5] [--frames 262144]"""
+import argparse
+import importlib.util
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+ap = argparse.ArgumentParser()
+ap.add_argument("dirs", nargs="+")
+ap.add_argument("--leg", choices=["config5", "headline", "dense"], default="config5")
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--frames", type=int, default=262144)
+ap.add_argument("--reps", type=int, default=10)
+args = ap.parse_args()
+N, NB, n = 53, 15, args.frames
+inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
+runs = []
+for d in args.dirs:
+    spec = importlib.util.spec_from_file_location("wce_" + os.path.basename(d.rstrip("/")),
+                                                  os.path.join(REPO, "80211parallelestimation_amd", "wce.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    m._lib = None
+    m.load(os.path.join(d, "libwce.so"))
+    st = m.Stream()
+    if args.leg == "dense":
+        import prof_leg
+        ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rhh())
+    else:
+        ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_TEXTBOOK)
+    tx, rx, pre = m.DeviceArray((n, NB, N)), m.DeviceArray((n, NB, N)), m.DeviceArray((n, N))
+    ctx.synth(tx, rx, pre, n, seed=0x80211)
+    keep = [tx, rx, pre]
+    if args.leg == "config5":
+        outs = [m.DeviceArray((n, N), np.complex64) for _ in range(4)] + [m.DeviceArray((n, N))]
+        eq = m.DeviceArray((n, NB, N), np.complex64)
+        o = m.Outputs(*(x.addr for x in outs), eq.addr, N, NB * N, N, 0, m.OUT_LS_F32)
+        fr = ctx.frames(tx, rx, n, rx_pre=pre)
+        f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.ALL, st.handle))(ctx, fr, o, st, m)
+        keep += outs + [eq]
+        check = outs[4]
+    elif args.leg == "headline":
+        H = m.DeviceArray((n, N))
+        fr = ctx.frames(tx, rx, n)
+        o = m.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+        f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.PS_MMSE, st.handle))(ctx, fr, o, st, m)
+        keep.append(H)
+        check = H
+    else:
+        W = m.DeviceArray((n, N))
+        fr = ctx.frames(tx, rx, n)
+        f = (lambda c, fr, W, st: lambda: c.mmse_solve(fr, W, N, st.handle))(ctx, fr, W, st)
+        keep.append(W)
+        check = W
+    runs.append((os.path.basename(d.rstrip("/")), m, st, f, check, keep, ctx))
+times = {r[0]: [] for r in runs}
+for rd in range(args.rounds):
+    for name, m, st, f, check, keep, ctx in runs:
+        for _ in range(3):
+            f()
+        e0, e1 = m.Event(), m.Event()
+        e0.record(st.handle)
+        for _ in range(args.reps):
+            f()
+        e1.record(st.handle)
+        times[name].append(e0.elapsed_ms(e1) / args.reps)
+outs = [r[4].numpy() for r in runs]
+for (name, *_), o in zip(runs, outs):
+    print(f"{args.leg} {name}: median {np.median(times[name]) * 1e3:.1f} us  "
+          f"({', '.join(f'{t * 1e3:.0f}' for t in times[name])})  same output as {runs[0][0]}: "
+          f"{bool(np.array_equal(o, outs[0]))}")

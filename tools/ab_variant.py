@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 N, NBLK = 53, 15
-WHICH = {"ref": 0, "ls": 1, "dense": 2}
+WHICH = {"ref": 0, "ls": 1, "dense": 2, "headline": 3}
 
 
 def main():
@@ -39,6 +39,17 @@ def main():
         o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
         run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
         alg, unit = bench.BYTES_REF_ALG, "alg"
+    elif args.leg == "headline":
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+        hlt = ctx.shared()[0]
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211, h_shared=wce.DeviceArray.from_numpy(hlt))
+        fr = ctx.frames(tx, rx, n)
+        H = wce.DeviceArray((n, N), zero=True)
+        outs = [H]
+        o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+        run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
+        alg, unit = bench.FLOP_SOLVE_TXT / 1000.0 + bench.FLOP_APPLY / 1000.0, "(= PF/s of F_alg)"
     elif args.leg == "dense":
         # COV mode (full-rank PDP covariance): the dense solve alone (W = X z)
         import prof_leg
