@@ -868,12 +868,9 @@ __device__ __forceinline__ void exact_first_step(const SolveArgs &a, SolveLds &s
 // The rank-1 read-out path (a != 0): Ryy = a (x o u)(w o x')^T + b I bordered
 // by conj(rx) (row 53) and (w o x)^T (row 54), factorised with row-per-lane
 // Cholesky panels 0..5 (chol_panel) and the block-cyclic last panel
-// (chol_last); returns s = -S(54, 53) = w^T X Ryy^-1 rx.  pf() is called
-// before the last panel, when most of the matrix registers are dead: the
-// config-5 kernel issues its epilogue's loads there (LsPrefetch).
-template <class PF>
+// (chol_last); returns s = -S(54, 53) = w^T X Ryy^-1 rx.
 __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
-                                              int64_t f, double ac, double bc, PF &pf)
+                                              int64_t f, double ac, double bc)
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
@@ -926,18 +923,12 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     chol_panel<3>(A, P, s, p, q, lane);
     chol_panel<4>(A, P, s, p, q, lane);
     chol_panel<5>(A, P, s, p, q, lane);
-    pf();
     return chol_last(A, s, p, q);
 }
 
-// no prefetch (every kernel but the config-5 fusion)
-struct NoPrefetch {
-    __device__ __forceinline__ void operator()() {}
-};
-
-template <bool FC, bool DOT = false, class PF = NoPrefetch>
+template <bool FC, bool DOT = false>
 __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
-                                               int64_t base, int64_t f, PF &&pf = PF())
+                                               int64_t base, int64_t f)
 {
     const int lane = threadIdx.x;
     const int p = lane >> 3, q = lane & 7;
@@ -974,10 +965,9 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
             double2 t = act ? cmul(cmul(wf, s.x[lane]), s.rx[lane]) : make_double2(0, 0);
 #pragma unroll
             for (int m = 32; m >= 1; m >>= 1) t = cadd(t, shfl_xor_c(t, m));
-            pf();
             return cscale(t, 1.0 / bc);   // s = w^T X rx / b
         }
-        return dot_factor(st, a, s, f, ac, bc, pf);
+        return dot_factor(st, a, s, f, ac, bc);
     }
     {
         if (FC && ac != 0.0) {   // a X u w^T X': both factors staged in the pivot buffers
@@ -1039,7 +1029,6 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     ldl_panel<5>(A, s, p, q, r);
     ldl_panel<6>(A, s, p, q, r);
     wave_lds_sync();
-    pf();
     // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
     double rq[RB];
 #pragma unroll
