@@ -43,7 +43,7 @@ for d in args.dirs:
             for off in range(0, n, chunk):
                 k = min(chunk, n - off)
                 for dst, h in ((tx, txh), (rx, rxh), (pre, preh)):
-                    lib.wce_memcpy_htod(dst.addr + off * N * 16, h[:k].ctypes.data, k * N * 16)
+                    assert lib.wce_memcpy_htod(dst.addr + off * N * 16, h[:k].ctypes.data, k * N * 16) == 0
             bsets.append((tx, rx, pre, [m.DeviceArray((n, args.ostride)) for _ in range(4)]))
     for si, (tx, rx, pre, outs) in enumerate(bsets):
         o = m.Outputs(*(x.addr for x in outs), None, None, args.ostride, 0, 0, 0, 0)

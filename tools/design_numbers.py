@@ -1,78 +1,127 @@
-"""Regenerate DESIGN.md's measurement table (section 6) from profiles/<round>_bench.json
-and profiles/<round>_pmc_summary.json, so the document never drifts from the
-committed evidence.  usage: python tools/design_numbers.py [r01]"""
+"""Regenerate DESIGN.md's measurement table (section 6) and its PMC
+paragraph from profiles/<round>_bench.json and profiles/<round>_pmc_legs.json,
+so the document never drifts from the committed evidence.
+usage: python tools/design_numbers.py [r02]"""
 import json
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+rnd = sys.argv[1] if len(sys.argv) > 1 else "r02"
 d = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_bench.json")))
-pm = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_pmc_headline.json")))
+legs = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_pmc_legs.json")))
 r = d["roofline"]
 refc = d["cpu_baseline"].get("reference_code", {})
-hp = d.get("host_pipeline")
-host_row = (f"| headline from pinned HOST memory (PCIe-inclusive; never `value`) | {hp['frames_per_s']:.3g} frames/s, "
-            f"{hp['pcie_GBs']:.0f} GB/s over PCIe ({hp['pcie_bytes_per_frame']} B per frame: tx, rx block 0 in, H out), "
-            f"{hp['ms_per_batch']:.2f} ms per 65,536 frames; bit-identical to the device-resident path: {hp['bit_identical_to_device_path']} |"
-            if hp else "| headline from pinned host memory | not measured in this bench line |")
+rows = []   # (quantity, value); None entries are skipped (never a blank table line)
+
+
+def row(q, v):
+    rows.append((q, v))
+
+
+row("MMSE frames/s, TEXTBOOK (headline)", f"**{d['value']:.3g}** (target ≥1e7)")
+row("`mmse_solve_fc_kernel` (the whole step: one launch)",
+    f"{r['avg_launch_ms']:.3f} ms per 65,536 frames. **{r['achieved']:.1f} TFLOP/s = {100 * r['frac']:.1f}%** of the FP64 "
+    f"spec peak by SURVEY's F_alg; executed flops {r['achieved_executed']:.1f} TFLOP/s = {100 * r['frac_executed']:.1f}%")
 c4, c5s = d.get("config4"), d.get("config5_sharded")
-c4_row = ""
 if c4:
-    c4_row += (f"| BASELINE configs[3] batch (1,048,576 frames, sharded over {c4['n_gpus']} GPU(s), strong scaling) | "
-               f"{c4['frames_per_s']:.3g} frames/s |")
+    row(f"BASELINE configs[3] batch (1,048,576 frames, sharded over {c4['n_gpus']} GPU(s), strong scaling)",
+        f"{c4['frames_per_s']:.3g} frames/s")
 if c5s:
-    c4_row += ("\n" if c4_row else "") + (f"| BASELINE configs[4] as named (1,048,576 frames, all 5 + eq fused, fp64 solve / fp32 LS, "
-               f"sharded over {c5s['n_gpus']} GPU(s)) | {c5s['frames_per_s']:.3g} frames/s |")
+    row(f"BASELINE configs[4] as named (1,048,576 frames, all 5 + eq fused, fp64 solve / fp32 LS, sharded over "
+        f"{c5s['n_gpus']} GPU(s))", f"{c5s['frames_per_s']:.3g} frames/s; non-finite outputs: {c5s.get('nonfinite_outputs')}")
+row("MMSE frames/s, REF (diagonal Ryy: no factorisation), 65,536 frames (MALL-resident)",
+    f"{d['ref_mode']['frames_per_s_per_gpu']:.3g}")
+rb = d["ref_mode"].get("b1048576")
+if rb:
+    rr = rb["roofline"]
+    row("REF, 1,048,576 frames (past the MALL), `mmse_ref_flat_kernel`",
+        f"{rb['frames_per_s']:.3g} frames/s; {rr['achieved'] / 1000:.2f} TB/s algorithmic (976 B/frame) = "
+        f"{100 * rr['frac']:.0f}% of 8 TB/s; {rr['achieved_sector_GBs'] / 1000:.2f} TB/s on the 1,360-B sector floor = "
+        f"{100 * rr['frac_sector']:.0f}%; PMC traffic {rr['traffic'] / rb['frames']:.0f} B/frame")
+cv = d["cov_mode"]
+row("MMSE with a dense model covariance (COV: LDLᴴ + back-substitution, then MFMA `C·W`)",
+    f"{cv['frames_per_s_per_gpu']:.3g} frames/s; solve {cv['solve_tflops']:.1f} TFLOP/s = "
+    f"{100 * cv['solve_frac_fp64_peak']:.0f}% of FP64 peak")
+ap = d["apply_kernel"]
+row("`matvec_kernel` as `H = C·W` (f64 MFMA, COV mode, 65,536 frames = 4,096 waves)",
+    f"{ap['achieved_tflops']:.1f} TFLOP/s algorithmic = {100 * ap['frac_fp64_peak']:.0f}% of FP64 peak; "
+    + (f"{ap['executed_tflops']:.1f} TFLOP/s executed; MFMA pipe busy {100 * ap['mfma_busy_frac_pmc']:.0f}% (PMC of "
+       f"same-size launches); traffic {ap['traffic'] / 1e6:.0f} MB vs {ap['algorithmic_bytes'] / 1e6:.0f} MB algorithmic"
+       if "executed_tflops" in ap else "no same-size PMC"))
+row("per-frame covariance MMSE (`FRAME_COV`)",
+    f"{d['frame_cov']['textbook']['frames_per_s']:.3g} frames/s TEXTBOOK, {d['frame_cov']['ref']['frames_per_s']:.3g} REF")
+row("config 5 share (131,072 frames, all 5 + equalization, fused)",
+    f"{d['config5']['fp64']['frames_per_s']:.3g} frames/s fp64; "
+    f"{d['config5']['mixed_fp64_solve_fp32_ls']['frames_per_s']:.3g} with fp32 LS outputs")
+ls = d["ls_config2"]["b1048576"]
+row("LS config 2 (LT_LS + PS_Linear), 1,048,576 frames",
+    f"{ls['achieved_GBs'] / 1000:.2f} TB/s algorithmic = {100 * ls['frac']:.0f}% of 8 TB/s; "
+    + (f"{ls['real_GBs'] / 1000:.2f} TB/s of PMC-measured HBM traffic ({ls['traffic_bytes_per_frame']:.0f} B/frame); "
+       if "real_GBs" in ls else "") + f"{ls['frames_per_s']:.2g} frames/s")
+l65 = d["ls_config2"]["b65536"]
+row("LS config 2, 65,536 frames (MALL-resident)", f"{l65['achieved_GBs'] / 1000:.2f} TB/s, {l65['frames_per_s']:.2g} frames/s")
+fe = d["front_end"]
+row("front end, 65,536 frames × 15 blocks",
+    f"{fe['blocks']['achieved_GBs'] / 1000:.2f} TB/s = {100 * fe['blocks']['frac']:.1f}% of 8 TB/s; "
+    f"LTF {fe['preamble']['achieved_GBs'] / 1000:.2f} TB/s")
+ns = d["ls_config2"]["nonfinite_scan"]
+row("non-finite guard (`wce_nonfinite_scan`), 1,048,576 LT_LS outputs",
+    f"{ns['achieved_GBs'] / 1000:.2f} TB/s = {100 * ns['frac']:.1f}% of 8 TB/s; headline output non-finite frames: "
+    f"{d['nonfinite_frames']}")
 sb = d["small_batch"]
-mlsb = (f"; MATLAB + FRAME_COV (several kernels): {sb['matlab_frame_cov_direct']['us_per_call']:.0f} µs direct, "
-        f"{sb['matlab_frame_cov_plan']['us_per_call']:.0f} µs as a plan" if "matlab_frame_cov_plan" in sb else "")
-table = f"""| Quantity | Value |
-|---|---|
-| MMSE frames/s, TEXTBOOK (headline) | **{d['value']:.3g}** (target ≥1e7) |
-| `mmse_solve_fc_kernel` (the whole step: one launch) | {r['avg_launch_ms']:.3f} ms per 65,536 frames. **{r['achieved']:.1f} TFLOP/s = {100 * r['frac']:.1f}%** of FP64 spec peak by SURVEY's F_alg. Executed flops: {r['achieved_executed']:.1f} TFLOP/s = {100 * r['achieved_executed'] / 78.6:.1f}% |
-{c4_row}
-| MMSE frames/s, REF (diagonal Ryy: no factorisation) | {d['ref_mode']['frames_per_s_per_gpu']:.3g} |
-| MMSE with a dense model covariance (COV: back-substitution + MFMA GEMM) | {d['cov_mode']['frames_per_s_per_gpu']:.3g} frames/s; solve {d['cov_mode']['solve_tflops']:.1f} TFLOP/s |
-| `matvec_kernel` as `H = C·W` (MFMA, COV mode) | {d['apply_kernel']['achieved_tflops']:.0f} TFLOP/s = {100 * d['apply_kernel']['frac_fp64_peak']:.0f}% of FP64 peak |
-| per-frame covariance MMSE (`FRAME_COV`) | {d['frame_cov']['textbook']['frames_per_s']:.3g} frames/s TEXTBOOK, {d['frame_cov']['ref']['frames_per_s']:.3g} REF |
-| config 5 (131,072 frames, all 5 + equalization, fused) | {d['config5']['fp64']['frames_per_s']:.3g} frames/s fp64; {d['config5']['mixed_fp64_solve_fp32_ls']['frames_per_s']:.3g} with fp32 LS outputs |
-| LS config 2 (LT_LS + PS_Linear), 1,048,576 frames | {d['ls_config2']['b1048576']['achieved_GBs'] / 1000:.2f} TB/s algorithmic = {100 * d['ls_config2']['b1048576']['frac']:.0f}% of 8 TB/s; {d['ls_config2']['b1048576'].get('real_GBs', 0) / 1000:.2f} TB/s of PMC-measured HBM traffic (pilot sectors counted); {d['ls_config2']['b1048576']['frames_per_s']:.2g} frames/s |
-| LS config 2, 65,536 frames (MALL-resident) | {d['ls_config2']['b65536']['achieved_GBs'] / 1000:.2f} TB/s, {d['ls_config2']['b65536']['frames_per_s']:.2g} frames/s |
-| front end, 65,536 frames × 15 blocks | {d['front_end']['blocks']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['front_end']['blocks']['frac']:.1f}% of 8 TB/s (PMC traffic = algorithmic bytes to 1e-4); LTF {d['front_end']['preamble']['achieved_GBs'] / 1000:.2f} TB/s |
-| non-finite guard (`wce_nonfinite_scan`), 1,048,576 LT_LS outputs | {d['ls_config2']['nonfinite_scan']['achieved_GBs'] / 1000:.2f} TB/s = {100 * d['ls_config2']['nonfinite_scan']['frac']:.1f}% of 8 TB/s; headline output non-finite frames: {d['nonfinite_frames']} |
-| small batches (1,024 frames, all 5 + eq) | {d['small_batch']['direct']['us_per_call']:.0f} µs per call direct, {d['small_batch']['plan']['us_per_call']:.0f} µs as a replayed HIP-graph plan{mlsb} |
-{host_row}
-| CPU baseline (oracle fp64 port, 16 host cores, dense path) | {d['cpu_baseline']['value']:.2g} MMSE frames/s (4–6e5, host-load dependent) |
-"""
+row("small batches (1,024 frames, all 5 + eq)",
+    f"{sb['direct']['us_per_call']:.0f} µs per call direct, {sb['plan']['us_per_call']:.0f} µs as a replayed "
+    f"HIP-graph plan; MATLAB + FRAME_COV (several kernels): {sb['matlab_frame_cov_direct']['us_per_call']:.0f} µs "
+    f"direct, {sb['matlab_frame_cov_plan']['us_per_call']:.0f} µs as a plan")
+hp = d.get("host_pipeline")
+if hp:
+    row("headline from pinned HOST memory (PCIe-inclusive; never `value`)",
+        f"{hp['frames_per_s']:.3g} frames/s, {hp['pcie_GBs']:.0f} GB/s over PCIe ({hp['pcie_bytes_per_frame']} B per "
+        f"frame), {100 * hp['frac_of_h2d_bound']:.0f}% of the H2D copy bound; bit-identical to the device-resident "
+        f"path: {hp['bit_identical_to_device_path']}")
+cb = d["cpu_baseline"]
+row(f"CPU baseline (oracle fp64 port, {cb['cores']} host cores, dense path)",
+    f"{cb['value']:.2g} MMSE frames/s; its H vs the GPU's on the same {cb.get('err_frames', 0)} frames: max "
+    f"{cb.get('max_normrel_err_vs_gpu', float('nan')):.1e} norm-relative")
 if refc:
-    table += (f"| the reference's own code (`oracle/_ref`, 1 core) | LT_LS + PS_Linear {refc['ls_config2']['value']:.2g} frames/s; "
-              f"REF-mode PS_MMSE through its matrix routines {refc['mmse_ref_mode']['value']:.0f} frames/s "
-              f"(NaN inverse repaired, per-frame 4-s `inverse(F)` hoisted) |\n")
+    row("the reference's own code (`oracle/_ref`, 1 core)",
+        f"LT_LS + PS_Linear {refc['ls_config2']['value']:.2g} frames/s; REF-mode PS_MMSE through its matrix routines "
+        f"{refc['mmse_ref_mode']['value']:.0f} frames/s (NaN inverse repaired, per-frame 4-s `inverse(F)` hoisted)")
     if "ls_config2_omp" in refc:
-        table += (f"| the reference's own functions, frames-parallel OpenMP loop ({refc['ls_config2_omp']['cores']} host cores; "
-                  f"its own OpenMP driver crashes) | LT_LS + PS_Linear {refc['ls_config2_omp']['value']:.2g} frames/s; "
-                  f"REF-mode PS_MMSE {refc['mmse_ref_mode_omp']['value']:.0f} frames/s |\n")
-table += "| reference `main.c` MMSE as written | ~0.004 frames/s, 1 core, NaN output; best published number 0.18 frames/s over 20 MPI ranks |\n"
-k = [x for x in pm if x.endswith("mmse_solve_fc_kernel")]
+        row(f"the reference's own functions, frames-parallel OpenMP loop ({refc['ls_config2_omp']['cores']} host "
+            f"cores; its own OpenMP driver crashes)",
+            f"LT_LS + PS_Linear {refc['ls_config2_omp']['value']:.2g} frames/s; REF-mode PS_MMSE "
+            f"{refc['mmse_ref_mode_omp']['value']:.0f} frames/s")
+row("reference `main.c` MMSE as written", "~0.004 frames/s, 1 core, NaN output; best published number 0.18 frames/s "
+    "over 20 MPI ranks")
+table = "| Quantity | Value |\n|---|---|\n" + "".join(f"| {q} | {v} |\n" for q, v in rows if q)
+
+h = legs.get("headline")
 pmc = ""
-if k:
-    v = {c: x / 65536 for c, x in pm[k[0]].items()}
+if h:
+    n = h["frames"]
+    v = {c: x / n for c, x in h["counters"].items()}
     busy = 3 * v["SQ_ACTIVE_INST_VALU"] / v["SQ_WAVE_CYCLES"]
-    traffic = (2 * pm[k[0]]["FETCH_SIZE"] + pm[k[0]]["WRITE_SIZE"]) * 1024 / 1e6
-    pmc = f"""**PMC**, `mmse_solve_fc_kernel`, headline run only (TEXTBOOK), per frame (= per wave). Source: `profiles/{rnd}_pmc_headline.json`, collected with `tools/refresh_profiles.sh`, one pass per counter group.
-- {v['SQ_INSTS_VALU']:,.0f} VALU instructions, of which {v['SQ_INSTS_VALU_FMA_F64']:,.0f} are `FMA_F64` and {v['SQ_INSTS_VALU_MUL_F64']:,.0f} `MUL_F64`.
-- {v['SQ_INSTS_LDS']:,.0f} LDS instructions with {v['SQ_LDS_BANK_CONFLICT']:.0f} bank conflicts.
-- VALU active {v['SQ_ACTIVE_INST_VALU']:,.0f} of {v['SQ_WAVE_CYCLES']:,.0f} quad-cycles per wave. Over 3 co-resident waves that is ≈{100 * busy:.0f}% of SIMD time.
-- HBM: FETCH_SIZE×2 + WRITE_SIZE = {traffic:.0f} MB per 65,536-frame launch, against 167 MB algorithmic.
-"""
+    traffic = (2 * h["counters"]["FETCH_SIZE"] + h["counters"]["WRITE_SIZE"]) * 1024 / 1e6
+    pmc = (f"**PMC**, `mmse_solve_fc_kernel` alone at the bench's launch size (65,536 frames, {h['dispatches']} "
+           f"dispatches per pass), per frame (= per wave). Source: `profiles/{rnd}_pmc_legs.json` "
+           f"(`tools/pmc_legs.sh`, one pass per counter group).\n"
+           f"- {v['SQ_INSTS_VALU']:,.0f} VALU instructions, of which {v['SQ_INSTS_VALU_FMA_F64']:,.0f} are `FMA_F64` and "
+           f"{v['SQ_INSTS_VALU_MUL_F64']:,.0f} `MUL_F64`.\n"
+           f"- {v['SQ_INSTS_LDS']:,.0f} LDS instructions with {v['SQ_LDS_BANK_CONFLICT']:.0f} bank conflicts.\n"
+           f"- VALU active {v['SQ_ACTIVE_INST_VALU']:,.0f} of {v['SQ_WAVE_CYCLES']:,.0f} quad-cycles per wave. Over 3 "
+           f"co-resident waves that is ≈{100 * busy:.0f}% of SIMD time.\n"
+           f"- HBM: FETCH_SIZE×2 + WRITE_SIZE = {traffic:.0f} MB per 65,536-frame launch, against 167 MB algorithmic.\n")
 p = os.path.join(REPO, "DESIGN.md")
 s = open(p).read()
 a = s.index("| Quantity | Value |")
 b = s.index("The bench brings the GPU to its steady clock")
 s = s[:a] + table + "\n" + s[b:]
-a = s.index("**PMC**, `mmse_solve")
-b = s.index("**What limits it now**")
-s = s[:a] + pmc + "\n" + s[b:]
+if pmc:
+    a = s.index("**PMC**, `mmse_solve")
+    b = s.index("**What limits it now**")
+    s = s[:a] + pmc + "\n" + s[b:]
 open(p, "w").write(s)
 print(table)
+print(pmc)
