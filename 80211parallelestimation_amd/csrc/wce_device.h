@@ -24,10 +24,22 @@ __device__ __forceinline__ double rcp_nr(double d)
     e = fma(-d, r, 1.0);
     return fma(r, e, r);
 }
+// a / b.  Contraction is off here and the fmas are spelled out, so that every
+// kernel that divides -- the LS kernels, the fused epilogue -- rounds alike
+// whatever consumes the quotient (a kernel that feeds it straight into
+// clerp would otherwise fuse the quotient's product into the subtraction),
+// and their outputs stay bit-identical to each other.
 __device__ __forceinline__ double2 cdiv(double2 a, double2 b)
 {
-    const double inv = rcp_nr(b.x * b.x + b.y * b.y);
-    return make_double2((a.x * b.x + a.y * b.y) * inv, (a.y * b.x - a.x * b.y) * inv);
+#pragma clang fp contract(off)
+    const double inv = rcp_nr(fma(b.x, b.x, b.y * b.y));
+    return make_double2(fma(a.x, b.x, a.y * b.y) * inv, fma(a.y, b.x, -(a.x * b.y)) * inv);
+}
+// lo + (hi - lo) alpha (main.c:86-99's linear interpolation), one rounding order everywhere
+__device__ __forceinline__ double2 clerp(double2 lo, double2 hi, double alpha)
+{
+#pragma clang fp contract(off)
+    return make_double2(fma(hi.x - lo.x, alpha, lo.x), fma(hi.y - lo.y, alpha, lo.y));
 }
 // acc -= l * conj(c)   (4 DFMA)
 __device__ __forceinline__ void cmsub_conj(double2 &acc, double2 l, double2 c)

@@ -130,8 +130,10 @@ int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t 
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
 // kernel variants for A/B timing (wce_debug_set_variant)
-constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks, 1 = 64-frame tiles
-constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks, 1 = 64-frame tiles
+constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks (default), 1 = 64-frame tiles,
+                                      // 2 = chunks with an uncapped grid
+constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks (grid capped at 2,048 blocks),
+                                      // 1 = the same uncapped, 2 = one element per thread (ls_elem_kernel, default)
 constexpr int WCE_VARIANT_COUNT = 4;
 int set_variant(int which, int value);
 int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,

@@ -94,7 +94,7 @@ __device__ __forceinline__ void ps_lane(const LsLane &c, uint32_t mask, double2 
     if (mask & (WCE_EST_PS_LINEAR | WCE_EQUALIZE)) {      // main.c:86-99
         const double2 lo = c.seg == 0 ? h0 : (c.seg == 1 ? h1 : h2);
         const double2 hi = c.seg == 0 ? h1 : (c.seg == 1 ? h2 : h3);
-        hlin = cadd(lo, cscale(csub(hi, lo), c.alpha));
+        hlin = clerp(lo, hi, c.alpha);
     }
     if (mask & WCE_EST_PS_CUBIC) {         // main.c:112-121, every divisor 14
         const double r = 1.0 / 14.0;     // MATLAB (PS_Cubic.m:11-13): 14, 28, 42
@@ -343,10 +343,61 @@ __global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ 
                 const int fl = (int)(f - ff) * 4 + seg;
                 const double2 lo = hp_tab[fl < 4 * FLAT_FR - 1 ? fl : 4 * FLAT_FR - 2];
                 const double2 hi = hp_tab[fl < 4 * FLAT_FR - 1 ? fl + 1 : 4 * FLAT_FR - 1];
-                if (e < E) st_out(a.lin, o, cadd(lo, cscale(csub(hi, lo), alpha)), f32);
+                if (e < E) st_out(a.lin, o, clerp(lo, hi, alpha), f32);
             }
         }
         wave_lds_sync();                                    // hp_tab is rewritten by the next chunk
+    }
+}
+
+// One (frame, subcarrier) element per thread, no grid stride (round 2): the
+// store pattern that streams fastest on MI355X (7.0 TB/s one-shot against
+// 4.7 TB/s grid-strided, profiles/r02_ubench_hbm.txt).  Each lane loads the
+// two pilot pairs its linear segment needs (the lanes of a wave cover ~1.2
+// frames, so one pilot load instruction touches ~2 sectors) and divides them
+// itself; the arithmetic is ls_kernel's, so outputs are bit-identical.
+__global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ st, LsArgs a, int64_t f_begin,
+                                                      uint32_t nfr)
+{
+    __shared__ double2 s_txp[64], s_hlt[64];
+    if (threadIdx.x < NSC) {
+        s_txp[threadIdx.x] = ld2(a.tx_pre ? a.tx_pre : st->tx_pre, threadIdx.x);
+        s_hlt[threadIdx.x] = ld2(st->h_lt, threadIdx.x);
+    }
+    __syncthreads();
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= nfr * (uint32_t)NSC) return;
+    const uint32_t f = e / NSC, k = e - f * NSC;
+    const bool do_lt = (a.mask & WCE_EST_LT_LS) && a.lt, do_lin = (a.mask & WCE_EST_PS_LINEAR) && a.lin;
+    const bool f32 = a.f32 != 0;
+    const int64_t fg = f_begin + f;
+    const int seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
+    double2 plo_t = make_double2(1, 0), plo_r = make_double2(0, 0), phi_t = plo_t, phi_r = plo_r, rp = plo_r;
+    if (do_lin) {
+        const int64_t o = fg * a.fs + (int64_t)a.blk * a.bs;
+        const int plo = seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2);
+        const int phi = seg == 0 ? WCE_P1 : (seg == 1 ? WCE_P2 : WCE_P3);
+        plo_t = ld2(a.tx, o + plo);
+        plo_r = ld2(a.rx, o + plo);
+        phi_t = ld2(a.tx, o + phi);
+        phi_r = ld2(a.rx, o + phi);
+    }
+    if (do_lt && a.rx_pre) rp = ld2(a.rx_pre, fg * a.ps + k);
+    const int64_t out = fg * a.os + k;
+    if (do_lt) {                                    // main.c:66-75
+        double2 h = s_hlt[k];
+        if (a.rx_pre) {
+            const double2 t = s_txp[k];
+            const double cq = t.x - t.y;
+            h = cdiv(make_double2(cq * rp.x, cq * rp.y), make_double2(cq * t.x, cq * t.y));
+        }
+        if (k == WCE_DC) h = make_double2(0, 0);
+        st_out(a.lt, out, h, f32);
+    }
+    if (do_lin) {                                   // main.c:82-99
+        const double alpha = (double)((int)k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) * (1.0 / 14.0);
+        const double2 lo = cdiv(plo_r, plo_t), hi = cdiv(phi_r, phi_t);
+        st_out(a.lin, out, clerp(lo, hi, alpha), f32);
     }
 }
 
@@ -1327,7 +1378,7 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 
 // A/B kernel variants, process-wide (wce_debug_set_variant): lets one process
 // time two kernels on the same buffers, interleaved.  Defaults = the product.
-static int g_variant[WCE_VARIANT_COUNT] = {0, 0, 0, 0};
+static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, 0};
 int set_variant(int which, int value)
 {
     if (which < 0 || which >= WCE_VARIANT_COUNT || value < 0 || value > 15) return WCE_EINVAL;
@@ -1364,6 +1415,12 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
         (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0) {
         for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
+            if (variant(WCE_VARIANT_LS) == 2) {
+                const int64_t blocks = (nf * NSC + 255) / 256;
+                hipLaunchKernelGGL(ls_elem_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a,
+                                   f0, (uint32_t)nf);
+                continue;
+            }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
             if (fb > 256 * 8 && variant(WCE_VARIANT_LS) == 0) fb = 256 * 8;   // grid-stride the rest

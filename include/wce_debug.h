@@ -25,9 +25,11 @@ int wce_debug_set_border_dot(struct wce_ctx *ctx, int on);
  * sizes.  0 restores the default.  Process-wide. */
 int wce_debug_set_flat_chunk(long long frames);
 /* Kernel variant knobs for interleaved A/B timing in one process (same
- * buffers, same placement).  which 0: REF PS_MMSE (0 = 512-element chunks, default,
- * 1 = 64-frame tiles); which 1: LT_LS + PS_Linear (same choices).
- * Process-wide; results are identical across variants (tests check it). */
+ * buffers, same placement).  which 0: REF PS_MMSE (0 = 512-element chunks,
+ * default; 1 = 64-frame tiles; 2 = chunks, uncapped grid).  which 1: LT_LS +
+ * PS_Linear in C semantics (0 = 512-element chunks, grid capped at 2,048
+ * blocks; 1 = the same uncapped; 2 = one element per thread, default).
+ * Process-wide; every variant gives bit-identical results (tests check it). */
 int wce_debug_set_variant(int which, int value);
 #ifdef __cplusplus
 }

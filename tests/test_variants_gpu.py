@@ -1,0 +1,65 @@
+"""The HBM kernels' A/B variants (wce_debug_set_variant) are interchangeable:
+bit-identical outputs on ragged batch sizes, across launch splits
+(wce_debug_set_flat_chunk), for fp64 and fp32 outputs.  The product default
+is the last variant of each list (LS: one element per thread; REF: chunks)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N, NBLK = 53, 15
+
+
+@pytest.fixture()
+def lib(gpu_wce):
+    lib = gpu_wce.load()
+    yield lib
+    assert lib.wce_debug_set_variant(0, 0) == 0
+    assert lib.wce_debug_set_variant(1, 2) == 0
+    assert lib.wce_debug_set_flat_chunk(ctypes.c_longlong(0)) == 0
+
+
+@pytest.mark.parametrize("chunk", [0, 4096])
+def test_ls_variants_identical(gpu_wce, golden, lib, chunk):
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    B = 40003
+    tx, rx, pre = gpu_wce.DeviceArray((B, NBLK, N)), gpu_wce.DeviceArray((B, NBLK, N)), gpu_wce.DeviceArray((B, N))
+    ctx.synth(tx, rx, pre, B, seed=0x1A)
+    assert lib.wce_debug_set_flat_chunk(ctypes.c_longlong(chunk)) == 0
+    for f32, dt in ((0, np.complex128), (gpu_wce.OUT_LS_F32, np.complex64)):
+        got = []
+        for v in (0, 1, 2):
+            assert lib.wce_debug_set_variant(1, v) == 0
+            lt, lin = gpu_wce.DeviceArray((B, N), dt, zero=True), gpu_wce.DeviceArray((B, N), dt, zero=True)
+            ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre),
+                         gpu_wce.Outputs(lt.addr, lin.addr, None, None, None, None, N, 0, 0, 0, f32),
+                         gpu_wce.LT_LS | gpu_wce.PS_LINEAR)
+            gpu_wce.synchronize()
+            got.append((lt.numpy(), lin.numpy()))
+        for v in (1, 2):
+            assert np.array_equal(got[v][0], got[0][0]) and np.array_equal(got[v][1], got[0][1]), (f32, v)
+
+
+@pytest.mark.parametrize("frame_cov", [False, True])
+def test_ref_variants_identical(gpu_wce, golden, lib, frame_cov):
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    B = 33331
+    tx, rx, pre = gpu_wce.DeviceArray((B, NBLK, N)), gpu_wce.DeviceArray((B, NBLK, N)), gpu_wce.DeviceArray((B, N))
+    ctx.synth(tx, rx, pre, B, seed=0x2B)
+    ctx.reserve(B)
+    mask = gpu_wce.PS_MMSE | (gpu_wce.FRAME_COV if frame_cov else 0)
+    got = []
+    for v in (0, 1, 2):
+        assert lib.wce_debug_set_variant(0, v) == 0
+        H = gpu_wce.DeviceArray((B, N), zero=True)
+        ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre if frame_cov else None),
+                     gpu_wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0), mask)
+        gpu_wce.synchronize()
+        got.append(H.numpy())
+    assert np.isfinite(got[0]).all()
+    for v in (1, 2):
+        assert np.array_equal(got[v], got[0]), v
