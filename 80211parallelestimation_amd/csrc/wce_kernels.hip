@@ -611,6 +611,69 @@ __device__ __forceinline__ double rsq_nr(double d)
     return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
+#ifndef WCE_MASK_DEAD   // A/B: exec-mask the lanes whose updates are never read
+#define WCE_MASK_DEAD 1
+#endif
+// acc -= l conj(c) on the lanes of the (compile-time) lane mask m only.  The
+// other lanes carry elements that are never read (upper halves of diagonal
+// blocks, padding row 55, rows above the pivot in a row panel).  With
+// WCE_MASK_DEAD their FMAs are switched off in EXEC for the four FMAs (and
+// EXEC restored) inside one asm statement: written as a C++ branch the
+// compiler turns it into selects and divergent control flow that spills.
+// The masked lanes keep their old (dead) values: "+v" ties in to out.
+__device__ __forceinline__ void cmsub_live(uint64_t m, double2 &acc, double2 l, double2 c)
+{
+    if (WCE_MASK_DEAD && m != ~0ull) {
+        // m & EXEC is formed by the compiler: the asm itself writes no SCC
+        // (an s_and_b64 in here would clobber an SCC live across it)
+        const uint64_t em = m & __builtin_amdgcn_read_exec();
+        uint64_t sv;
+        asm("s_mov_b64 %[sv], exec\n\t"
+            "s_mov_b64 exec, %[m]\n\t"
+            "v_fma_f64 %[ax], -%[lx], %[cx], %[ax]\n\t"
+            "v_fma_f64 %[ax], -%[ly], %[cy], %[ax]\n\t"
+            "v_fma_f64 %[ay], -%[ly], %[cx], %[ay]\n\t"
+            "v_fma_f64 %[ay], %[lx], %[cy], %[ay]\n\t"
+            "s_mov_b64 exec, %[sv]"
+            : [ax] "+v"(acc.x), [ay] "+v"(acc.y), [sv] "=&s"(sv)
+            : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(c.x), [cy] "v"(c.y), [m] "s"(em));
+    } else {
+        cmsub_conj(acc, l, c);
+    }
+}
+// compile-time lane masks (lane = 8p + q)
+constexpr uint64_t lanes_from(int lo, int hi)   // lanes lo..hi
+{
+    uint64_t m = 0;
+    for (int l = lo; l <= hi && l < 64; ++l) m |= 1ull << l;
+    return m;
+}
+constexpr uint64_t lanes_lower(int qmin)   // q <= p, p < 7, q > qmin
+{
+    uint64_t m = 0;
+    for (int p = 0; p < 7; ++p)
+        for (int q = qmin + 1; q <= p; ++q) m |= 1ull << (8 * p + q);
+    return m;
+}
+constexpr uint64_t kRows55 = lanes_from(0, 55);   // p < 7: block row 6 without padding row 55
+
+// Trailing block column BB: the diagonal block keeps its lower triangle
+// (q <= p; in block 6 that includes the (54, 53) corner), and block row 6
+// has no row 55 (p < 7).  cm: lanes whose column is still live (all but the
+// LDL lookahead's own block column).
+constexpr uint64_t kLower = lanes_lower(-1) | ~kRows55;   // q <= p, block rows 0..5
+template <int BB>
+__device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v, uint64_t cm = ~0ull)
+{
+    if constexpr (BB == RB - 1) {
+        cmsub_live(cm & lanes_lower(-1), A[BB][BB], Ur[BB], v);
+    } else {
+        cmsub_live(cm & kLower, A[BB][BB], Ur[BB], v);
+#pragma unroll
+        for (int aa = BB + 1; aa < RB - 1; ++aa) cmsub_live(cm, A[aa][BB], Ur[aa], v);
+        cmsub_live(cm & kRows55, A[RB - 1][BB], Ur[RB - 1], v);
+    }
+}
 // A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
 template <int BB>
 __device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v)
@@ -627,7 +690,7 @@ __device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double
                                               int q, double r)
 {
     if constexpr (BB < RB) {
-        upd_col<BB>(A, Ur, cscale(col[q + 8 * BB], r));
+        upd_col_live<BB>(A, Ur, cscale(col[q + 8 * BB], r));
         upd_cols_from<BB + 1>(A, Ur, col, q, r);
     }
 }
@@ -661,12 +724,17 @@ __device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int 
     if constexpr (NEXT_IN_BLOCK) {
         // lookahead: columns > k of block KB first; the lane mask is folded into r
         const double rm = (q > kq) ? rk : 0.0;
-        upd_col<KB>(A, Ur, cscale(col[q + 8 * KB], rm));
+        if (WCE_MASK_DEAD == 2) {   // columns <= kq of block KB are final: masked instead of scaled by 0
+            const uint64_t byte = (0xffull << (kq + 1)) & 0xffull;
+            upd_col_live<KB>(A, Ur, cscale(col[q + 8 * KB], rk), byte * 0x0101010101010101ull);
+        } else {   // (a runtime mask costs more SALU than it saves here: A/B in profiles/r02_ab_mask.txt)
+            upd_col<KB>(A, Ur, cscale(col[q + 8 * KB], rm));
+        }
         r = rcp_nr(readlane_f64(A[KB][KB].x, 9 * (kq + 1)));
         publish_col<KB>(A, next, p, q, kq + 1);
         upd_cols_from<KB + 1>(A, Ur, col, q, rk);
     } else if constexpr (KB + 1 < RB) {
-        upd_col<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
+        upd_col_live<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
         r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
         publish_col<KB + 1>(A, next, p, q, 0);
         upd_cols_from<KB + 2>(A, Ur, col, q, rk);
@@ -774,11 +842,18 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 // panel.  The price is 1/sqrt instead of 1/d (3 more VALU per step).
 // ---------------------------------------------------------------------
 template <int BB>
-__device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col, int q)
+__device__ __forceinline__ void upd_col_chol(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v, int p, int q)
+{
+    upd_col_live<BB>(A, Ur, v);
+}
+
+template <int BB>
+__device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col, int p,
+                                              int q)
 {
     if constexpr (BB < RB) {
-        upd_col<BB>(A, Ur, col[q + 8 * BB]);
-        upd_cols_chol<BB + 1>(A, Ur, col, q);
+        upd_col_chol<BB>(A, Ur, col[q + 8 * BB], p, q);
+        upd_cols_chol<BB + 1>(A, Ur, col, p, q);
     }
 }
 
@@ -797,15 +872,17 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
 #pragma unroll
         for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
         if (kq < 7) {
-            cmsub_conj(P[kq + 1], P[kq], col[8 * KB + kq + 1]);   // lookahead: column k+1
+            // row lane of column 8KB+c is live for 8KB+c <= lane <= 54
+            cmsub_live(lanes_from(k + 1, NSC + 1), P[kq + 1], P[kq], col[8 * KB + kq + 1]);   // lookahead
             const double rs = rsq_nr(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
 #pragma unroll
-            for (int c = kq + 2; c < 8; ++c) cmsub_conj(P[c], P[kq], col[8 * KB + c]);
-            upd_cols_chol<KB + 1>(A, Ur, col, q);
+            for (int c = kq + 2; c < 8; ++c)
+                cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], col[8 * KB + c]);
+            upd_cols_chol<KB + 1>(A, Ur, col, p, q);
         } else {
-            upd_col<KB + 1>(A, Ur, col[q + 8 * (KB + 1)]);
+            upd_col_chol<KB + 1>(A, Ur, col[q + 8 * (KB + 1)], p, q);
             if constexpr (KB + 2 < RB) {
                 to_rows<KB + 1>(A, P, s, p, q, lane);
                 const double rs = rsq_nr(readlane_f64(P[0].x, k + 1));
@@ -816,7 +893,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
                 if (q == 0) next[p + 8 * (KB + 1)] = cs;
             }
-            upd_cols_chol<KB + 2>(A, Ur, col, q);
+            upd_cols_chol<KB + 2>(A, Ur, col, p, q);
         }
         wave_lds_sync();
     }
@@ -833,7 +910,7 @@ __device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, 
         const int k = B6 + kq;
         const double2 *col = s.u[k & 1];
         double2 *next = s.u[(k + 1) & 1];
-        cmsub_conj(A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
+        cmsub_live(lanes_lower(kq), A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
         const double rs = rsq_nr(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;

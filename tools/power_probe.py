@@ -1,0 +1,98 @@
+"""Board power and shader clock while a kernel runs back to back.
+
+Runs one leg (headline TEXTBOOK solve by default, 65,536 frames) in a loop on
+one thread for --seconds, and samples `amd-smi metric` (power, clocks) from
+the main thread.  Read-only SMI queries; nothing is set.
+usage: python tools/power_probe.py [--leg headline|ls|idle] [--seconds 8]"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+N, NBLK = 53, 15
+
+
+def smi():
+    for cmd in (["amd-smi", "metric", "-g", "0", "-p", "-c", "--json"],
+                ["rocm-smi", "-d", "0", "--showpower", "--showclocks", "--json"]):
+        try:
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=10)
+            if out.returncode == 0 and out.stdout.strip():
+                return cmd[0], out.stdout.strip()
+        except Exception as e:   # noqa: BLE001 -- report and try the other tool
+            last = repr(e)
+    return "none", last if "last" in dir() else "no output"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "idle"])
+    ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--frames", type=int, default=65536)
+    ap.add_argument("--lib", default=None, help="libwce.so to load (default: the in-tree build)")
+    args = ap.parse_args()
+    import importlib
+    wce = importlib.import_module("80211parallelestimation_amd")
+    if args.lib:
+        sys.modules["80211parallelestimation_amd.wce"]._lib = None
+        wce.load(os.path.abspath(args.lib))
+    import bench
+    inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
+    n = args.frames
+    stream = wce.Stream()
+    s = stream.handle
+    run = None
+    if args.leg == "headline":
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211)
+        fr = ctx.frames(tx, rx, n)
+        H = wce.DeviceArray((n, N), zero=True)
+        o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+        run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
+    elif args.leg == "ls":
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        bufs, fr = bench.ls_frames(wce, ctx, n)
+        hlt, hlin = wce.DeviceArray((n, N)), wce.DeviceArray((n, N))
+        o = wce.Outputs(hlt.addr, hlin.addr, None, None, None, None, N, 0, 0, 0, 0)
+        run = lambda: ctx.estimate(fr, o, wce.LT_LS | wce.PS_LINEAR, s)
+    stop = threading.Event()
+    stats = {"launches": 0, "secs": 0.0}
+
+    def loop():
+        if run is None:
+            return
+        t0 = time.perf_counter()
+        while not stop.is_set():
+            for _ in range(50):
+                run()
+            stream.synchronize()
+            stats["launches"] += 50
+        stats["secs"] = time.perf_counter() - t0
+
+    th = threading.Thread(target=loop)
+    th.start()
+    samples = []
+    t_end = time.time() + args.seconds
+    while time.time() < t_end:
+        samples.append((round(time.time(), 2),) + smi())
+        time.sleep(0.3)
+    stop.set()
+    th.join()
+    per = stats["secs"] / stats["launches"] * 1e3 if stats["launches"] else None
+    print(json.dumps({"leg": args.leg, "frames": n, "launches": stats["launches"],
+                      "ms_per_launch_wall": per}))
+    for t, tool, out in samples:
+        print(f"--- t={t} {tool}")
+        print(out)
+
+
+if __name__ == "__main__":
+    main()
