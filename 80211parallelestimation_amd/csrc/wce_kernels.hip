@@ -847,22 +847,101 @@ __device__ __forceinline__ void upd_col_chol(double2 (&A)[RB][RB], const double2
     upd_col_live<BB>(A, Ur, v);
 }
 
+#ifndef WCE_ABLATE_LDS   // timing-only builds (wrong results): 1 = no in-panel operand reads, 2 = no trailing column reads
+#define WCE_ABLATE_LDS 0
+#endif
 template <int BB>
 __device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col, int p,
                                               int q)
 {
     if constexpr (BB < RB) {
-        upd_col_chol<BB>(A, Ur, col[q + 8 * BB], p, q);
+        upd_col_chol<BB>(A, Ur, WCE_ABLATE_LDS == 2 ? Ur[BB] : col[q + 8 * BB], p, q);
         upd_cols_chol<BB + 1>(A, Ur, col, p, q);
+    }
+}
+
+#ifndef WCE_DPP_PANEL   // in-panel operands by DPP row_newbcast from one LDS read per step
+#define WCE_DPP_PANEL 3
+#endif
+// acc -= l conj(c_k[8KB + N]) for the row-per-lane panel, where R holds
+// c_k[8KB + (lane & 7)]: DPP row_newbcast:N hands lane N of each 16-lane row
+// (= c_k[8KB + N]) to the whole row as the FMA's first operand (gfx950's
+// DPP64 on v_fmac_f64), so the 7 - kq wave-uniform operands of a step cost
+// one LDS read instead of one each.  row_mask RM switches off the 16-lane
+// rows that hold no live row (all lanes < 8KB + N).  R comes straight from a
+// ds_read, so the "VALU writes VGPR -> DPP reads it: 2 wait states" hazard
+// cannot arise unless the compiler copies R with a VALU move just before;
+// tests/test_isa.py checks the compiled code for exactly that.
+template <int N, int RM>
+__device__ __forceinline__ void cmsub_bc(double2 &acc, double2 l, double2 R)
+{
+    asm("v_fmac_f64_dpp %[ax], -%[cx], %[lx] row_newbcast:%c[n] row_mask:%c[rm] bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ax], -%[cy], %[ly] row_newbcast:%c[n] row_mask:%c[rm] bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], -%[cx], %[ly] row_newbcast:%c[n] row_mask:%c[rm] bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], %[cy], %[lx] row_newbcast:%c[n] row_mask:%c[rm] bank_mask:0xf"
+        : [ax] "+v"(acc.x), [ay] "+v"(acc.y)
+        : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(R.x), [cy] "v"(R.y), [n] "i"(N), [rm] "i"(RM));
+}
+// variant 2: exact lane mask in EXEC (as cmsub_live) around the DPP FMAs
+template <int N>
+__device__ __forceinline__ void cmsub_bc_exec(uint64_t m, double2 &acc, double2 l, double2 R)
+{
+    const uint64_t em = m & __builtin_amdgcn_read_exec();
+    uint64_t sv;
+    asm("s_mov_b64 %[sv], exec\n\t"
+        "s_mov_b64 exec, %[m]\n\t"
+        "v_fmac_f64_dpp %[ax], -%[cx], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ax], -%[cy], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], -%[cx], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], %[cy], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [ax] "+v"(acc.x), [ay] "+v"(acc.y), [sv] "=&s"(sv)
+        : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(R.x), [cy] "v"(R.y), [n] "i"(N), [m] "s"(em));
+}
+constexpr int live_rows(int first) { return 0xf & ~((1 << (first / 16)) - 1); }   // 16-lane rows holding lanes >= first
+template <int KB>
+__device__ __forceinline__ void cmsub_panel(int c, double2 &acc, double2 l, double2 R)
+{
+    if (WCE_DPP_PANEL == 2) {
+        // DPP reads nothing from a lane that is off in EXEC (the destination
+        // lane is then not written), so the broadcast source must be live in
+        // every row that has live lanes: lane 16r + 8(KB & 1) + c is the first
+        // live lane of the partly live row, and lanes 55..63 stay on.
+        const uint64_t m = lanes_from(8 * KB + c, 63);
+        constexpr int H = 8 * (KB & 1);
+        switch (c) {
+        case 1: cmsub_bc_exec<H + 1>(m, acc, l, R); break;
+        case 2: cmsub_bc_exec<H + 2>(m, acc, l, R); break;
+        case 3: cmsub_bc_exec<H + 3>(m, acc, l, R); break;
+        case 4: cmsub_bc_exec<H + 4>(m, acc, l, R); break;
+        case 5: cmsub_bc_exec<H + 5>(m, acc, l, R); break;
+        case 6: cmsub_bc_exec<H + 6>(m, acc, l, R); break;
+        default: cmsub_bc_exec<H + 7>(m, acc, l, R); break;
+        }
+        return;
+    }
+    switch (c) {   // c is a constant after unrolling: one case survives
+    case 1: cmsub_bc<1, live_rows(8 * KB + 1)>(acc, l, R); break;
+    case 2: cmsub_bc<2, live_rows(8 * KB + 2)>(acc, l, R); break;
+    case 3: cmsub_bc<3, live_rows(8 * KB + 3)>(acc, l, R); break;
+    case 4: cmsub_bc<4, live_rows(8 * KB + 4)>(acc, l, R); break;
+    case 5: cmsub_bc<5, live_rows(8 * KB + 5)>(acc, l, R); break;
+    case 6: cmsub_bc<6, live_rows(8 * KB + 6)>(acc, l, R); break;
+    default: cmsub_bc<7, live_rows(8 * KB + 7)>(acc, l, R); break;
     }
 }
 
 // Panel KB in row form.  Entering: P = block column KB with P[0] = c_{8KB}
 // (scaled), c_{8KB} published.
 // K0 = 1: pivot 8KB is already eliminated (exact_first_step), c_{8KB+1} published.
+// R (WCE_DPP_PANEL): c_k[8KB + (lane & 7)] for the step about to run.  With
+// WCE_DPP_PANEL == 3 it is read for step k+1 right after c_{k+1} is
+// published, so the next lookahead does not wait for an LDS round trip.
 template <int KB, int K0 = 0>
-__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q, int lane)
+__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s, int p,
+                                           int q, int lane)
 {
+    constexpr bool PRE = WCE_DPP_PANEL == 3;
 #pragma unroll
     for (int kq = K0; kq < 8; ++kq) {
         const int k = 8 * KB + kq;
@@ -873,14 +952,24 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
         for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
         if (kq < 7) {
             // row lane of column 8KB+c is live for 8KB+c <= lane <= 54
-            cmsub_live(lanes_from(k + 1, NSC + 1), P[kq + 1], P[kq], col[8 * KB + kq + 1]);   // lookahead
+            if (WCE_DPP_PANEL && !PRE) R = col[8 * KB + (lane & 7)];
+            if (WCE_DPP_PANEL) cmsub_panel<KB>(kq + 1, P[kq + 1], P[kq], R);   // lookahead
+            else cmsub_live(lanes_from(k + 1, NSC + 1), P[kq + 1], P[kq], col[8 * KB + kq + 1]);
             const double rs = rsq_nr(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
+            double2 Rn = R;
+            if (PRE) {
+                wave_lds_sync();
+                Rn = next[8 * KB + (lane & 7)];
+            }
 #pragma unroll
-            for (int c = kq + 2; c < 8; ++c)
-                cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], col[8 * KB + c]);
+            for (int c = kq + 2; c < 8; ++c) {
+                if (WCE_DPP_PANEL) cmsub_panel<KB>(c, P[c], P[kq], R);
+                else cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], WCE_ABLATE_LDS == 1 ? P[kq + 1] : col[8 * KB + c]);
+            }
             upd_cols_chol<KB + 1>(A, Ur, col, p, q);
+            R = Rn;
         } else {
             upd_col_chol<KB + 1>(A, Ur, col[q + 8 * (KB + 1)], p, q);
             if constexpr (KB + 2 < RB) {
@@ -888,6 +977,10 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double rs = rsq_nr(readlane_f64(P[0].x, k + 1));
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
+                if (PRE) {
+                    wave_lds_sync();
+                    R = next[8 * (KB + 1) + (lane & 7)];
+                }
             } else {   // block column 6 stays block-cyclic: the 8 owners of column 48 publish
                 const double rs = rsq_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
@@ -1045,12 +1138,13 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     P[1] = cscale(P[1], rsq_nr(readlane_f64(P[1].x, 1)));
     s.u[1][lane] = P[1];
     wave_lds_sync();
-    chol_panel<0, 1>(A, P, s, p, q, lane);
-    chol_panel<1>(A, P, s, p, q, lane);
-    chol_panel<2>(A, P, s, p, q, lane);
-    chol_panel<3>(A, P, s, p, q, lane);
-    chol_panel<4>(A, P, s, p, q, lane);
-    chol_panel<5>(A, P, s, p, q, lane);
+    double2 R = WCE_DPP_PANEL == 3 ? s.u[1][lane & 7] : make_double2(0.0, 0.0);
+    chol_panel<0, 1>(A, P, R, s, p, q, lane);
+    chol_panel<1>(A, P, R, s, p, q, lane);
+    chol_panel<2>(A, P, R, s, p, q, lane);
+    chol_panel<3>(A, P, R, s, p, q, lane);
+    chol_panel<4>(A, P, R, s, p, q, lane);
+    chol_panel<5>(A, P, R, s, p, q, lane);
     return chol_last(A, s, p, q);
 }
 

@@ -1,0 +1,31 @@
+"""Static checks on the compiled gfx950 code (CPU: hipcc cross-compiles).
+
+The rank-1 solve issues DPP64 FMAs from inline asm (wce_kernels.hip
+cmsub_bc); the compiler's hazard recognizer does not look inside them, so
+the emitted code is checked for a VALU write of a DPP source VGPR within the
+2 wait states the hardware needs (tools/isa_check.py)."""
+import os
+import shutil
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+@pytest.mark.skipif(not shutil.which("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
+def test_no_dpp_source_hazards():
+    import isa_check
+    text = isa_check.compile_asm()
+    n = sum(1 for i in isa_check.instructions(text) if "_dpp" in i.split()[0])
+    assert n > 600, "the headline's DPP in-panel FMAs are missing"
+    assert isa_check.dpp_hazards(text) == []
+
+
+def test_checker_flags_a_hazard():
+    import isa_check
+    bad = "v_mov_b32 v122, v1\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
+    assert len(isa_check.dpp_hazards(bad)) == 1
+    ok = "v_mov_b32 v122, v1\ns_nop 1\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
+    assert isa_check.dpp_hazards(ok) == []

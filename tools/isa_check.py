@@ -1,0 +1,86 @@
+"""Static checks on the compiled gfx950 assembly of the kernels.
+
+The solve kernels issue DPP64 FMAs from inline asm (row_newbcast operands,
+wce_kernels.hip cmsub_bc).  The hardware needs 2 wait states between a VALU
+write of a VGPR and a DPP instruction reading it through the DPP crossbar;
+the compiler cannot see into inline asm, so this checks the emitted code:
+no VALU instruction in the 2 wait states before a DPP instruction writes
+that instruction's DPP source (src0).
+usage: python tools/isa_check.py [file.s]   (default: compile wce_kernels.hip)"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "80211parallelestimation_amd", "csrc", "wce_kernels.hip")
+REG = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)\b")
+
+
+def regs(tok: str):
+    m = REG.search(tok)
+    if not m:
+        return set()
+    if m.group(3) is not None:
+        return {int(m.group(3))}
+    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+
+
+def instructions(text: str):
+    for line in text.splitlines():
+        t = line.split(";")[0].strip()
+        if not t or t.startswith(".") or t.endswith(":"):
+            continue
+        yield t
+
+
+def dpp_hazards(text: str):
+    """List of (dpp instruction, offending earlier instruction)."""
+    out, prev = [], []   # prev: (wait states the instruction provides, text)
+    for ins in instructions(text):
+        op = ins.split()[0]
+        if "_dpp" in op:
+            ops = [o.strip() for o in ins[len(op):].split(",")]
+            src0 = regs(ops[1].lstrip("-|")) if len(ops) > 1 else set()
+            ws = 0
+            for w, p in reversed(prev):
+                if ws >= 2:
+                    break
+                pop = p.split()[0]
+                if pop.startswith("v_") and not pop.startswith(("v_readlane", "v_readfirstlane", "v_cmp")):
+                    dst = regs(p[len(pop):].split(",")[0])
+                    if dst & src0:
+                        out.append((ins, p))
+                ws += w
+        ws_self = 1
+        if op == "s_nop":
+            ws_self = int(ins.split()[1], 0) + 1
+        prev.append((ws_self, ins))
+        prev = prev[-8:]
+    return out
+
+
+def compile_asm(flags=()):
+    fd, path = tempfile.mkstemp(suffix=".s")
+    os.close(fd)
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(REPO, "include"),
+           "--cuda-device-only", "-S", SRC, "-o", path, *flags]
+    subprocess.run(cmd, check=True, capture_output=True)
+    text = open(path).read()
+    os.unlink(path)
+    return text
+
+
+def main():
+    text = open(sys.argv[1]).read() if len(sys.argv) > 1 else compile_asm()
+    n_dpp = sum(1 for i in instructions(text) if "_dpp" in i.split()[0])
+    bad = dpp_hazards(text)
+    print(f"{n_dpp} DPP instructions, {len(bad)} hazards")
+    for d, p in bad[:20]:
+        print("  ", p, "->", d)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
