@@ -825,6 +825,12 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_SOLVE_WAVES_PER_SIMD
 #define WCE_SOLVE_WAVES_PER_SIMD 3
 #endif
+#ifndef WCE_DENSE_CHOL   // A/B: dense-C solve by row-panel Cholesky keeping L (else block-cyclic LDL^H)
+#define WCE_DENSE_CHOL 0
+#endif
+#ifndef WCE_DENSE_WAVES_PER_SIMD
+#define WCE_DENSE_WAVES_PER_SIMD WCE_SOLVE_WAVES_PER_SIMD
+#endif
 // One block's solve; returns w_lane = x_lane z_lane (0 for lanes >= 53 is
 // not guaranteed: callers store lanes < 53 only).
 // FC: per-frame rank-1 covariance C_f = cu_f cw_f^T (SolveArgs::cu/cw, frame f)
@@ -937,9 +943,34 @@ __device__ __forceinline__ void cmsub_panel(int c, double2 &acc, double2 l, doub
 // R (WCE_DPP_PANEL): c_k[8KB + (lane & 7)] for the step about to run.  With
 // WCE_DPP_PANEL == 3 it is read for step k+1 right after c_{k+1} is
 // published, so the next lookahead does not wait for an LDS round trip.
-template <int KB, int K0 = 0>
+// a = c where sel (component selects on values: a select between an A
+// element and a temporary as lvalues would defeat SROA and put A in scratch)
+__device__ __forceinline__ void keep_where(bool sel, double2 &a, double2 c)
+{
+    a.x = sel ? c.x : a.x;
+    a.y = sel ? c.y : a.y;
+}
+
+// KEEP (the dense-C path, which back-substitutes): every finished panel is
+// written back into its block column of A (to_blocks), block column 6 keeps
+// its scaled columns, and rsel collects 1/sqrt(d_k) in lane k.
+template <int KB>
+__device__ __forceinline__ void to_blocks(double2 (&A)[RB][RB], const double2 (&P)[8], SolveLds &s, int p, int q,
+                                          int lane)
+{
+    if (lane < 56) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) s.conv[conv_idx(lane, c)] = P[c];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int aa = KB; aa < RB; ++aa) A[aa][KB] = s.conv[conv_idx(p + 8 * aa, q)];
+    wave_lds_sync();   // to_rows<KB + 1> reuses conv
+}
+
+template <int KB, int K0 = 0, bool KEEP = false>
 __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s, int p,
-                                           int q, int lane)
+                                           int q, int lane, double &rsel)
 {
     constexpr bool PRE = WCE_DPP_PANEL == 3;
 #pragma unroll
@@ -958,6 +989,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             const double rs = rsq_nr(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
+            if (KEEP) rsel = lane == k + 1 ? rs : rsel;
             double2 Rn = R;
             if (PRE) {
                 wave_lds_sync();
@@ -972,11 +1004,13 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             R = Rn;
         } else {
             upd_col_chol<KB + 1>(A, Ur, col[q + 8 * (KB + 1)], p, q);
+            if (KEEP) to_blocks<KB>(A, P, s, p, q, lane);
             if constexpr (KB + 2 < RB) {
                 to_rows<KB + 1>(A, P, s, p, q, lane);
                 const double rs = rsq_nr(readlane_f64(P[0].x, k + 1));
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
+                if (KEEP) rsel = lane == k + 1 ? rs : rsel;
                 if (PRE) {
                     wave_lds_sync();
                     R = next[8 * (KB + 1) + (lane & 7)];
@@ -985,6 +1019,10 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double rs = rsq_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
                 if (q == 0) next[p + 8 * (KB + 1)] = cs;
+                if (KEEP) {
+                    rsel = lane == k + 1 ? rs : rsel;
+                    keep_where(q == 0, A[KB + 1][KB + 1], cs);
+                }
             }
             upd_cols_chol<KB + 2>(A, Ur, col, p, q);
         }
@@ -1013,6 +1051,55 @@ __device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, 
     double2 sc = readlane_c(A[RB - 1][RB - 1], 8 * (NSC + 1 - B6) + (NSC - B6));   // (54, 53)
     cmsub_conj(sc, col[NSC + 1], col[NSC]);
     return make_double2(-sc.x, -sc.y);   // s = -S(54, 53)
+}
+
+// Pivots 49..52 on register block (6, 6) keeping L (the dense-C path):
+// each finished column is scaled in place (lanes q == kq), rsel collects
+// 1/sqrt(d).  Entering: column 48 scaled in place and published.
+__device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane, double &rsel)
+{
+    constexpr int B6 = 8 * (RB - 1);
+#pragma unroll
+    for (int kq = 0; kq < NSC - 1 - B6; ++kq) {
+        const int k = B6 + kq;
+        const double2 *col = s.u[k & 1];
+        double2 *next = s.u[(k + 1) & 1];
+        cmsub_live(lanes_lower(kq), A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
+        const double rs = rsq_nr(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
+        const double2 cs = cscale(A[RB - 1][RB - 1], rs);
+        if (q == kq + 1) next[p + B6] = cs;
+        rsel = lane == k + 1 ? rs : rsel;
+        keep_where(q == kq + 1, A[RB - 1][RB - 1], cs);
+        wave_lds_sync();
+    }
+}
+
+// The dense-C factorisation (WCE_DENSE_CHOL): the headline's row-per-lane
+// Cholesky panels on Ryy bordered by conj(rx) (row 53), keeping L in the
+// block-cyclic registers for the back-substitution; s.rd = 1/sqrt(d_k).
+// Entering: A built (all 28 blocks, row 53 = conj(rx)).
+__device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane)
+{
+    double2 P[8];
+    to_rows<0>(A, P, s, p, q, lane);
+    const double r0 = rsq_nr(readlane_f64(P[0].x, 0));
+    double rsel = lane == 0 ? r0 : 0.0;
+    P[0] = cscale(P[0], r0);
+    wave_lds_sync();   // conv reads done before the publish (s.u is separate; order only)
+    s.u[0][lane] = P[0];
+    wave_lds_sync();
+    double2 R = WCE_DPP_PANEL == 3 ? s.u[0][lane & 7] : make_double2(0.0, 0.0);
+    chol_panel<0, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<1, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<2, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<3, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<4, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<5, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_last_keep(A, s, p, q, lane, rsel);
+    wave_lds_sync();
+    s.rd[lane] = lane < NSC ? rsel : 0.0;   // conv is dead: rd and z share its LDS
+    s.z[lane] = make_double2(0.0, 0.0);     // rows >= 53 must read 0 in the back-substitution
+    wave_lds_sync();
 }
 
 // ---------------------------------------------------------------------
@@ -1139,12 +1226,13 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     s.u[1][lane] = P[1];
     wave_lds_sync();
     double2 R = WCE_DPP_PANEL == 3 ? s.u[1][lane & 7] : make_double2(0.0, 0.0);
-    chol_panel<0, 1>(A, P, R, s, p, q, lane);
-    chol_panel<1>(A, P, R, s, p, q, lane);
-    chol_panel<2>(A, P, R, s, p, q, lane);
-    chol_panel<3>(A, P, R, s, p, q, lane);
-    chol_panel<4>(A, P, R, s, p, q, lane);
-    chol_panel<5>(A, P, R, s, p, q, lane);
+    double rsel = 0.0;   // unused (no back-substitution)
+    chol_panel<0, 1>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<1>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<2>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<3>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<4>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<5>(A, P, R, s, p, q, lane, rsel);
     return chol_last(A, s, p, q);
 }
 
@@ -1239,17 +1327,21 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
             for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
         }
     }
-    // pivot 0 and its column
-    double r = rcp_nr(readlane_f64(A[0][0].x, 0));
-    publish_col<0>(A, s.u[0], p, q, 0);
-    wave_lds_sync();
-    ldl_panel<0>(A, s, p, q, r);
-    ldl_panel<1>(A, s, p, q, r);
-    ldl_panel<2>(A, s, p, q, r);
-    ldl_panel<3>(A, s, p, q, r);
-    ldl_panel<4>(A, s, p, q, r);
-    ldl_panel<5>(A, s, p, q, r);
-    ldl_panel<6>(A, s, p, q, r);
+    if (WCE_DENSE_CHOL) {
+        dense_chol(A, s, p, q, lane);
+    } else {
+        // pivot 0 and its column
+        double r = rcp_nr(readlane_f64(A[0][0].x, 0));
+        publish_col<0>(A, s.u[0], p, q, 0);
+        wave_lds_sync();
+        ldl_panel<0>(A, s, p, q, r);
+        ldl_panel<1>(A, s, p, q, r);
+        ldl_panel<2>(A, s, p, q, r);
+        ldl_panel<3>(A, s, p, q, r);
+        ldl_panel<4>(A, s, p, q, r);
+        ldl_panel<5>(A, s, p, q, r);
+        ldl_panel<6>(A, s, p, q, r);
+    }
     wave_lds_sync();
     // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
     double rq[RB];
@@ -1282,7 +1374,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 // instead of the dense State::C (COV mode, or a = 0).
 // split (MATLAB averaging): one wave per (frame, block), W_b to row g of a.w.
 template <bool R1>
-__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
+__global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
     const int64_t g = blockIdx.x;

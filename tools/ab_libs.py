@@ -75,4 +75,5 @@ outs = [r[4].numpy() for r in runs]
 for (name, *_), o in zip(runs, outs):
     print(f"{args.leg} {name}: median {np.median(times[name]) * 1e3:.1f} us  "
           f"({', '.join(f'{t * 1e3:.0f}' for t in times[name])})  same output as {runs[0][0]}: "
-          f"{bool(np.array_equal(o, outs[0]))}")
+          f"{bool(np.array_equal(o, outs[0]))}  max norm-rel diff "
+          f"{float(np.max(np.abs(o - outs[0]).reshape(n, -1).max(1) / np.abs(outs[0]).reshape(n, -1).max(1))):.2e}")
