@@ -674,6 +674,38 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
         cmsub_live(cm & kRows55, A[RB - 1][BB], Ur[RB - 1], v);
     }
 }
+#ifndef WCE_CHAIN_1LANE   // A/B: the pivot's 1/sqrt on one lane (EXEC = 1), result to SGPRs
+#define WCE_CHAIN_1LANE 1
+#endif
+// 1/sqrt(d) of a wave-uniform pivot d.  The kernel is power-capped, so the
+// 6-op chain runs on lane 0 alone (EXEC = 1 inside the asm) and comes back
+// through v_readfirstlane as a scalar: the same arithmetic as rsq_nr (one
+// third-order step after v_rsq_f64), bit-identical, at 1/64 of its energy.
+__device__ __forceinline__ double rsq_uniform(double d)
+{
+    if (!WCE_CHAIN_1LANE) return rsq_nr(d);
+    double y, t, e, sv_unused;
+    (void)sv_unused;
+    uint64_t sv;
+    const double c38 = 0.375;
+    asm("s_mov_b64 %[sv], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "v_rsq_f64 %[y], %[d]\n\t"
+        "s_nop 1\n\t"
+        "v_mul_f64 %[t], %[d], %[y]\n\t"
+        "v_fma_f64 %[e], -%[t], %[y], 1.0\n\t"
+        "v_mul_f64 %[t], %[y], %[e]\n\t"
+        "v_fma_f64 %[e], %[e], %[c], 0.5\n\t"
+        "v_fma_f64 %[y], %[t], %[e], %[y]\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [y] "=&v"(y), [t] "=&v"(t), [e] "=&v"(e), [sv] "=&s"(sv)
+        : [d] "s"(d), [c] "s"(c38));
+    const long long b = __double_as_longlong(y);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
 template <int BB>
 __device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v)
@@ -986,7 +1018,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             if (WCE_DPP_PANEL && !PRE) R = col[8 * KB + (lane & 7)];
             if (WCE_DPP_PANEL) cmsub_panel<KB>(kq + 1, P[kq + 1], P[kq], R);   // lookahead
             else cmsub_live(lanes_from(k + 1, NSC + 1), P[kq + 1], P[kq], col[8 * KB + kq + 1]);
-            const double rs = rsq_nr(readlane_f64(P[kq + 1].x, k + 1));
+            const double rs = rsq_uniform(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
             if (KEEP) rsel = lane == k + 1 ? rs : rsel;
@@ -1007,7 +1039,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             if (KEEP) to_blocks<KB>(A, P, s, p, q, lane);
             if constexpr (KB + 2 < RB) {
                 to_rows<KB + 1>(A, P, s, p, q, lane);
-                const double rs = rsq_nr(readlane_f64(P[0].x, k + 1));
+                const double rs = rsq_uniform(readlane_f64(P[0].x, k + 1));
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
                 if (KEEP) rsel = lane == k + 1 ? rs : rsel;
@@ -1016,7 +1048,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                     R = next[8 * (KB + 1) + (lane & 7)];
                 }
             } else {   // block column 6 stays block-cyclic: the 8 owners of column 48 publish
-                const double rs = rsq_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
+                const double rs = rsq_uniform(readlane_f64(A[KB + 1][KB + 1].x, 0));
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
                 if (q == 0) next[p + 8 * (KB + 1)] = cs;
                 if (KEEP) {
@@ -1042,7 +1074,7 @@ __device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, 
         const double2 *col = s.u[k & 1];
         double2 *next = s.u[(k + 1) & 1];
         cmsub_live(lanes_lower(kq), A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
-        const double rs = rsq_nr(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
+        const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;
         wave_lds_sync();
@@ -1065,7 +1097,7 @@ __device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s
         const double2 *col = s.u[k & 1];
         double2 *next = s.u[(k + 1) & 1];
         cmsub_live(lanes_lower(kq), A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
-        const double rs = rsq_nr(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
+        const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;
         rsel = lane == k + 1 ? rs : rsel;
