@@ -33,7 +33,7 @@ def smi():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "idle"])
+    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "config5", "idle"])
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--frames", type=int, default=65536)
     ap.add_argument("--lib", default=None, help="libwce.so to load (default: the in-tree build)")
@@ -57,6 +57,15 @@ def main():
         H = wce.DeviceArray((n, N), zero=True)
         o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
         run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
+    elif args.leg == "config5":   # all 5 + eq fused, fp32 LS/eq outputs, per-frame preambles
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+        tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+        ctx.synth(tx, rx, pre, n, seed=0x80211)
+        outs = [wce.DeviceArray((n, N), np.complex64) for _ in range(4)] + [wce.DeviceArray((n, N))]
+        eq = wce.DeviceArray((n, NBLK, N), np.complex64)
+        o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32)
+        fr = ctx.frames(tx, rx, n, rx_pre=pre)
+        run = lambda: ctx.estimate(fr, o, wce.ALL, s)
     elif args.leg == "ls":
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
         bufs, fr = bench.ls_frames(wce, ctx, n)
