@@ -337,6 +337,29 @@ int wce_nonfinite_scan(wce_ctx *c, const void *H, int64_t stride, int64_t n, uin
     return rc ? fail(rc, "nonfinite_scan launch") : WCE_OK;
 }
 
+// x87 long double complex <-> complex double (wce_ldconv.hip)
+static int ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, void *stream)
+{
+    if (n < 0) return fail(WCE_EINVAL, "n < 0");
+    if (n == 0) return WCE_OK;
+    if (!src || !dst) return fail(WCE_EINVAL, "null src/dst");
+    const char *a = static_cast<const char *>(src), *b = static_cast<const char *>(dst);
+    const int64_t sb = n * (to_complex ? 32 : 16), db = n * (to_complex ? 16 : 32);
+    if (a < b + db && b < a + sb) return fail(WCE_EINVAL, "src and dst overlap");
+    const int rc = wce::launch_ldc_convert(src, dst, n, to_complex, stream);
+    return rc ? fail(rc, "ldc convert launch") : WCE_OK;
+}
+
+extern "C" int wce_ldc_to_complex(const void *src, wce_complex *dst, int64_t n, void *stream)
+{
+    return ldc_convert(src, dst, n, true, stream);
+}
+
+extern "C" int wce_complex_to_ldc(const wce_complex *src, void *dst, int64_t n, void *stream)
+{
+    return ldc_convert(src, dst, n, false, stream);
+}
+
 // grow `w` to n frames; the old buffer may still be read by work queued on
 // `stream`, so that stream drains first (hipFree would wait for it anyway)
 static int grow_ws(wce_ctx *c, wce::Workspace &w, int64_t n, void *stream)

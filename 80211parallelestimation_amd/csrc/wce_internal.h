@@ -136,6 +136,7 @@ constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks (
                                       // 1 = the same uncapped, 2 = one element per thread (ls_elem_kernel, default)
 constexpr int WCE_VARIANT_COUNT = 4;
 int set_variant(int which, int value);
+int launch_ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, void *stream);
 int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,
                           unsigned long long *n_bad, void *stream);
 

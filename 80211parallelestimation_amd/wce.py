@@ -133,6 +133,8 @@ ABI = {
     "wce_memcpy_htod": [c_void_p, c_void_p, c_size_t],
     "wce_memcpy_dtoh": [c_void_p, c_void_p, c_size_t],
     "wce_memcpy_dtod": [c_void_p, c_void_p, c_size_t, c_void_p],
+    "wce_ldc_to_complex": [c_void_p, c_void_p, ctypes.c_int64, c_void_p],
+    "wce_complex_to_ldc": [c_void_p, c_void_p, ctypes.c_int64, c_void_p],
     "wce_memset": [c_void_p, c_int, c_size_t],
     "wce_host_alloc": [POINTER(c_void_p), c_size_t],
     "wce_host_free": [c_void_p],
@@ -501,6 +503,18 @@ def state_blob(tx_pre, rx_pre, ow2, mode=MMSE_REF, Rhh=None) -> np.ndarray:
     _check(lib.wce_state_build(blob.ctypes.data_as(c_void_p), n, tp.ctypes.data_as(c_void_p),
                                rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_state_build")
     return blob
+
+
+def ldc_to_complex(src, dst, n, stream=None):
+    """wce_ldc_to_complex: n long double _Complex values (the reference's
+    format, raw x87 bytes in device memory, e.g. DeviceArray of clongdouble)
+    -> complex double in dst, rounded as C's (double) cast."""
+    _check(load().wce_ldc_to_complex(_addr(src), _addr(dst), int(n), stream), "wce_ldc_to_complex")
+
+
+def complex_to_ldc(src, dst, n, stream=None):
+    """wce_complex_to_ldc: n complex double -> long double _Complex (exact)."""
+    _check(load().wce_complex_to_ldc(_addr(src), _addr(dst), int(n), stream), "wce_complex_to_ldc")
 
 
 def synchronize(stream=None):

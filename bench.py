@@ -356,6 +356,7 @@ def main():
             res["frame_cov"] = bench_frame_cov(wce, local_ctx, stream, B, reps)
             res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
             res["small_batch"] = bench_small_batch(wce, ctx, stream)
+            res["ldc_convert"] = bench_ldc_convert(wce, stream, reps)
             # REF past the MALL: 1,048,576 full frames (27 GB), last of the rank-0 legs
             ctx_ref = local_ctx(wce.MMSE_REF)
             res.setdefault("ref_mode", {})["b%d" % args.ls_frames] = bench_ref_large(wce, ctx_ref, stream,
@@ -595,6 +596,27 @@ def bench_front(wce, ctx, stream, n, reps):
                       "frames_per_s": n / (t * 1e-3), "algorithmic_bytes_per_unit": per, "achieved_GBs": gbs,
                       "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS,
                       "algorithmic_bytes": per * units, "traffic": traffic}
+    return out
+
+
+def bench_ldc_convert(wce, stream, reps, frames=65536):
+    """The reference's data format on the device (wce_ldconv.hip): frames
+    held as long double complex (x87, 32 B per value) converted to complex
+    double and back, 15 x 53 values per frame.  HBM-bound: 48 B per value
+    either way."""
+    s = stream.handle
+    n = frames * NBLK * N
+    ld = wce.DeviceArray((n,), np.clongdouble, zero=True)
+    c = wce.DeviceArray((n,), zero=True)
+    out = {"workload": f"{frames} frames x 15 x 53 values, long double complex <-> complex double"}
+    for label, f in (("to_complex", lambda: wce.ldc_to_complex(ld, c, n, s)),
+                     ("to_ldc", lambda: wce.complex_to_ldc(c, ld, n, s))):
+        for _ in range(3):
+            f()
+        t = time_events(wce, stream, f, reps)
+        gbs = 48.0 * n / (t * 1e-3) / 1e9
+        out[label] = {"avg_launch_ms": t, "frames_per_s": frames / (t * 1e-3), "achieved_GBs": gbs,
+                      "peak_GBs": PEAK_HBM_GBS, "frac": gbs / PEAK_HBM_GBS}
     return out
 
 

@@ -255,6 +255,22 @@ int wce_front_end_preamble(wce_ctx *ctx, const wce_complex *lptot, int64_t lptot
 int wce_nonfinite_scan(wce_ctx *ctx, const void *H, int64_t stride, int64_t n_frames, uint32_t flags,
                        uint32_t *bitmap, unsigned long long *n_bad, void *stream);
 
+/* The reference's data format on the device.  Its arrays are `long double
+ * complex` (main.c:4-8): on x86-64, two x87 80-bit extended values in 16-byte
+ * slots (32 B per complex; bytes 10-15 of a slot are padding).  A host that
+ * keeps frames in that format copies the raw bytes to the device and converts
+ * there:
+ *   wce_ldc_to_complex: n complex values, x87 -> fp64, rounded exactly as the
+ *     C cast (double)x on x86 (nearest-even, overflow to Inf, gradual
+ *     underflow; NaNs quieted and truncated; invalid encodings -> the x87
+ *     default NaN);
+ *   wce_complex_to_ldc: fp64 -> x87, exact (the C cast (long double)x),
+ *     padding written as zero.
+ * Device pointers, src and dst must not overlap; asynchronous on `stream`
+ * (current device). */
+int wce_ldc_to_complex(const void *src, wce_complex *dst, int64_t n, void *stream);
+int wce_complex_to_ldc(const wce_complex *src, void *dst, int64_t n, void *stream);
+
 /* ---- multi-GPU: frames are independent, so a batch is sharded
  * over GPUs with no data-path collective; the only exchange is ONE RCCL
  * broadcast of the packed shared state (wce_ctx_state) over xGMI, the
