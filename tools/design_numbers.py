@@ -69,6 +69,11 @@ ns = d["ls_config2"]["nonfinite_scan"]
 row("non-finite guard (`wce_nonfinite_scan`), 1,048,576 LT_LS outputs",
     f"{ns['achieved_GBs'] / 1000:.2f} TB/s = {100 * ns['frac']:.1f}% of 8 TB/s; headline output non-finite frames: "
     f"{d['nonfinite_frames']}")
+if "ldc_convert" in d:
+    lc = d["ldc_convert"]
+    row("reference-format conversion (`wce_ldc_to_complex` / `wce_complex_to_ldc`), 65,536 frames × 795 values",
+        f"{lc['to_complex']['achieved_GBs'] / 1000:.2f} / {lc['to_ldc']['achieved_GBs'] / 1000:.2f} TB/s = "
+        f"{100 * lc['to_complex']['frac']:.0f}% / {100 * lc['to_ldc']['frac']:.0f}% of 8 TB/s (48 B per value)")
 sb = d["small_batch"]
 row("small batches (1,024 frames, all 5 + eq)",
     f"{sb['direct']['us_per_call']:.0f} µs per call direct, {sb['plan']['us_per_call']:.0f} µs as a replayed "
