@@ -171,6 +171,48 @@ def hbm_bytes(k, narrow_fetch_kib: float = 0.0):
     return (2.0 * (k["FETCH_SIZE"] - narrow_fetch_kib) + narrow_fetch_kib + k["WRITE_SIZE"]) * 1024.0
 
 
+def power_clock(stream, step, seconds=2.5):
+    """Board power and shader clock while the headline kernel runs back to
+    back (untimed, after the timed region): `amd-smi metric` sampled from a
+    second thread, read only.  The FP64 solve is power-capped on MI355X
+    (DESIGN.md s6), so the clock it holds is part of its roofline story.
+    None when amd-smi is unavailable."""
+    import shutil
+    import subprocess
+    import threading
+    if not shutil.which("amd-smi"):
+        return None
+    stop, samples = threading.Event(), []
+
+    def sample():
+        time.sleep(0.4)   # past the ramp
+        while not stop.is_set():
+            try:
+                out = subprocess.run(["amd-smi", "metric", "-g", "0", "-p", "-c", "--json"], capture_output=True,
+                                     text=True, timeout=5)
+                g = json.loads(out.stdout)["gpu_data"][0]
+                clk = [v["clk"]["value"] for k, v in g["clock"].items() if k.startswith("gfx_")]
+                samples.append((float(g["power"]["socket_power"]["value"]), sum(clk) / len(clk)))
+            except Exception:   # noqa: BLE001 -- best effort, informational
+                pass
+            time.sleep(0.2)
+
+    th = threading.Thread(target=sample)
+    th.start()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            step()
+        stream.synchronize()
+    stop.set()
+    th.join()
+    if not samples:
+        return None
+    return {"socket_power_W": sum(p for p, _ in samples) / len(samples),
+            "gfx_clock_MHz": sum(c for _, c in samples) / len(samples), "samples": len(samples),
+            "note": "amd-smi metric during back-to-back headline launches (untimed); the spec peak assumes 2,400 MHz"}
+
+
 def time_events(wce, stream, fn, reps):
     e0, e1 = wce.Event(), wce.Event()
     e0.record(stream)
@@ -280,6 +322,10 @@ def main():
                                    "solves; no back-substitution, no C W product). peak = MI355X FP64 vector "
                                    "(= FP64 matrix), spec, 2.4 GHz"}
         res["mmse_frac_of_roofline"] = value / dist.world * fl_alg / (PEAK_FP64_TFLOPS * 1e12)
+        if dist.rank == 0:
+            pc = power_clock(stream, step)
+            if pc:
+                res["roofline"]["board"] = pc
 
     if not args.no_extras and dist.rank == 0:
         # the general path: dense C (WCE_MMSE_COV, full-rank model Rhh): solve with
