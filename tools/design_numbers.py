@@ -23,6 +23,11 @@ row("MMSE frames/s, TEXTBOOK (headline)", f"**{d['value']:.3g}** (target ≥1e7)
 row("`mmse_solve_fc_kernel` (the whole step: one launch)",
     f"{r['avg_launch_ms']:.3f} ms per 65,536 frames. **{r['achieved']:.1f} TFLOP/s = {100 * r['frac']:.1f}%** of the FP64 "
     f"spec peak by SURVEY's F_alg; executed flops {r['achieved_executed']:.1f} TFLOP/s = {100 * r['frac_executed']:.1f}%")
+if r.get("board"):
+    b = r["board"]
+    row("board during the headline (`amd-smi`, untimed, back-to-back launches)",
+        f"{b['socket_power_W']:.0f} W, shader clock {b['gfx_clock_MHz']:.0f} MHz (spec peak assumes 2,400): "
+        f"{100 * r['frac'] * 2400 / b['gfx_clock_MHz']:.1f}% of the FP64 peak at that clock")
 c4, c5s = d.get("config4"), d.get("config5_sharded")
 if c4:
     row(f"BASELINE configs[3] batch (1,048,576 frames, sharded over {c4['n_gpus']} GPU(s), strong scaling)",

@@ -29,8 +29,8 @@ LEGS = {
     "apply": ("matvec_kernel<false, false, 1>", 65536),
     "cov_solve": ("mmse_solve_kernel<false>", 65536),
     "ref": ("mmse_ref_flat_kernel", 1 << 20),
-    "ls": ("ls_flat_kernel", 1 << 20),
-    "ls_pilots": ("ls_flat_kernel", 1 << 20),      # PS_Linear only: calibrates the pilot-sector reads
+    "ls": ("ls_elem_kernel", 1 << 20),
+    "ls_pilots": ("ls_elem_kernel", 1 << 20),      # PS_Linear only: calibrates the pilot-sector reads
     "front_blocks": ("front_kernel<false>", 65536),
     "front_preamble": ("front_kernel<true>", 65536),
     "config5": ("mmse_solve_ls_kernel<true, true, true>", 1 << 20),
