@@ -684,8 +684,7 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
 __device__ __forceinline__ double rsq_uniform(double d)
 {
     if (!WCE_CHAIN_1LANE) return rsq_nr(d);
-    double y, t, e, sv_unused;
-    (void)sv_unused;
+    double y, t, e;
     uint64_t sv;
     const double c38 = 0.375;
     asm("s_mov_b64 %[sv], exec\n\t"
