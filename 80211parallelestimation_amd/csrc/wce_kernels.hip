@@ -856,8 +856,11 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_SOLVE_WAVES_PER_SIMD
 #define WCE_SOLVE_WAVES_PER_SIMD 3
 #endif
+#ifndef WCE_STASH_COLS   // dense Cholesky: finished panel columns to LDS as they complete
+#define WCE_STASH_COLS 1
+#endif
 #ifndef WCE_DENSE_CHOL   // A/B: dense-C solve by row-panel Cholesky keeping L (else block-cyclic LDL^H)
-#define WCE_DENSE_CHOL 0
+#define WCE_DENSE_CHOL 1
 #endif
 #ifndef WCE_DENSE_WAVES_PER_SIMD
 #define WCE_DENSE_WAVES_PER_SIMD WCE_SOLVE_WAVES_PER_SIMD
@@ -974,6 +977,14 @@ __device__ __forceinline__ void cmsub_panel(int c, double2 &acc, double2 l, doub
 // R (WCE_DPP_PANEL): c_k[8KB + (lane & 7)] for the step about to run.  With
 // WCE_DPP_PANEL == 3 it is read for step k+1 right after c_{k+1} is
 // published, so the next lookahead does not wait for an LDS round trip.
+// rsel = sel ? rs : rsel, materialised now: left to itself the compiler
+// sinks the chain of selects to the end and keeps every pivot's rs alive
+__device__ __forceinline__ void keep_rsel(double &rsel, bool sel, double rs)
+{
+    rsel = sel ? rs : rsel;
+    asm volatile("" : "+v"(rsel));
+}
+
 // a = c where sel (component selects on values: a select between an A
 // element and a temporary as lvalues would defeat SROA and put A in scratch)
 __device__ __forceinline__ void keep_where(bool sel, double2 &a, double2 c)
@@ -985,14 +996,22 @@ __device__ __forceinline__ void keep_where(bool sel, double2 &a, double2 c)
 // KEEP (the dense-C path, which back-substitutes): every finished panel is
 // written back into its block column of A (to_blocks), block column 6 keeps
 // its scaled columns, and rsel collects 1/sqrt(d_k) in lane k.
+// Column c of a finished panel goes to conv as soon as it is final (after its
+// own step's in-panel updates, stash_col), so the panel's registers free up
+// column by column; to_blocks then only reads the block column back.
+__device__ __forceinline__ void stash_col(SolveLds &s, int lane, int c, double2 v)
+{
+    if (lane < 56) s.conv[conv_idx(lane, c)] = v;
+}
 template <int KB>
 __device__ __forceinline__ void to_blocks(double2 (&A)[RB][RB], const double2 (&P)[8], SolveLds &s, int p, int q,
                                           int lane)
 {
-    if (lane < 56) {
+    if (!WCE_STASH_COLS && lane < 56) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) s.conv[conv_idx(lane, c)] = P[c];
     }
+    if (WCE_STASH_COLS) stash_col(s, lane, 7, P[7]);
     wave_lds_sync();
 #pragma unroll
     for (int aa = KB; aa < RB; ++aa) A[aa][KB] = s.conv[conv_idx(p + 8 * aa, q)];
@@ -1020,7 +1039,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             const double rs = rsq_uniform(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
-            if (KEEP) rsel = lane == k + 1 ? rs : rsel;
+            if (KEEP) keep_rsel(rsel, lane == k + 1, rs);
             double2 Rn = R;
             if (PRE) {
                 wave_lds_sync();
@@ -1031,6 +1050,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 if (WCE_DPP_PANEL) cmsub_panel<KB>(c, P[c], P[kq], R);
                 else cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], WCE_ABLATE_LDS == 1 ? P[kq + 1] : col[8 * KB + c]);
             }
+            if (KEEP && WCE_STASH_COLS) stash_col(s, lane, kq, P[kq]);   // final: its last use was above
             upd_cols_chol<KB + 1>(A, Ur, col, p, q);
             R = Rn;
         } else {
@@ -1041,7 +1061,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double rs = rsq_uniform(readlane_f64(P[0].x, k + 1));
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
-                if (KEEP) rsel = lane == k + 1 ? rs : rsel;
+                if (KEEP) keep_rsel(rsel, lane == k + 1, rs);
                 if (PRE) {
                     wave_lds_sync();
                     R = next[8 * (KB + 1) + (lane & 7)];
@@ -1051,7 +1071,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
                 if (q == 0) next[p + 8 * (KB + 1)] = cs;
                 if (KEEP) {
-                    rsel = lane == k + 1 ? rs : rsel;
+                    keep_rsel(rsel, lane == k + 1, rs);
                     keep_where(q == 0, A[KB + 1][KB + 1], cs);
                 }
             }
@@ -1099,7 +1119,7 @@ __device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s
         const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;
-        rsel = lane == k + 1 ? rs : rsel;
+        keep_rsel(rsel, lane == k + 1, rs);
         keep_where(q == kq + 1, A[RB - 1][RB - 1], cs);
         wave_lds_sync();
     }
