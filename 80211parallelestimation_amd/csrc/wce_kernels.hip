@@ -811,6 +811,36 @@ __device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)
 
 // Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
 // registers hold u = L D; r_j = 1/d_j rescales sums once per column.
+#ifndef WCE_BS_DPP   // A/B: back-substitution's diagonal solve takes z_t by DPP broadcast
+#define WCE_BS_DPP 1
+#endif
+template <int N>
+__device__ __forceinline__ double2 bcast_lane_c(double2 w)
+{
+    double2 z;
+    asm volatile("s_nop 1\n\t"
+                 "v_mov_b64_dpp %[zx], %[wx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %[zy], %[wy] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf"
+                 : [zx] "=&v"(z.x), [zy] "=&v"(z.y)
+                 : [wx] "v"(w.x), [wy] "v"(w.y), [n] "i"(N));
+    return z;
+}
+// lane t (< NMAX) of every 16-lane row, to all lanes (t a constant after unrolling)
+template <int NMAX>
+__device__ __forceinline__ double2 bcast_row_lane(double2 w, int t)
+{
+    switch (t) {
+    case 0: return bcast_lane_c<0>(w);
+    case 1: return bcast_lane_c<1>(w);
+    case 2: return bcast_lane_c<2>(w);
+    case 3: return bcast_lane_c<3>(w);
+    case 4: return bcast_lane_c<4>(w);
+    case 5: return bcast_lane_c<5>(w);
+    case 6: return bcast_lane_c<6>(w);
+    default: return bcast_lane_c<7>(w);
+    }
+}
+
 template <int BLK>
 __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
                                            SolveLds &s, int p, int q, int lane)
@@ -837,7 +867,10 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     for (int t = 0; t < NROW; ++t) lb[t] = s.blk[8 * t + q];
 #pragma unroll
     for (int t = NROW - 1; t >= 0; --t) {
-        const double2 z = readlane_c(w, t);                   // lane t = (0, t) holds w_t = z_t
+        // every lane with q = t holds w_t = z_t; DPP row_newbcast:t hands lane t
+        // of each 16-lane row to the whole row (two VALU movs instead of four
+        // readlanes through SGPRs; s_nop 1: w was written by the previous row)
+        const double2 z = WCE_BS_DPP ? bcast_row_lane<8>(w, t) : readlane_c(w, t);
         cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i, q < t
     }
     if (p == 0 && q < NROW) s.z[8 * BLK + q] = w;              // one store per block

@@ -16,6 +16,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
 N, NBLK = 53, 15
 
 
@@ -33,7 +34,7 @@ def smi():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "config5", "idle"])
+    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "config5", "cov", "idle"])
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--frames", type=int, default=65536)
     ap.add_argument("--lib", default=None, help="libwce.so to load (default: the in-tree build)")
@@ -66,6 +67,14 @@ def main():
         o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32)
         fr = ctx.frames(tx, rx, n, rx_pre=pre)
         run = lambda: ctx.estimate(fr, o, wce.ALL, s)
+    elif args.leg == "cov":   # dense-C solve alone (WCE_MMSE_COV, full-rank PDP covariance)
+        import prof_leg
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rhh())
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211)
+        fr = ctx.frames(tx, rx, n)
+        W = wce.DeviceArray((n, N), zero=True)
+        run = lambda: ctx.mmse_solve(fr, W, N, s)
     elif args.leg == "ls":
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
         bufs, fr = bench.ls_frames(wce, ctx, n)
