@@ -45,7 +45,7 @@ if rb:
         f"{100 * rr['frac']:.0f}% of 8 TB/s; {rr['achieved_sector_GBs'] / 1000:.2f} TB/s on the 1,360-B sector floor = "
         f"{100 * rr['frac_sector']:.0f}%; PMC traffic {rr['traffic'] / rb['frames']:.0f} B/frame")
 cv = d["cov_mode"]
-row("MMSE with a dense model covariance (COV: LDLᴴ + back-substitution, then MFMA `C·W`)",
+row("MMSE with a dense model covariance (COV: Cholesky keeping L + back-substitution, then MFMA `C·W`)",
     f"{cv['frames_per_s_per_gpu']:.3g} frames/s; solve {cv['solve_tflops']:.1f} TFLOP/s = "
     f"{100 * cv['solve_frac_fp64_peak']:.0f}% of FP64 peak")
 ap = d["apply_kernel"]
