@@ -920,21 +920,18 @@ __device__ __forceinline__ void upd_col_chol(double2 (&A)[RB][RB], const double2
     upd_col_live<BB>(A, Ur, v);
 }
 
-#ifndef WCE_ABLATE_LDS   // timing-only builds (wrong results): 1 = no in-panel operand reads, 2 = no trailing column reads
-#define WCE_ABLATE_LDS 0
-#endif
 template <int BB>
 __device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col, int p,
                                               int q)
 {
     if constexpr (BB < RB) {
-        upd_col_chol<BB>(A, Ur, WCE_ABLATE_LDS == 2 ? Ur[BB] : col[q + 8 * BB], p, q);
+        upd_col_chol<BB>(A, Ur, col[q + 8 * BB], p, q);
         upd_cols_chol<BB + 1>(A, Ur, col, p, q);
     }
 }
 
-#ifndef WCE_DPP_PANEL   // in-panel operands by DPP row_newbcast from one LDS read per step
-#define WCE_DPP_PANEL 3
+#ifndef WCE_DPP_PANEL   // in-panel operands by DPP row_newbcast from one prefetched LDS read per step
+#define WCE_DPP_PANEL 1
 #endif
 // acc -= l conj(c_k[8KB + N]) for the row-per-lane panel, where R holds
 // c_k[8KB + (lane & 7)]: DPP row_newbcast:N hands lane N of each 16-lane row
@@ -955,44 +952,10 @@ __device__ __forceinline__ void cmsub_bc(double2 &acc, double2 l, double2 R)
         : [ax] "+v"(acc.x), [ay] "+v"(acc.y)
         : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(R.x), [cy] "v"(R.y), [n] "i"(N), [rm] "i"(RM));
 }
-// variant 2: exact lane mask in EXEC (as cmsub_live) around the DPP FMAs
-template <int N>
-__device__ __forceinline__ void cmsub_bc_exec(uint64_t m, double2 &acc, double2 l, double2 R)
-{
-    const uint64_t em = m & __builtin_amdgcn_read_exec();
-    uint64_t sv;
-    asm("s_mov_b64 %[sv], exec\n\t"
-        "s_mov_b64 exec, %[m]\n\t"
-        "v_fmac_f64_dpp %[ax], -%[cx], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ax], -%[cy], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ay], -%[cx], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ay], %[cy], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "s_mov_b64 exec, %[sv]"
-        : [ax] "+v"(acc.x), [ay] "+v"(acc.y), [sv] "=&s"(sv)
-        : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(R.x), [cy] "v"(R.y), [n] "i"(N), [m] "s"(em));
-}
 constexpr int live_rows(int first) { return 0xf & ~((1 << (first / 16)) - 1); }   // 16-lane rows holding lanes >= first
 template <int KB>
 __device__ __forceinline__ void cmsub_panel(int c, double2 &acc, double2 l, double2 R)
 {
-    if (WCE_DPP_PANEL == 2) {
-        // DPP reads nothing from a lane that is off in EXEC (the destination
-        // lane is then not written), so the broadcast source must be live in
-        // every row that has live lanes: lane 16r + 8(KB & 1) + c is the first
-        // live lane of the partly live row, and lanes 55..63 stay on.
-        const uint64_t m = lanes_from(8 * KB + c, 63);
-        constexpr int H = 8 * (KB & 1);
-        switch (c) {
-        case 1: cmsub_bc_exec<H + 1>(m, acc, l, R); break;
-        case 2: cmsub_bc_exec<H + 2>(m, acc, l, R); break;
-        case 3: cmsub_bc_exec<H + 3>(m, acc, l, R); break;
-        case 4: cmsub_bc_exec<H + 4>(m, acc, l, R); break;
-        case 5: cmsub_bc_exec<H + 5>(m, acc, l, R); break;
-        case 6: cmsub_bc_exec<H + 6>(m, acc, l, R); break;
-        default: cmsub_bc_exec<H + 7>(m, acc, l, R); break;
-        }
-        return;
-    }
     switch (c) {   // c is a constant after unrolling: one case survives
     case 1: cmsub_bc<1, live_rows(8 * KB + 1)>(acc, l, R); break;
     case 2: cmsub_bc<2, live_rows(8 * KB + 2)>(acc, l, R); break;
@@ -1007,9 +970,9 @@ __device__ __forceinline__ void cmsub_panel(int c, double2 &acc, double2 l, doub
 // Panel KB in row form.  Entering: P = block column KB with P[0] = c_{8KB}
 // (scaled), c_{8KB} published.
 // K0 = 1: pivot 8KB is already eliminated (exact_first_step), c_{8KB+1} published.
-// R (WCE_DPP_PANEL): c_k[8KB + (lane & 7)] for the step about to run.  With
-// WCE_DPP_PANEL == 3 it is read for step k+1 right after c_{k+1} is
-// published, so the next lookahead does not wait for an LDS round trip.
+// R (WCE_DPP_PANEL): c_k[8KB + (lane & 7)] for the step about to run, read
+// for step k+1 right after c_{k+1} is published, so the next lookahead does
+// not wait for an LDS round trip.
 // rsel = sel ? rs : rsel, materialised now: left to itself the compiler
 // sinks the chain of selects to the end and keeps every pivot's rs alive
 __device__ __forceinline__ void keep_rsel(double &rsel, bool sel, double rs)
@@ -1055,7 +1018,7 @@ template <int KB, int K0 = 0, bool KEEP = false>
 __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s, int p,
                                            int q, int lane, double &rsel)
 {
-    constexpr bool PRE = WCE_DPP_PANEL == 3;
+    constexpr bool PRE = WCE_DPP_PANEL != 0;
 #pragma unroll
     for (int kq = K0; kq < 8; ++kq) {
         const int k = 8 * KB + kq;
@@ -1066,7 +1029,6 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
         for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
         if (kq < 7) {
             // row lane of column 8KB+c is live for 8KB+c <= lane <= 54
-            if (WCE_DPP_PANEL && !PRE) R = col[8 * KB + (lane & 7)];
             if (WCE_DPP_PANEL) cmsub_panel<KB>(kq + 1, P[kq + 1], P[kq], R);   // lookahead
             else cmsub_live(lanes_from(k + 1, NSC + 1), P[kq + 1], P[kq], col[8 * KB + kq + 1]);
             const double rs = rsq_uniform(readlane_f64(P[kq + 1].x, k + 1));
@@ -1081,7 +1043,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
 #pragma unroll
             for (int c = kq + 2; c < 8; ++c) {
                 if (WCE_DPP_PANEL) cmsub_panel<KB>(c, P[c], P[kq], R);
-                else cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], WCE_ABLATE_LDS == 1 ? P[kq + 1] : col[8 * KB + c]);
+                else cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], col[8 * KB + c]);
             }
             if (KEEP && WCE_STASH_COLS) stash_col(s, lane, kq, P[kq]);   // final: its last use was above
             upd_cols_chol<KB + 1>(A, Ur, col, p, q);
@@ -1172,7 +1134,7 @@ __device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], SolveLds &s, in
     wave_lds_sync();   // conv reads done before the publish (s.u is separate; order only)
     s.u[0][lane] = P[0];
     wave_lds_sync();
-    double2 R = WCE_DPP_PANEL == 3 ? s.u[0][lane & 7] : make_double2(0.0, 0.0);
+    double2 R = WCE_DPP_PANEL ? s.u[0][lane & 7] : make_double2(0.0, 0.0);
     chol_panel<0, 0, true>(A, P, R, s, p, q, lane, rsel);
     chol_panel<1, 0, true>(A, P, R, s, p, q, lane, rsel);
     chol_panel<2, 0, true>(A, P, R, s, p, q, lane, rsel);
@@ -1309,7 +1271,7 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     P[1] = cscale(P[1], rsq_nr(readlane_f64(P[1].x, 1)));
     s.u[1][lane] = P[1];
     wave_lds_sync();
-    double2 R = WCE_DPP_PANEL == 3 ? s.u[1][lane & 7] : make_double2(0.0, 0.0);
+    double2 R = WCE_DPP_PANEL ? s.u[1][lane & 7] : make_double2(0.0, 0.0);
     double rsel = 0.0;   // unused (no back-substitution)
     chol_panel<0, 1>(A, P, R, s, p, q, lane, rsel);
     chol_panel<1>(A, P, R, s, p, q, lane, rsel);
