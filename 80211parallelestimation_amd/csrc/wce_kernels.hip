@@ -681,6 +681,7 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
 // 6-op chain runs on lane 0 alone (EXEC = 1 inside the asm) and comes back
 // through v_readfirstlane as a scalar: the same arithmetic as rsq_nr (one
 // third-order step after v_rsq_f64), bit-identical, at 1/64 of its energy.
+// (through v_readlane of lane 0, not readfirstlane: correct under any EXEC)
 __device__ __forceinline__ double rsq_uniform(double d)
 {
     if (!WCE_CHAIN_1LANE) return rsq_nr(d);
@@ -699,10 +700,7 @@ __device__ __forceinline__ double rsq_uniform(double d)
         "s_mov_b64 exec, %[sv]"
         : [y] "=&v"(y), [t] "=&v"(t), [e] "=&v"(e), [sv] "=&s"(sv)
         : [d] "s"(d), [c] "s"(c38));
-    const long long b = __double_as_longlong(y);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    return readlane_f64(y, 0);   // lane 0 computed it, whatever EXEC was around the call
 }
 
 // A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
