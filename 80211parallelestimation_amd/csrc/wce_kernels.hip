@@ -679,9 +679,9 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
 #endif
 // 1/sqrt(d) of a wave-uniform pivot d.  The kernel is power-capped, so the
 // 6-op chain runs on lane 0 alone (EXEC = 1 inside the asm) and comes back
-// through v_readfirstlane as a scalar: the same arithmetic as rsq_nr (one
+// as a scalar (v_readlane of lane 0): the same arithmetic as rsq_nr (one
 // third-order step after v_rsq_f64), bit-identical, at 1/64 of its energy.
-// (through v_readlane of lane 0, not readfirstlane: correct under any EXEC)
+// Lane 0 is read explicitly (not readfirstlane), so it is right under any EXEC.
 __device__ __forceinline__ double rsq_uniform(double d)
 {
     if (!WCE_CHAIN_1LANE) return rsq_nr(d);
