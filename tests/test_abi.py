@@ -149,7 +149,7 @@ def test_c_host_cli_runs():
         subprocess.check_call(["make", "-C", os.path.join(REPO, "80211parallelestimation_amd", "csrc"), "cli"])
     r = subprocess.run([cli, "4096", "textbook", "2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    assert "frames/s" in r.stdout and "front end" in r.stdout
+    assert "frames/s" in r.stdout and "front end" in r.stdout and "bit-identical to the C casts" in r.stdout
 
 
 @pytest.mark.gpu

@@ -131,6 +131,51 @@ int main(int argc, char **argv)
         wce_free(lptot);
         wce_free(sig2);
     }
+    /* the reference's own data format (long double complex, main.c:4-8): raw
+       x87 bytes to the device, converted there; every value must equal this
+       compiler's C casts bit for bit, both ways */
+    {
+        const long nv = (B < 4096 ? B : 4096) * (long)fr;
+        long double _Complex *hld = malloc(nv * sizeof(*hld)), *back = malloc(nv * sizeof(*back));
+        wce_complex *hc = malloc(nv * sizeof(*hc));
+        if (!hld || !back || !hc) {
+            fprintf(stderr, "host alloc\n");
+            return 4;
+        }
+        for (long i = 0; i < nv; i++) {   /* bits below fp64, so (double) must round */
+            long double re = A * sinl(0.37L * i) * (1 + 0x1p-60L * (i % 7));
+            long double im = A * cosl(0.11L * i) * (1 - 0x1p-61L * (i % 5));
+            __real__ hld[i] = re;
+            __imag__ hld[i] = im;
+        }
+        void *dld;
+        wce_complex *dc;
+        CHECK(wce_malloc(&dld, nv * sizeof(*hld)));
+        CHECK(wce_malloc((void **)&dc, nv * sizeof(*hc)));
+        CHECK(wce_memcpy_htod(dld, hld, nv * sizeof(*hld)));
+        CHECK(wce_ldc_to_complex(dld, dc, nv, stream));
+        CHECK(wce_complex_to_ldc(dc, dld, nv, stream));
+        CHECK(wce_stream_synchronize(stream));
+        CHECK(wce_memcpy_dtoh(hc, dc, nv * sizeof(*hc)));
+        CHECK(wce_memcpy_dtoh(back, dld, nv * sizeof(*back)));
+        long bad = 0;
+        for (long i = 0; i < nv; i++) {
+            const double re = (double)__real__ hld[i], im = (double)__imag__ hld[i];
+            const long double bre = re, bim = im;
+            bad += memcmp(&re, &hc[i].re, 8) != 0 || memcmp(&im, &hc[i].im, 8) != 0;
+            bad += memcmp(&bre, &__real__ back[i], 10) != 0 || memcmp(&bim, &__imag__ back[i], 10) != 0;
+        }
+        if (bad) {
+            fprintf(stderr, "long double conversion: %ld mismatches\n", bad);
+            return 4;
+        }
+        printf("  %-38s %ld values, bit-identical to the C casts\n", "long double complex <-> device", nv);
+        wce_free(dld);
+        wce_free(dc);
+        free(hld);
+        free(back);
+        free(hc);
+    }
     /* spot check: LT_LS of frame 0 at DC must be 0 (main.c:74) */
     wce_complex h0[WCE_NSC];
     CHECK(wce_stream_synchronize(stream));
