@@ -343,6 +343,8 @@ static int ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, v
     if (n < 0) return fail(WCE_EINVAL, "n < 0");
     if (n == 0) return WCE_OK;
     if (!src || !dst) return fail(WCE_EINVAL, "null src/dst");
+    if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
+        return fail(WCE_EINVAL, "src/dst not 16-byte aligned");   // 16-B vector loads and stores
     const char *a = static_cast<const char *>(src), *b = static_cast<const char *>(dst);
     const int64_t sb = n * (to_complex ? 32 : 16), db = n * (to_complex ? 16 : 32);
     if (a < b + db && b < a + sb) return fail(WCE_EINVAL, "src and dst overlap");

@@ -266,8 +266,8 @@ int wce_nonfinite_scan(wce_ctx *ctx, const void *H, int64_t stride, int64_t n_fr
  *     default NaN);
  *   wce_complex_to_ldc: fp64 -> x87, exact (the C cast (long double)x),
  *     padding written as zero.
- * Device pointers, src and dst must not overlap; asynchronous on `stream`
- * (current device). */
+ * Device pointers, 16-byte aligned, not overlapping; asynchronous on
+ * `stream` (current device). */
 int wce_ldc_to_complex(const void *src, wce_complex *dst, int64_t n, void *stream);
 int wce_complex_to_ldc(const wce_complex *src, void *dst, int64_t n, void *stream);
 

@@ -84,3 +84,5 @@ def test_argument_errors(gpu_wce):
     assert lib.wce_ldc_to_complex(a.ptr, None, 4, None) != 0
     assert lib.wce_complex_to_ldc(a.ptr, a.ptr, -1, None) != 0
     assert lib.wce_ldc_to_complex(a.ptr, None, 0, None) == 0                          # empty: no-op
+    b = wce.DeviceArray((64,), zero=True)
+    assert lib.wce_ldc_to_complex(ctypes.c_void_p(a.addr + 8), b.ptr, 4, None) != 0   # misaligned
