@@ -77,6 +77,12 @@ __device__ __forceinline__ void st2(double *p, int64_t idx, double2 v)
     reinterpret_cast<double2 *>(p)[idx] = v;
 }
 typedef double v2d __attribute__((ext_vector_type(2)));
+// streaming (non-temporal) 16-B load of inputs read once
+__device__ __forceinline__ double2 ld2_nt(const double *p, int64_t idx)
+{
+    const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p) + idx);
+    return make_double2(t[0], t[1]);
+}
 // streaming (non-temporal) 16-B store of outputs nobody re-reads in this kernel
 __device__ __forceinline__ void st2_nt(double *p, int64_t idx, double2 v)
 {

@@ -356,6 +356,12 @@ __global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ 
 // two pilot pairs its linear segment needs (the lanes of a wave cover ~1.2
 // frames, so one pilot load instruction touches ~2 sectors) and divides them
 // itself; the arithmetic is ls_kernel's, so outputs are bit-identical.
+#ifndef WCE_LS_NT_LOAD   // A/B: nontemporal loads of rx_pre in ls_elem_kernel
+#define WCE_LS_NT_LOAD 1
+#endif
+#ifndef WCE_LS_NT_PILOT  // A/B: nontemporal pilot loads too
+#define WCE_LS_NT_PILOT 0
+#endif
 __global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ st, LsArgs a, int64_t f_begin,
                                                       uint32_t nfr)
 {
@@ -377,12 +383,25 @@ __global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ 
         const int64_t o = fg * a.fs + (int64_t)a.blk * a.bs;
         const int plo = seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2);
         const int phi = seg == 0 ? WCE_P1 : (seg == 1 ? WCE_P2 : WCE_P3);
-        plo_t = ld2(a.tx, o + plo);
-        plo_r = ld2(a.rx, o + plo);
-        phi_t = ld2(a.tx, o + phi);
-        phi_r = ld2(a.rx, o + phi);
+        if (WCE_LS_NT_PILOT) {
+            plo_t = ld2_nt(a.tx, o + plo);
+            plo_r = ld2_nt(a.rx, o + plo);
+            phi_t = ld2_nt(a.tx, o + phi);
+            phi_r = ld2_nt(a.rx, o + phi);
+        } else {
+            plo_t = ld2(a.tx, o + plo);
+            plo_r = ld2(a.rx, o + plo);
+            phi_t = ld2(a.tx, o + phi);
+            phi_r = ld2(a.rx, o + phi);
+        }
     }
-    if (do_lt && a.rx_pre) rp = ld2(a.rx_pre, fg * a.ps + k);
+    if (do_lt && a.rx_pre) {
+        if (WCE_LS_NT_LOAD) {   // streamed once: nontemporal
+            rp = ld2_nt(a.rx_pre, fg * a.ps + k);
+        } else {
+            rp = ld2(a.rx_pre, fg * a.ps + k);
+        }
+    }
     const int64_t out = fg * a.os + k;
     if (do_lt) {                                    // main.c:66-75
         double2 h = s_hlt[k];
