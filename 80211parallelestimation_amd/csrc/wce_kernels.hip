@@ -915,6 +915,20 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_DENSE_WAVES_PER_SIMD
 #define WCE_DENSE_WAVES_PER_SIMD WCE_SOLVE_WAVES_PER_SIMD
 #endif
+#ifndef WCE_DENSE_SCALED   // A/B: dense C solved as M = C + diag(b / (a |x|^2)) (no per-element X scaling)
+#define WCE_DENSE_SCALED 1
+#endif
+// Dense C, scaled form.  Ryy = a X C X^H + b I = a X M X^H with
+// M = C + diag(b / (a |x_i|^2)), so Ryy^-1 rx = X^-H M^-1 y / a, y = X^-1 rx,
+// and W = X z = (x / (a conj x)) o (M^-1 y).  M is C itself off the diagonal:
+// the build is the 28 block loads and a diagonal add, instead of two complex
+// products per element.  Cholesky's accuracy is invariant under the diagonal
+// scaling X (van der Sluis), so this is the same solve.  A subcarrier with
+// x_i = 0 (or a |x_i|^2 < 1e-200 b) leaves Ryy's row i as b e_i and W_i = 0:
+// it gets y_i = 0 and M_ii = 1e200, whose coupling |C_ij|^2 / M_ii is below
+// half an ulp of every other entry, and phase 0.
+constexpr double kDenseMaskedDiag = 1e200;
+__device__ __forceinline__ bool dense_keep(double tt, double bc) { return tt > 0.0 && tt * 1e200 > bc; }
 // One block's solve; returns w_lane = x_lane z_lane (0 for lanes >= 53 is
 // not guaranteed: callers store lanes < 53 only).
 // FC: per-frame rank-1 covariance C_f = cu_f cw_f^T (SolveArgs::cu/cw, frame f)
@@ -1328,6 +1342,14 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
         s.rx[lane] = r;
         s.z[lane] = make_double2(0, 0);
         s.rd[lane] = 0.0;
+        if (WCE_DENSE_SCALED && !DOT && cbuild) {   // y = rx / x to u[0], M's diagonal to u[1] (read by the build)
+            const double2 xl = inx ? t : make_double2(0, 0);
+            const double tt = ac * (xl.x * xl.x + xl.y * xl.y);
+            const bool keep = dense_keep(tt, bc);
+            const double inv = keep ? 1.0 / tt : 0.0;
+            s.u[0][lane] = cscale(cmul(r, cconj(xl)), ac * inv);
+            s.u[1][lane] = make_double2(keep ? bc * inv : kDenseMaskedDiag, 0.0);
+        }
     }
     wave_lds_sync();
     if constexpr (DOT) {
@@ -1356,7 +1378,14 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = cmul(s.u[0][p + 8 * aa], s.u[1][q + 8 * bb]);
             wave_lds_sync();   // publish_col<0> reuses s.u[0]
-        } else if (WCE_PREFETCH_C ? !FC : cbuild) {   // a X C X'  (C zero-padded: no bounds checks)
+        } else if (WCE_DENSE_SCALED && cbuild) {   // M = C + diag(b / (a |x|^2))  (C zero-padded)
+            if (!WCE_PREFETCH_C) {   // (else A holds C already)
+#pragma unroll
+                for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+                    for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
+            }
+        } else if (!WCE_DENSE_SCALED && (WCE_PREFETCH_C ? !FC : cbuild)) {   // a X C X'  (C zero-padded: no bounds checks)
             double2 yr[RB], xc[RB];
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa) {
@@ -1379,15 +1408,17 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0, 0);
         }
-        const double bdiag = (p == q) ? bc : 0.0;
+        // scaled dense form: M's diagonal from u[1], bordered row conj(y) from u[0]
+        const bool scaled = WCE_DENSE_SCALED && cbuild;
+        const double2 *brow = scaled ? s.u[0] : s.rx;
 #pragma unroll
-        for (int aa = 0; aa < RB - 1; ++aa) A[aa][aa].x += bdiag;
-        A[RB - 1][RB - 1].x += (p == q && p < NSC - 8 * (RB - 1)) ? bc : 0.0;
+        for (int aa = 0; aa < RB - 1; ++aa) A[aa][aa].x += (p == q) ? (scaled ? s.u[1][p + 8 * aa].x : bc) : 0.0;
+        A[RB - 1][RB - 1].x += (p == q && p < NSC - 8 * (RB - 1)) ? (scaled ? s.u[1][p + 8 * (RB - 1)].x : bc) : 0.0;
         // bordered row 53 = conj(rx)  (lanes p == 5, register row 6).  A branch, not
         // a select: a select on an A element defeats SROA (A would live in scratch).
         if (p == NSC - 8 * (RB - 1)) {
 #pragma unroll
-            for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(s.rx[q + 8 * bb]);
+            for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(brow[q + 8 * bb]);
         }
     }
     if (WCE_DENSE_CHOL) {
@@ -1430,7 +1461,13 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     back_block<0>(A, P, rq, s, p, q, lane);
 #endif
     wave_lds_sync();
-    return cmul(s.x[lane], s.z[lane]);
+    const double2 xl = s.x[lane];
+    if (WCE_DENSE_SCALED && cbuild) {   // W = (x / (a conj x)) o (M^-1 y)
+        const double tt = ac * (xl.x * xl.x + xl.y * xl.y);
+        const double2 ph = dense_keep(tt, bc) ? cscale(cmul(xl, xl), 1.0 / tt) : make_double2(0.0, 0.0);
+        return cmul(ph, s.z[lane]);
+    }
+    return cmul(xl, s.z[lane]);
 }
 
 // R1: Ryy built from the rank-1 factors SolveArgs::cu/cw (TEXTBOOK: State::cvec)

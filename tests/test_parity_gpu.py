@@ -365,6 +365,40 @@ def test_model_covariance_dense_solve(gpu_wce, golden, oracle):
         assert normrel(out["ps_mmse"][f], exp) < TOL, f
 
 
+def test_model_covariance_qam_nulls_and_tiny_symbols(gpu_wce, golden, oracle):
+    """The dense solve's scaled form (M = C + diag(b / (a |x|^2)), W = x / (a
+    conj x) o M^-1 (rx / x)) on what it must special-case: non-constant-modulus
+    (16-QAM) symbols, null subcarriers (x = 0, e.g. DC), symbols so small that
+    a |x|^2 underflows, a frame of all-zero symbols, and tiny but representable
+    symbols; against the long double unified solve of Ryy = a X C X^H + b I."""
+    inp = golden["inputs"]
+    p = np.exp(-0.12 * np.arange(N))
+    R = np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    _, C, a, b = ctx.shared()
+    rng = np.random.default_rng(41)
+    B = 24
+    lv = np.array([-3, -1, 1, 3], float) * (8.8753 / np.sqrt(10))
+    tx = lv[rng.integers(0, 4, (B, NBLK, N))] + 1j * lv[rng.integers(0, 4, (B, NBLK, N))]
+    h = (rng.standard_normal((B, 1, N)) + 1j * rng.standard_normal((B, 1, N))) * 0.01
+    rx = tx * h + 1e-4 * (rng.standard_normal(tx.shape) + 1j * rng.standard_normal(tx.shape))
+    tx[1:, :, 26] = 0                 # DC null
+    tx[2, 0, [3, 40]] = 0             # more nulls
+    tx[3, 0, 7] = 1e-170 + 1e-170j    # |x|^2 underflows
+    tx[4, 0, 11] = 1e-90              # tiny, kept
+    tx[5, 0, :] = 0                   # no symbols at all: H = 0
+    out = ctx.estimate_host(tx, rx, mask=gpu_wce.PS_MMSE)
+    ones = np.ones(N, np.uint8)
+    for f in range(B):
+        exp = oracle.mmse_unified(C, ones, a, b, tx[f, 0], rx[f, 0])
+        got = out["ps_mmse"][f]
+        assert np.all(np.isfinite(got)), f
+        if not np.any(exp):
+            assert not np.any(got), f
+        else:
+            assert normrel(got, exp) < TOL, f
+
+
 @pytest.mark.parametrize("mask_name", ["ALL", "MMSE_FC_ML"])
 def test_plan_graph_replay_matches_estimate(gpu_wce, golden, mask_name):
     """wce_plan (HIP graph capture of one estimate call) replays to bit-identical
