@@ -148,13 +148,17 @@ __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, u
     }
 }
 template <bool EQ>
+#ifndef WCE_EQ_NT_LOAD   // A/B: the equalizer's rx blocks (read once) by nontemporal loads
+#define WCE_EQ_NT_LOAD 1
+#endif
 __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
                                          double2 hcub, double2 hsnc)
 {
     double2 rv[NBLK];
     if constexpr (EQ) {
 #pragma unroll
-        for (int b = 0; b < NBLK; b++) rv[b] = ld2(a.rx, f * a.fs + k + b * a.bs);
+        for (int b = 0; b < NBLK; b++)
+            rv[b] = WCE_EQ_NT_LOAD ? ld2_nt(a.rx, f * a.fs + k + b * a.bs) : ld2(a.rx, f * a.fs + k + b * a.bs);
     }
     ls_store_rv<EQ>(a, f, k, mask, hlt, hlin, hcub, hsnc, rv);
 }
@@ -1509,7 +1513,7 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     // ---- LS family + equalization of frame f (main.c:66-146, WiFi_Equalization.m)
     const uint32_t mask = l.mask;
     if (!mask) return;
-    const double2 rp = l.rx_pre ? ld2(l.rx_pre, f * l.ps + k) : make_double2(0, 0);
+    const double2 rp = !l.rx_pre ? make_double2(0, 0) : WCE_EQ_NT_LOAD ? ld2_nt(l.rx_pre, f * l.ps + k) : ld2(l.rx_pre, f * l.ps + k);
     const LsLane c = ls_lane(st, l.tx_pre, k);
     // pilot LS from the frame data the solve staged in LDS (pilots are in X in both modes)
     // lane j < 4 divides pilot j once; the four values are broadcast by readlane
