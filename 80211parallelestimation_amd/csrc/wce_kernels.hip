@@ -1756,7 +1756,7 @@ static inline int variant(int which) { return __atomic_load_n(&g_variant[which],
 
 // blocks of 4 waves for a tile kernel: one wave per tile up to the device's
 // resident-wave budget (CUs x waves per CU), grid-stride past it
-static int64_t tile_blocks(int64_t tiles, int waves_per_cu)
+static int cu_count()
 {
     static int cus = 0;
     if (!cus) {
@@ -1765,7 +1765,12 @@ static int64_t tile_blocks(int64_t tiles, int waves_per_cu)
             cus = n;
         if (cus <= 0) cus = 256;
     }
-    const int64_t cap = (int64_t)cus * waves_per_cu / LS_WAVES;
+    return cus;
+}
+
+static int64_t tile_blocks(int64_t tiles, int waves_per_cu)
+{
+    const int64_t cap = (int64_t)cu_count() * waves_per_cu / LS_WAVES;
     const int64_t need = (tiles + LS_WAVES - 1) / LS_WAVES;
     return need < cap ? need : cap;
 }
@@ -1867,9 +1872,94 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
     return hip_status(hipGetLastError());
 }
 
+// H = C W for the dense-C (COV) path, streaming form.  matvec_kernel runs one
+// 16-frame tile per wave and one wave round for a whole launch, so every wave
+// loads W, multiplies, then stores at the same time: the HBM and MFMA phases
+// never overlap.  Here C is staged once per workgroup in LDS (row stride 57
+// complex: the 16 rows a read touches start 4 banks apart) and each wave
+// walks a strided sequence of 16-frame tiles, loading tile t + 1's W while
+// its MFMAs run on tile t.  Same fragment maps and summation order as
+// matvec_kernel, so H is bit-identical.
+#ifndef WCE_APPLY_V2
+#define WCE_APPLY_V2 1
+#endif
+#ifndef WCE_APPLY_WG_PER_CU
+#define WCE_APPLY_WG_PER_CU 2
+#endif
+constexpr int ACS = 57;
+__device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t n, int64_t g, int ml, int kl,
+                                           double2 (&w)[KSTEPS])
+{
+    const int64_t fa = 16 * g + ml;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        w[s] = (fa < n && j < NSC) ? ld2(X, fa * xs + j) : make_double2(0, 0);
+    }
+}
+
+__global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const double *__restrict__ M, const double *X,
+                                                                        int64_t xs, double *Y, int64_t ys, int64_t n)
+{
+    __shared__ double2 sc[64 * ACS];
+    for (int e = threadIdx.x; e < 64 * 4 * KSTEPS; e += 256) {
+        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
+        sc[i * ACS + j] = ld2(M, i * CLD + j);   // M zero-padded 64 x 64
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t ng = (n + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * APPLY_WAVES;
+    int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6);
+    if (g >= ng) return;
+    double2 wn[KSTEPS];
+    apply_load(X, xs, n, g, ml, kl, wn);
+    for (; g < ng; g += stride) {
+        double ar[KSTEPS], ai[KSTEPS];
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            ar[s] = wn[s].x;
+            ai[s] = wn[s].y;
+        }
+        if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);   // next tile, under this one's MFMAs
+        const int64_t f0 = 16 * g;
+#pragma unroll 1
+        for (int nt = 0; nt < 4; ++nt) {
+            const int i = 16 * nt + ml;
+            v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s) {
+                const double2 c = sc[i * ACS + 4 * s + kl];
+                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
+                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai[s], c.y, accr, 0, 0, 0);
+                acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
+                acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
+            }
+            if (i < NSC) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t fr = f0 + kl + 4 * r;
+                    if (fr < n) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
+                }
+            }
+        }
+    }
+}
+
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream)
 {
-    return launch_matvec(st->C, nullptr, W, stride, H, nullptr, stride, n, false, stream);
+    // the streaming kernel once every wave gets >= 4 tiles (131,072 frames on
+    // 256 CUs); below that one wave round of matvec_kernel is as fast or faster
+    // (profiles/r02_ab_apply.txt)
+    const int64_t tiles = (n + 15) / 16;
+    if (!WCE_APPLY_V2 || tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * WCE_APPLY_WG_PER_CU)
+        return launch_matvec(st->C, nullptr, W, stride, H, nullptr, stride, n, false, stream);
+    static_assert(APPLY_WAVES == LS_WAVES, "tile_blocks counts LS_WAVES waves per workgroup");
+    const int64_t blocks = tile_blocks(tiles, APPLY_WAVES * WCE_APPLY_WG_PER_CU);
+    hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st->C, W, stride, H,
+                       stride, n);
+    return hip_status(hipGetLastError());
 }
 
 int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, double *Y, int64_t ys, int64_t n,

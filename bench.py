@@ -369,6 +369,23 @@ def main():
                         "mfma_busy_frac_pmc": ka["SQ_VALU_MFMA_BUSY_CYCLES"] / (ka["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4),
                         "note": "executed = 224 MFMA/wave x 2,048 flop: 56 x 64 zero-padded (53 x 53 useful, "
                                 "x1.276); busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
+        # the same product at 1,048,576 frames (the configs[3] batch): past 131,072
+        # frames mmse_apply switches to apply_kernel (C staged in LDS, each wave
+        # streaming 16-frame tiles with the next tile's W loaded under the MFMAs).
+        # W = the 65,536 solved frames tiled 16 times (device copies), so the
+        # operands are real solutions, not zeros.
+        nbig = 16 * B
+        Wb, Hb = wce.DeviceArray((nbig, N)), wce.DeviceArray((nbig, N))
+        for t in range(16):
+            assert wce.load().wce_memcpy_dtod(Wb.addr + t * B * N * 16, W.addr, B * N * 16, s) == 0
+        for _ in range(2):
+            ctx3.mmse_apply(Wb, Hb, nbig, N, s)
+        t_big = time_events(wce, stream, lambda: ctx3.mmse_apply(Wb, Hb, nbig, N, s), reps)
+        ach_big = FLOP_APPLY * nbig / (t_big * 1e-3) / 1e12
+        app["frames_1M"] = {"kernel": "apply_kernel (streaming, C in LDS)", "frames": nbig, "avg_launch_ms": t_big,
+                            "achieved_tflops": ach_big, "frac_fp64_peak": ach_big / PEAK_FP64_TFLOPS,
+                            "achieved_GBs": 2 * N * 16 * nbig / (t_big * 1e-3) / 1e9}
+        del Wb, Hb
         res["apply_kernel"] = app
         del ctx3
 

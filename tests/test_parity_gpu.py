@@ -152,13 +152,15 @@ def test_mfma_apply_exact_integers(gpu_wce, golden):
     Cpad = np.zeros((64, 64), np.complex128)     # State.C is zero-padded to 64 x 64
     Cpad[:N, :N] = C
     assert lib.wce_memcpy_htod(ptr, Cpad.ctypes.data_as(ctypes.c_void_p), Cpad.nbytes) == 0
-    for B in (1, 16, 37):
+    # 131,109 frames: several 16-frame tiles per wave of the streaming apply
+    for B in (1, 16, 37, 16 * 4 * 2048 + 37):
         W = (rng.integers(-5, 6, (B, N)) + 1j * rng.integers(-5, 6, (B, N))).astype(np.complex128)
         dW = gpu_wce.DeviceArray.from_numpy(W)
         dH = gpu_wce.DeviceArray((B, N), zero=True)
         ctx.mmse_apply(dW, dH, B)
         gpu_wce.synchronize()
-        assert np.array_equal(dH.numpy(), W @ C.T), B
+        got, want = dH.numpy(), W @ C.T
+        assert np.array_equal(got, want), (B, np.nonzero((got != want).any(1))[0][:8])
         ctx.mmse_apply(dW, dW, B)           # in place
         gpu_wce.synchronize()
         assert np.array_equal(dW.numpy(), W @ C.T), B

@@ -1,7 +1,7 @@
 """Interleaved A/B of whole libwce.so builds (tools/variants.sh) on one leg,
 one process: rounds x libraries, HIP-event timing per launch.
 legs: config5 (all 5 estimators + equalization fused, fp32 LS/eq outputs,
-per-frame preambles), headline (PS_MMSE TEXTBOOK), dense (COV mmse_solve).
+per-frame preambles), headline (PS_MMSE TEXTBOOK), dense (COV mmse_solve), apply (COV H = C W).
 usage: python tools/ab_libs.py build_variants/A build_variants/B [--leg config5] [--frames 262144]"""
 import argparse
 import importlib.util
@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
-ap.add_argument("--leg", choices=["config5", "headline", "dense"], default="config5")
+ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply"], default="config5")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--frames", type=int, default=262144)
 ap.add_argument("--reps", type=int, default=10)
@@ -30,13 +30,14 @@ for d in args.dirs:
     m._lib = None
     m.load(os.path.join(d, "libwce.so"))
     st = m.Stream()
-    if args.leg == "dense":
+    if args.leg in ("dense", "apply"):
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rhh())
     else:
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_TEXTBOOK)
     tx, rx, pre = m.DeviceArray((n, NB, N)), m.DeviceArray((n, NB, N)), m.DeviceArray((n, N))
     ctx.synth(tx, rx, pre, n, seed=0x80211)
+    m.synchronize()   # synth runs on the null stream; the legs on st
     keep = [tx, rx, pre]
     if args.leg == "config5":
         outs = [m.DeviceArray((n, N), np.complex64) for _ in range(4)] + [m.DeviceArray((n, N))]
@@ -52,6 +53,12 @@ for d in args.dirs:
         o = m.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
         f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.PS_MMSE, st.handle))(ctx, fr, o, st, m)
         keep.append(H)
+        check = H
+    elif args.leg == "apply":   # H = C W alone, on the solve's W
+        W, H = m.DeviceArray((n, N)), m.DeviceArray((n, N))
+        ctx.mmse_solve(ctx.frames(tx, rx, n), W, N, st.handle)
+        f = (lambda c, W, H, st: lambda: c.mmse_apply(W, H, n, N, st.handle))(ctx, W, H, st)
+        keep += [W, H]
         check = H
     else:
         W = m.DeviceArray((n, N))
@@ -72,8 +79,19 @@ for rd in range(args.rounds):
         e1.record(st.handle)
         times[name].append(e0.elapsed_ms(e1) / args.reps)
 outs = [r[4].numpy() for r in runs]
+if args.leg == "apply":   # each library's H against its own W: H = C W exactly as numpy forms it (to rounding)
+    for name, m, st, f, check, keep, ctx in runs:
+        Wh = keep[3].numpy()
+        C = ctx.shared()[1]
+        ref = Wh @ C.T
+        o = check.numpy()
+        den = np.abs(ref).max(1)
+        err = np.abs(o - ref).max(1) / np.where(den > 0, den, 1)
+        print(f"apply {name}: W all-zero frames {int(np.sum(~Wh.any(1)))}, max norm-rel |H - W C^T| {err.max():.2e}")
 for (name, *_), o in zip(runs, outs):
     print(f"{args.leg} {name}: median {np.median(times[name]) * 1e3:.1f} us  "
           f"({', '.join(f'{t * 1e3:.0f}' for t in times[name])})  same output as {runs[0][0]}: "
-          f"{bool(np.array_equal(o, outs[0]))}  max norm-rel diff "
-          f"{float(np.max(np.abs(o - outs[0]).reshape(n, -1).max(1) / np.abs(outs[0]).reshape(n, -1).max(1))):.2e}")
+          f"{bool(np.array_equal(o, outs[0], equal_nan=True))}  max norm-rel diff "
+          f"{float(np.nanmax(np.abs(o - outs[0]).reshape(n, -1).max(1) / np.abs(outs[0]).reshape(n, -1).max(1))):.2e}"
+          f"  non-finite frames {int(np.sum(~np.isfinite(o.reshape(n, -1)).all(1)))}"
+          f"  all-zero frames {int(np.sum(~o.reshape(n, -1).any(1)))}")
