@@ -342,6 +342,7 @@ static int ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, v
 {
     if (n < 0) return fail(WCE_EINVAL, "n < 0");
     if (n == 0) return WCE_OK;
+    if (n > (int64_t)0x7fffffff * 256) return fail(WCE_EINVAL, "n too large for one launch");   // also keeps n * 32 in range
     if (!src || !dst) return fail(WCE_EINVAL, "null src/dst");
     if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
         return fail(WCE_EINVAL, "src/dst not 16-byte aligned");   // 16-B vector loads and stores
