@@ -42,14 +42,17 @@ def _run(wce, ctx, fr, mask, f32=False):
     return [x.numpy() for x in outs] + [eq.numpy()]
 
 
-@pytest.mark.parametrize("mode,mask,f32", [
-    ("TEXTBOOK", "PS_MMSE", False),           # mmse_solve_fc_kernel
-    ("REF", "PS_MMSE", False),                # mmse_ref_flat_kernel
-    ("TEXTBOOK", "LT_LS|PS_LINEAR", False),   # ls_elem_kernel
-    ("TEXTBOOK", "ALL", True),                # fused solve + LS family + equalization, fp32 outputs
-    ("COV", "PS_MMSE", False),                # dense solve + MFMA apply
+@pytest.mark.parametrize("mode,mask,f32,sem", [
+    ("TEXTBOOK", "PS_MMSE", False, "C"),             # mmse_solve_fc_kernel
+    ("REF", "PS_MMSE", False, "C"),                  # mmse_ref_flat_kernel
+    ("TEXTBOOK", "LT_LS|PS_LINEAR", False, "C"),     # ls_elem_kernel
+    ("TEXTBOOK", "ALL", True, "C"),                  # fused solve + LS family + equalization, fp32 outputs
+    ("COV", "PS_MMSE", False, "C"),                  # dense solve + MFMA apply
+    ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "C"),   # per-frame covariance: factor matvecs + solve
+    ("TEXTBOOK", "LS_ALL", False, "MATLAB"),         # ls_kernel, MATLAB semantics (4-block averages)
+    ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "MATLAB"),   # split per-block solves + fc_finish
 ])
-def test_64bit_frame_indexing(layouts, mode, mask, f32):
+def test_64bit_frame_indexing(layouts, mode, mask, f32, sem):
     wce, inp, (tx, rx, pre), big = layouts
     if mode == "COV":
         p = np.exp(-0.12 * np.arange(N))
@@ -59,8 +62,9 @@ def test_64bit_frame_indexing(layouts, mode, mask, f32):
     m = 0
     for name in mask.split("|"):
         m |= getattr(wce, name)
-    dense = ctx.frames(tx, rx, B, rx_pre=pre)
-    strided = ctx.frames(big[0], big[1], B, frame_stride=S, rx_pre=big[2], pre_stride=S)
+    se = getattr(wce, "SEM_" + sem)
+    dense = ctx.frames(tx, rx, B, rx_pre=pre, semantics=se)
+    strided = ctx.frames(big[0], big[1], B, frame_stride=S, rx_pre=big[2], pre_stride=S, semantics=se)
     want = _run(wce, ctx, dense, m, f32)
     got = _run(wce, ctx, strided, m, f32)
     for i, (g, w) in enumerate(zip(got, want)):
