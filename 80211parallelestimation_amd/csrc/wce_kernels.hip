@@ -904,6 +904,9 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_PREFETCH_C
 #define WCE_PREFETCH_C 0
 #endif
+#ifndef WCE_ABLATE_KEEP  // timing-only build: dense Cholesky without keeping L (with WCE_ABLATE_BACKSOLVE)
+#define WCE_ABLATE_KEEP 0
+#endif
 #ifndef WCE_ABLATE_RYY   // timing-only build: Ryy = b I (no C loads, no build)
 #define WCE_ABLATE_RYY 0
 #endif
@@ -1024,6 +1027,43 @@ __device__ __forceinline__ void keep_where(bool sel, double2 &a, double2 c)
     a.y = sel ? c.y : a.y;
 }
 
+#ifndef WCE_KEEP_EXEC   // the KEEP path's per-step lane writes as EXEC-masked moves instead of compare + selects
+#define WCE_KEEP_EXEC 1
+#endif
+// rsel[lane L] = rs (wave-uniform, in SGPRs): one v_mov_b64 under EXEC = lane L
+// instead of v_cmp + two v_cndmask per step.  L is a constant after unrolling.
+__device__ __forceinline__ void keep_rsel_lane(double &rsel, int L, double rs)
+{
+    if (!WCE_KEEP_EXEC) {
+        keep_rsel(rsel, (int)threadIdx.x == L, rs);
+        return;
+    }
+    uint64_t sv;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_mov_b64 exec, %[m]\n\t"
+                 "v_mov_b64 %[r], %[v]\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [r] "+v"(rsel), [sv] "=&s"(sv)
+                 : [m] "s"(1ull << L), [v] "s"(rs));
+}
+// a = c on the lanes of mask m (a constant): two v_mov_b64 under EXEC
+__device__ __forceinline__ void keep_where_mask(uint64_t m, bool sel, double2 &a, double2 c)
+{
+    if (!WCE_KEEP_EXEC) {
+        keep_where(sel, a, c);
+        return;
+    }
+    uint64_t sv;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_mov_b64 exec, %[m]\n\t"
+                 "v_mov_b64 %[ax], %[cx]\n\t"
+                 "v_mov_b64 %[ay], %[cy]\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [ax] "+v"(a.x), [ay] "+v"(a.y), [sv] "=&s"(sv)
+                 : [m] "s"(m), [cx] "v"(c.x), [cy] "v"(c.y));
+}
+constexpr uint64_t lanes_q(int qq) { return 0x0101010101010101ull << qq; }   // lanes with q == qq
+
 // KEEP (the dense-C path, which back-substitutes): every finished panel is
 // written back into its block column of A (to_blocks), block column 6 keeps
 // its scaled columns, and rsel collects 1/sqrt(d_k) in lane k.
@@ -1069,7 +1109,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             const double rs = rsq_uniform(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
-            if (KEEP) keep_rsel(rsel, lane == k + 1, rs);
+            if (KEEP) keep_rsel_lane(rsel, k + 1, rs);
             double2 Rn = R;
             if (PRE) {
                 wave_lds_sync();
@@ -1091,7 +1131,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double rs = rsq_uniform(readlane_f64(P[0].x, k + 1));
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
-                if (KEEP) keep_rsel(rsel, lane == k + 1, rs);
+                if (KEEP) keep_rsel_lane(rsel, k + 1, rs);
                 if (PRE) {
                     wave_lds_sync();
                     R = next[8 * (KB + 1) + (lane & 7)];
@@ -1101,8 +1141,8 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
                 if (q == 0) next[p + 8 * (KB + 1)] = cs;
                 if (KEEP) {
-                    keep_rsel(rsel, lane == k + 1, rs);
-                    keep_where(q == 0, A[KB + 1][KB + 1], cs);
+                    keep_rsel_lane(rsel, k + 1, rs);
+                    keep_where_mask(lanes_q(0), q == 0, A[KB + 1][KB + 1], cs);
                 }
             }
             upd_cols_chol<KB + 2>(A, Ur, col, p, q);
@@ -1149,8 +1189,8 @@ __device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s
         const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;
-        keep_rsel(rsel, lane == k + 1, rs);
-        keep_where(q == kq + 1, A[RB - 1][RB - 1], cs);
+        keep_rsel_lane(rsel, k + 1, rs);
+        keep_where_mask(lanes_q(kq + 1), q == kq + 1, A[RB - 1][RB - 1], cs);
         wave_lds_sync();
     }
 }
@@ -1170,12 +1210,12 @@ __device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], SolveLds &s, in
     s.u[0][lane] = P[0];
     wave_lds_sync();
     double2 R = WCE_DPP_PANEL ? s.u[0][lane & 7] : make_double2(0.0, 0.0);
-    chol_panel<0, 0, true>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<1, 0, true>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<2, 0, true>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<3, 0, true>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<4, 0, true>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<5, 0, true>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<0, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<1, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<2, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<3, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<4, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+    chol_panel<5, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
     chol_last_keep(A, s, p, q, lane, rsel);
     wave_lds_sync();
     s.rd[lane] = lane < NSC ? rsel : 0.0;   // conv is dead: rd and z share its LDS

@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
-ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply"], default="config5")
+ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense"], default="config5")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--frames", type=int, default=262144)
 ap.add_argument("--reps", type=int, default=10)
@@ -60,7 +60,9 @@ for d in args.dirs:
         f = (lambda c, W, H, st: lambda: c.mmse_apply(W, H, n, N, st.handle))(ctx, W, H, st)
         keep += [W, H]
         check = H
-    else:
+    else:   # dense: COV mmse_solve_kernel<false>; r1dense: TEXTBOOK through the same back-substitution kernel (<true>)
+        if args.leg == "r1dense":
+            ctx.set_border_dot(False)
         W = m.DeviceArray((n, N))
         fr = ctx.frames(tx, rx, n)
         f = (lambda c, fr, W, st: lambda: c.mmse_solve(fr, W, N, st.handle))(ctx, fr, W, st)
