@@ -935,7 +935,8 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 // it gets y_i = 0 and M_ii = 1e200, whose coupling |C_ij|^2 / M_ii is below
 // half an ulp of every other entry, and phase 0.
 constexpr double kDenseMaskedDiag = 1e200;
-__device__ __forceinline__ bool dense_keep(double tt, double bc) { return tt > 0.0 && tt * 1e200 > bc; }
+// (written so that a NaN |x|^2 counts as kept: non-finite input stays non-finite in H, where the guard sees it)
+__device__ __forceinline__ bool dense_keep(double tt, double bc) { return !(tt <= 0.0 || tt * 1e200 <= bc); }
 // One block's solve; returns w_lane = x_lane z_lane (0 for lanes >= 53 is
 // not guaranteed: callers store lanes < 53 only).
 // FC: per-frame rank-1 covariance C_f = cu_f cw_f^T (SolveArgs::cu/cw, frame f)

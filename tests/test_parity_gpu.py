@@ -389,9 +389,13 @@ def test_model_covariance_qam_nulls_and_tiny_symbols(gpu_wce, golden, oracle):
     tx[3, 0, 7] = 1e-170 + 1e-170j    # |x|^2 underflows
     tx[4, 0, 11] = 1e-90              # tiny, kept
     tx[5, 0, :] = 0                   # no symbols at all: H = 0
+    tx[6, 0, 9] = np.nan              # non-finite input must stay visible in H (not masked as a null)
     out = ctx.estimate_host(tx, rx, mask=gpu_wce.PS_MMSE)
+    assert not np.all(np.isfinite(out["ps_mmse"][6]))
     ones = np.ones(N, np.uint8)
     for f in range(B):
+        if f == 6:
+            continue
         exp = oracle.mmse_unified(C, ones, a, b, tx[f, 0], rx[f, 0])
         got = out["ps_mmse"][f]
         assert np.all(np.isfinite(got)), f
