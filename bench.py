@@ -384,7 +384,21 @@ def main():
         ach_big = FLOP_APPLY * nbig / (t_big * 1e-3) / 1e12
         app["frames_1M"] = {"kernel": "apply_kernel (streaming, C in LDS)", "frames": nbig, "avg_launch_ms": t_big,
                             "achieved_tflops": ach_big, "frac_fp64_peak": ach_big / PEAK_FP64_TFLOPS,
-                            "achieved_GBs": 2 * N * 16 * nbig / (t_big * 1e-3) / 1e9}
+                            "achieved_GBs": 2 * N * 16 * nbig / (t_big * 1e-3) / 1e9,
+                            "algorithmic_bytes": 2 * N * 16 * nbig}
+        # its MFMA counters from same-size launches (tools/pmc_legs.sh apply1m);
+        # the grid is capped at 2 workgroups per CU, so check the output bytes:
+        # WRITE_SIZE runs ~9% over them (the 5-row last output tile writes
+        # partial 64-B sectors, as matvec_kernel's does)
+        kb, bsrc = pmc_leg("apply1m", nbig, N * 16.0 * nbig, tol=0.12)
+        app["frames_1M"]["pmc_source"] = bsrc
+        if kb:
+            mf = kb["SQ_INSTS_VALU_MFMA_F64"]
+            app["frames_1M"].update({
+                "traffic": hbm_bytes(kb),
+                "mfma_insts": mf,
+                "executed_tflops": mf * 2 * 16 * 16 * 4 / (t_big * 1e-3) / 1e12,
+                "mfma_busy_frac_pmc": kb["SQ_VALU_MFMA_BUSY_CYCLES"] / (kb["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4)})
         del Wb, Hb
         res["apply_kernel"] = app
         del ctx3

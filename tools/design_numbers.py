@@ -58,7 +58,10 @@ if "frames_1M" in ap:
     ab = ap["frames_1M"]
     row("`apply_kernel` as `H = C·W`, 1,048,576 frames (streaming: C in LDS, next tile's W loaded under the MFMAs)",
         f"{ab['avg_launch_ms'] * 1e3:.0f} µs; {ab['achieved_tflops']:.1f} TFLOP/s algorithmic = "
-        f"{100 * ab['frac_fp64_peak']:.0f}% of FP64 peak; {ab['achieved_GBs'] / 1000:.2f} TB/s of W in + H out")
+        f"{100 * ab['frac_fp64_peak']:.0f}% of FP64 peak; {ab['achieved_GBs'] / 1000:.2f} TB/s of W in + H out"
+        + (f"; {ab['executed_tflops']:.1f} TFLOP/s executed, MFMA pipe busy {100 * ab['mfma_busy_frac_pmc']:.0f}% (PMC of "
+           f"same-size launches); traffic {ab['traffic'] / 1e6:.0f} MB vs {ab['algorithmic_bytes'] / 1e6:.0f} MB"
+           if "executed_tflops" in ab else ""))
 row("per-frame covariance MMSE (`FRAME_COV`)",
     f"{d['frame_cov']['textbook']['frames_per_s']:.3g} frames/s TEXTBOOK, {d['frame_cov']['ref']['frames_per_s']:.3g} REF")
 row("config 5 share (131,072 frames, all 5 + equalization, fused)",

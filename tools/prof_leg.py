@@ -27,6 +27,7 @@ N, NBLK = 53, 15
 LEGS = {
     "headline": ("mmse_solve_fc_kernel", 65536),
     "apply": ("matvec_kernel<false, false, 1>", 65536),
+    "apply1m": ("apply_kernel", 1 << 20),             # the streaming apply past 131,072 frames
     "cov_solve": ("mmse_solve_kernel<false>", 65536),
     "ref": ("mmse_ref_flat_kernel", 1 << 20),
     "ls": ("ls_elem_kernel", 1 << 20),
@@ -52,7 +53,7 @@ def main():
     inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
     leg = args.leg
     n = LEGS[leg][1]
-    if leg in ("headline", "apply", "cov_solve"):
+    if leg in ("headline", "apply", "apply1m", "cov_solve"):
         if leg == "headline":
             ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
         else:
