@@ -913,6 +913,9 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_SOLVE_WAVES_PER_SIMD
 #define WCE_SOLVE_WAVES_PER_SIMD 3
 #endif
+#ifndef WCE_SOLVE_NT_LOAD   // A/B: the solve's frame loads (read once) nontemporal
+#define WCE_SOLVE_NT_LOAD 0
+#endif
 #ifndef WCE_STASH_COLS   // dense Cholesky: finished panel columns to LDS as they complete
 #define WCE_STASH_COLS 1
 #endif
@@ -1380,8 +1383,8 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #endif
     {
         const bool act = lane < NSC;
-        const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
-        const double2 r = act ? ld2(a.rx, base + lane) : make_double2(0, 0);
+        const double2 t = !act ? make_double2(0, 0) : WCE_SOLVE_NT_LOAD ? ld2_nt(a.tx, base + lane) : ld2(a.tx, base + lane);
+        const double2 r = !act ? make_double2(0, 0) : WCE_SOLVE_NT_LOAD ? ld2_nt(a.rx, base + lane) : ld2(a.rx, base + lane);
         const bool inx = act && ((st->xmask >> lane) & 1ull);
         s.x[lane] = inx ? t : make_double2(0, 0);
         s.rx[lane] = r;
