@@ -142,7 +142,12 @@ __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, u
         for (int b = 0; b < NBLK; b++) {
             const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
             const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
+#ifdef WCE_ABLATE_EQ_VALU   // timing-only: store rx instead of rx / H (same traffic, no blend/division)
+            const double2 e = k == WCE_DC ? make_double2(0, 0) : rv[b];
+            (void)hu;
+#else
             const double2 e = k == WCE_DC ? make_double2(0, 0) : cdiv(rv[b], hu);
+#endif
             st_out(a.eq, eb + b * a.eqbs, e, f32);
         }
     }
