@@ -164,6 +164,15 @@ def test_mfma_apply_exact_integers(gpu_wce, golden):
         ctx.mmse_apply(dW, dW, B)           # in place
         gpu_wce.synchronize()
         assert np.array_equal(dW.numpy(), W @ C.T), B
+    # padded rows (stride 64, 1 KiB per frame), both kernels, in place
+    for B in (37, 16 * 4 * 2048 + 37):
+        W = (rng.integers(-5, 6, (B, 64)) + 1j * rng.integers(-5, 6, (B, 64))).astype(np.complex128)
+        dW = gpu_wce.DeviceArray.from_numpy(W)
+        ctx.mmse_apply(dW, dW, B, 64)
+        gpu_wce.synchronize()
+        got = dW.numpy()
+        assert np.array_equal(got[:, :N], W[:, :N] @ C.T), B
+        assert np.array_equal(got[:, N:], W[:, N:]), B      # the padding is never written
 
 
 def test_strided_layout_and_block(gpu_wce, golden, oracle):
