@@ -274,7 +274,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter()
     stream.synchronize()
+    t_done = time.perf_counter()
     dist.barrier()
     t1 = time.perf_counter()
     elapsed = dist.max(t1 - t0)
@@ -288,6 +290,10 @@ def main():
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "prewarm_s": args.prewarm_s, "nonfinite_frames": nonfinite,
+           # where this rank's timed region went: host enqueue of the K steps,
+           # the wait for the stream, the closing barrier (rank 0's view)
+           "timed_region_ms": {"enqueue": (t_enq - t0) * 1e3, "stream_sync": (t_done - t_enq) * 1e3,
+                               "barrier": (t1 - t_done) * 1e3},
            "config": {"workload": f"PS_MMSE {args.mode} (53x53 per-frame Hermitian solve of Ryy = X C X' + ow2 I, bordered read-out H = u s), BASELINE configs[2]",
                       "frames_per_gpu": B, "global_frames": B * dist.world, "subcarriers": N, "ofdm_blocks": NBLK,
                       "parallelism": f"dp{dist.world} (frames sharded, 1 RCCL state broadcast)"}}
@@ -442,8 +448,12 @@ def main():
 
         # BASELINE configs[3]: 1,048,576 frames in total, sharded over the
         # ranks (strong scaling), same kernel; all ranks, barrier + max
-        res["config4"] = bench_config4(wce, ctx, dist, stream, hs, max(5, args.steps // 5))
-        res["config5_sharded"] = bench_config5_sharded(wce, ctx, dist, stream, max(3, args.steps // 20))
+        # steps scale with the world size so every N times about the same
+        # per-rank work (at N=8 a shard is 131,072 frames, ~1 ms per step)
+        res["config4"] = bench_config4(wce, ctx, dist, stream, hs, max(5, args.steps // 5) * dist.world,
+                                       prewarm_s=args.prewarm_s)
+        res["config5_sharded"] = bench_config5_sharded(wce, ctx, dist, stream, max(3, args.steps // 20) * dist.world,
+                                                       prewarm_s=args.prewarm_s)
 
 
     if not args.no_cpu_baseline and dist.rank == 0 and dist.world == 1:
@@ -457,7 +467,22 @@ def main():
     dist.close()
 
 
-def bench_config5_sharded(wce, ctx, dist, stream, steps, total=1 << 20):
+def prewarm_sync(dist, stream, fn, seconds):
+    """Untimed clock ramp on every rank right before a sharded leg's timed
+    region.  Ranks > 0 reach these legs while rank 0 still runs its
+    single-GPU legs, and sit idle in the barrier meanwhile: without this their
+    GPUs start the timed steps cold, and the max over ranks is a cold rank's
+    time.  Barrier first so all ranks ramp together."""
+    stream.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(4):
+            fn()
+        stream.synchronize()
+
+
+def bench_config5_sharded(wce, ctx, dist, stream, steps, total=1 << 20, prewarm_s=0.3):
     """BASELINE configs[4] as the config names it: all 5 estimators +
     per-symbol equalization, fused, mixed precision (fp64 solve, LS family and
     equalized symbols stored fp32), per-frame preambles, `total` frames
@@ -474,6 +499,7 @@ def bench_config5_sharded(wce, ctx, dist, stream, steps, total=1 << 20):
     fr = ctx.frames(tx, rx, count, rx_pre=pre)
     for _ in range(3):
         ctx.estimate(fr, o, wce.ALL, s)
+    prewarm_sync(dist, stream, lambda: ctx.estimate(fr, o, wce.ALL, s), prewarm_s)
     stream.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
@@ -507,7 +533,7 @@ def config5_traffic(count, dt):
             "valu_insts_per_frame": k.get("SQ_INSTS_VALU", 0) / count}
 
 
-def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20):
+def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20, prewarm_s=0.3):
     """BASELINE configs[3]: `total` frames sharded contiguously over the
     ranks (wce_shard's partition), each rank generating its shard from the
     global frame index; timed like the headline (barrier + device sync on
@@ -522,6 +548,7 @@ def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20):
     o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
     for _ in range(3):
         ctx.estimate(fr, o, wce.PS_MMSE, stream.handle)
+    prewarm_sync(dist, stream, lambda: ctx.estimate(fr, o, wce.PS_MMSE, stream.handle), prewarm_s)
     stream.synchronize()
     dist.barrier()
     t0 = time.perf_counter()

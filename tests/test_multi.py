@@ -96,3 +96,40 @@ def test_native_comm_fails_loudly_without_device(wce):
     if wce.device_count() == 0:
         with pytest.raises(wce.WceError):
             multi.NativeComm(wce, b"\0" * multi.COMM_ID_BYTES, 1, 0, 0)
+
+
+class _NullStream:
+    def synchronize(self):
+        pass
+
+
+def _bench_dist_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), WCE_DIST_BACKEND="gloo")
+    sys.path.insert(0, REPO)
+    bench = importlib.import_module("bench")
+    d = bench.Dist()
+    try:
+        calls = []
+        bench.prewarm_sync(d, _NullStream(), lambda: calls.append(1), 0.05)
+        d.barrier()
+        q.put((rank, d.world, d.max(1.5 + rank), len(calls) > 0))
+    finally:
+        d.close()
+
+
+def test_bench_dist_control_path_gloo_world2():
+    """bench.py's Dist over gloo at world size 2 (the N>1 launch's control
+    path): the max over ranks every timed leg reports, the barriers, and the
+    synchronised prewarm the sharded legs run before their timed region."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, 2, 2.5, True), (1, 2, 2.5, True)]
