@@ -17,6 +17,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--pg", choices=["none", "nccl", "gloo"], default="none")
 ap.add_argument("--steps", type=int, default=100)
 ap.add_argument("--destroy", action="store_true")
+ap.add_argument("--barrier", action="store_true", help="dist.barrier(device_ids=[0]) before each region, as bench.py")
+ap.add_argument("--bcast", action="store_true", help="the state broadcast bench.py's make_ctx does")
 args = ap.parse_args()
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29551")
@@ -36,6 +38,8 @@ if args.pg != "none":
 wce = importlib.import_module("80211parallelestimation_amd")
 inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
 ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+if args.bcast:
+    importlib.import_module("80211parallelestimation_amd.multi").broadcast_state_device(dist, wce, ctx, src=0)
 st = wce.Stream()
 B, N = 65536, 53
 tx, rx = wce.DeviceArray((B, 15, N)), wce.DeviceArray((B, 15, N))
@@ -55,6 +59,9 @@ res = []
 for _ in range(3):
     e0, e1 = wce.Event(), wce.Event()
     st.synchronize()
+    if args.barrier:
+        dist.barrier(device_ids=[0])
+        st.synchronize()
     t0 = time.perf_counter()
     e0.record(st)
     for _ in range(args.steps):
@@ -62,5 +69,5 @@ for _ in range(3):
     e1.record(st)
     st.synchronize()
     res.append(((time.perf_counter() - t0) * 1e3 / args.steps, e0.elapsed_ms(e1) / args.steps))
-print(f"pg={args.pg}{' (destroyed)' if args.destroy else ''}: ms/step wall, events: "
+print(f"pg={args.pg}{' (destroyed)' if args.destroy else ''}{' barrier' if args.barrier else ''}{' bcast' if args.bcast else ''}: ms/step wall, events: "
       + "  ".join(f"{a:.4f} {b:.4f}" for a, b in res), flush=True)
