@@ -8,5 +8,5 @@ G=$R/gpurun_out
 cp "$G/bench_full.json" "$R/profiles/${RND}_bench.json"
 cp "$G/stats/run_kernel_stats.csv" "$R/profiles/${RND}_kernel_stats.csv"
 [ -f "$G/stats_head/run_kernel_stats.csv" ] && cp "$G/stats_head/run_kernel_stats.csv" "$R/profiles/${RND}_kernel_stats_headline.csv"
-cp "$G/pmc_legs.json" "$R/profiles/${RND}_pmc_legs.json"
+[ -f "$G/pmc_legs.json" ] && cp "$G/pmc_legs.json" "$R/profiles/${RND}_pmc_legs.json"
 echo "collected into profiles/ as ${RND}_*"

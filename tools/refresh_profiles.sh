@@ -11,8 +11,11 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 RND=${ROUND:-r02}
 mkdir -p "$R/gpurun_out"
-cd "$R" && bash tools/pmc_legs.sh > "$R/gpurun_out/pmc_legs.log" 2>&1 || exit $?
-cp "$R/gpurun_out/pmc_legs.json" "$R/profiles/${RND}_pmc_legs.json"   # the bench reads the newest
+# SKIP_PMC=1: keep the committed PMC legs (valid while the kernels are unchanged)
+if [ -z "$SKIP_PMC" ]; then
+  cd "$R" && bash tools/pmc_legs.sh > "$R/gpurun_out/pmc_legs.log" 2>&1 || exit $?
+  cp "$R/gpurun_out/pmc_legs.json" "$R/profiles/${RND}_pmc_legs.json"   # the bench reads the newest
+fi
 timeout -k 10 400 python3 "$R/bench.py" > "$R/gpurun_out/bench_full.json" 2> "$R/gpurun_out/bench_full.err" || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/stats" -o run \
