@@ -90,6 +90,9 @@ class Dist:
             if self.backend == "nccl":
                 torch.cuda.set_device(self.local)
                 dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+                # first all-reduce now, long before any timed region: the
+                # first one in a process sets RCCL up lazily
+                self.barrier()
             else:
                 self.device = self.local % max(1, torch.cuda.device_count())
                 dist.init_process_group("gloo")
