@@ -37,6 +37,15 @@ def test_contract_keys(line):
     assert abs(line["value"] - B / (line["ms_per_step"] * 1e-3)) / line["value"] < 1e-6
 
 
+def test_timed_region_breakdown(line):
+    """enqueue + stream wait + closing barrier = the timed wall of rank 0
+    (at N=1 it is the whole timed region; the closing barrier is a no-op)."""
+    t = line["timed_region_ms"]
+    total = t["enqueue"] + t["stream_sync"] + t["barrier"]
+    assert abs(total - line["ms_per_step"] * line["steps"]) / total < 1e-3
+    assert t["stream_sync"] > t["enqueue"]       # the launches queue ahead of the GPU
+
+
 def test_roofline_consistent(line):
     r = line["roofline"]
     assert r["bound"] in ("hbm", "mfma", "fp64-valu") and r["unit"] == "TFLOP/s"
