@@ -7,7 +7,7 @@ The package name starts with a digit, so import it with
 from .wce import (  # noqa: F401
     ALL, DC, EQUALIZE, FRAME_COV, LS_ALL, OUT_LS_F32, LT_LS, MMSE_COV, MMSE_REF, MMSE_TEXTBOOK, NBLK, NSC, PILOTS, PS_CUBIC, PS_LINEAR,
     PS_MMSE, PS_SINC, SEM_C, SEM_MATLAB, Context, DeviceArray, PinnedArray, Event, Frames, Outputs, Stream, WceError, device_count, load,
-    state_blob, synchronize, ldc_to_complex, complex_to_ldc, WiFi_channel_estimation_LT_LS, WiFi_channel_estimation_PS_Cubic,
+    state_blob, state_mode, cov_factor, synchronize, ldc_to_complex, complex_to_ldc, WiFi_channel_estimation_LT_LS, WiFi_channel_estimation_PS_Cubic,
     WiFi_channel_estimation_PS_Linear, WiFi_channel_estimation_PS_MMSE, WiFi_channel_estimation_PS_Sinc,
 )
 

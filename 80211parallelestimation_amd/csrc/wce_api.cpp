@@ -23,6 +23,9 @@ struct wce_ctx {
     int32_t mode = -1;          // State::mode, cached when the state becomes valid
     bool fuse = true;           // config-5 fusion (wce_debug_set_fusion turns it off for A/B)
     bool bdot = true;           // rank-1 C: second bordered row, no back-solve / GEMM (A/B switch)
+    int32_t cov_k0 = -1;        // State::cov_k0 (WCE_MMSE_COV: >= 0 low-rank Gram path, -1 dense)
+    int32_t cov_rank = 0;       // State::cov_rank
+    int cov_path = 0;           // wce_debug_set_cov_path: 0 auto, 1 dense, 2 low-rank
     // Workspaces (FRAME_COV factors, MATLAB per-block rows), one per stream:
     // calls on different streams never share scratch, so they may run
     // concurrently (SURVEY 8(b) threading).  A call holds its stream's entry
@@ -187,6 +190,10 @@ int wce_ctx_mark_ready(wce_ctx *c)
     if (magic != wce::STATE_MAGIC) return fail(WCE_ESTATE, "state buffer does not hold a valid state");
     HIPCHECK(hipMemcpy(&c->mode, reinterpret_cast<char *>(c->d_state) + offsetof(State, mode), sizeof(c->mode),
                        hipMemcpyDeviceToHost), "read state mode");
+    HIPCHECK(hipMemcpy(&c->cov_rank, reinterpret_cast<char *>(c->d_state) + offsetof(State, cov_rank),
+                       sizeof(c->cov_rank), hipMemcpyDeviceToHost), "read state rank");
+    HIPCHECK(hipMemcpy(&c->cov_k0, reinterpret_cast<char *>(c->d_state) + offsetof(State, cov_k0), sizeof(c->cov_k0),
+                       hipMemcpyDeviceToHost), "read state path");
     c->ready = true;
     return WCE_OK;
 }
@@ -199,6 +206,8 @@ int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
     DeviceGuard g(c->device);
     HIPCHECK(hipMemcpy(c->d_state, host_state, sizeof(State), hipMemcpyHostToDevice), "upload state");
     c->mode = static_cast<const State *>(host_state)->mode;
+    c->cov_k0 = static_cast<const State *>(host_state)->cov_k0;
+    c->cov_rank = static_cast<const State *>(host_state)->cov_rank;
     c->ready = true;
     return WCE_OK;
 }
@@ -219,6 +228,43 @@ int wce_ctx_get_shared(wce_ctx *c, wce_complex *h_lt, wce_complex *C, double *a,
     if (a) *a = h->acoef;
     if (b) *b = h->bcoef;
     delete h;
+    return WCE_OK;
+}
+
+// the WCE_MMSE_COV solve this ctx runs: -1 dense Ryy solve, else the block
+// row of the embedded Gram system (mmse_lr_kernel)
+static int cov_lr_k0(const wce_ctx *c)
+{
+    if (c->mode != WCE_MMSE_COV) return -1;
+    if (c->cov_path == 1) return -1;
+    if (c->cov_path == 2) {
+        const int k0 = (wce::NSC - c->cov_rank) / 8;
+        return k0 < wce::COV_K0_MAX ? k0 : wce::COV_K0_MAX;
+    }
+    return c->cov_k0;
+}
+
+int wce_ctx_cov_info(wce_ctx *c, int *rank, int *low_rank, double *lambda_max, double *lambda_min)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    if (c->mode != WCE_MMSE_COV) return fail(WCE_EINVAL, "not a WCE_MMSE_COV context");
+    double lm[2] = {0.0, 0.0};
+    DeviceGuard g(c->device);
+    HIPCHECK(hipMemcpy(lm, reinterpret_cast<char *>(c->d_state) + offsetof(State, cov_lmax), sizeof(lm),
+                       hipMemcpyDeviceToHost), "read state eigenvalues");
+    if (rank) *rank = c->cov_rank;
+    if (low_rank) *low_rank = cov_lr_k0(c) >= 0;
+    if (lambda_max) *lambda_max = lm[0];
+    if (lambda_min) *lambda_min = lm[1];
+    return WCE_OK;
+}
+
+extern "C" int wce_debug_set_cov_path(wce_ctx *c, int path)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (path < 0 || path > 2) return fail(WCE_EINVAL, "cov path: 0 auto, 1 dense, 2 low-rank");
+    c->cov_path = path;
     return WCE_OK;
 }
 
@@ -300,6 +346,9 @@ int wce_mmse_solve(wce_ctx *c, const wce_frames *in, wce_complex *W, int64_t w_s
     if (!W || (in->n_frames > 1 && w_stride < wce::NSC)) return fail(WCE_EINVAL, "bad W");
     if (in->semantics != WCE_SEM_C)
         return fail(WCE_EINVAL, "wce_mmse_solve (profiling entry) takes C semantics; MATLAB runs via wce_estimate");
+    if (cov_lr_k0(c) >= 0)
+        return fail(WCE_EINVAL, "wce_mmse_solve: this WCE_MMSE_COV ctx runs the low-rank path (H = U s, no W / apply "
+                                "stages); use wce_estimate");
     wce::SolveArgs a = solve_args(c, in, W, w_stride);
     if (a.hout) {   // the profiling pair solve -> apply keeps W = X z: rank-1 build only
         a.hout = 0;
@@ -496,7 +545,8 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     const bool mmse = (mask & WCE_EST_PS_MMSE) != 0;
     // Config-5 fusion: the LS family and equalization ride in the MMSE solve's
     // epilogue (C semantics); otherwise one HBM-streaming LS pass.
-    const bool fuse = c->fuse && ls && mmse && in->semantics == WCE_SEM_C;
+    const int lr_k0 = (mask & WCE_MMSE_FRAME_COV) ? -1 : cov_lr_k0(c);   // WCE_MMSE_COV low-rank path
+    const bool fuse = c->fuse && ls && mmse && in->semantics == WCE_SEM_C && lr_k0 < 0;
     const wce::LsArgs la = ls_args(in, out, mask, eq_src);
     if (ls && !fuse) {
         rc = wce::launch_ls(c->d_state, la, stream);
@@ -541,9 +591,15 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
             sa.ws = WS_LD;
         }
     }
+    double *H = reinterpret_cast<double *>(out->ps_mmse);
+    if (lr_k0 >= 0) {   // H = U s straight from the solve (split: H_b rows, then the block mean)
+        rc = wce::launch_mmse_lr(c->d_state, lr_k0, sa, stream);
+        if (rc) return fail(rc, "mmse_lr launch");
+        if (split) rc = wce::launch_avg_blocks(ws, WS_LD, H, out->out_stride, n, stream);
+        return rc ? fail(rc, "block average launch") : WCE_OK;
+    }
     rc = fuse ? wce::launch_mmse_solve_ls(c->d_state, sa, la, stream) : wce::launch_mmse_solve(c->d_state, sa, stream);
     if (rc) return fail(rc, "mmse_solve launch");
-    double *H = reinterpret_cast<double *>(out->ps_mmse);
     if (sa.hout && split) rc = wce::launch_fc_finish(sa, aux, H, out->out_stride, stream);
     else if (split) rc = wce::launch_matvec_avg(c->d_state->C, ws, WS_LD, sa.nblk, H, out->out_stride, n, stream);
     else if (!sa.hout) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream);   // H = C W in place

@@ -14,6 +14,7 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
+constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
 // others (one RCCL broadcast, 68 KB).  Complex values are {re, im} fp64.
@@ -38,9 +39,19 @@ struct State {
     double acoef, bcoef;       // Ryy = a X C X' + b I
     double ow2;                // noise variance (inputs.h:18)
     uint64_t xmask;            // bit k set: subcarrier k enters X
-    int32_t mode;              // WCE_MMSE_REF / WCE_MMSE_TEXTBOOK
+    int32_t mode;              // WCE_MMSE_REF / WCE_MMSE_TEXTBOOK / WCE_MMSE_COV
     int32_t magic;             // STATE_MAGIC once valid
-    int32_t pad[2];
+    // WCE_MMSE_COV low-rank factor (wce_state_build_cov): C = U U^H with
+    // U = F V_r sqrt(Lambda_r) from the 80-bit eigendecomposition of Rhh,
+    // zero-padded to 64 x 64 (U[k][j], k = subcarrier, j = eigen-direction),
+    // and its transpose UT[j][k].  cov_k0 >= 0: the per-frame solve runs the
+    // Gram system (a G^H G + b I) t = G^H rx, G = X U, embedded at block row
+    // cov_k0 of the register layout (mmse_lr_kernel); -1: the dense Ryy solve.
+    double U[CLD * CLD * 2];
+    double UT[CLD * CLD * 2];
+    double cov_lmax, cov_lmin; // largest / smallest kept eigenvalue of C
+    int32_t cov_rank;          // r = number of kept eigen-directions (0..53)
+    int32_t cov_k0;            // -1 dense; else first block row of the embedded Gram system
 };
 static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
 
@@ -128,12 +139,19 @@ int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, doub
 // H[f] = cu_f * mean_b dots[f*nb + b]  (per-frame covariance, MATLAB averaging)
 int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream);
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
+// WCE_MMSE_COV low-rank path: H (or, split, H_b per (frame, block) row) from
+// the Gram system embedded at block row k0 (State::cov_k0)
+int launch_mmse_lr(const State *st, int k0, const SolveArgs &a, void *stream);
+// H[f] = mean of X rows 4f .. 4f+3 (MATLAB block average, left to right)
+int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
 // kernel variants for A/B timing (wce_debug_set_variant)
 constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks (default), 1 = 64-frame tiles,
                                       // 2 = chunks with an uncapped grid
 constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks (grid capped at 2,048 blocks),
                                       // 1 = the same uncapped, 2 = one element per thread (ls_elem_kernel, default)
+constexpr int WCE_VARIANT_REF_LS = 2;  // REF PS_MMSE + LS family (+ eq), C semantics: 0 = ref_ls_elem_kernel
+                                      // (one element per thread, default), 1 = mmse_solve_ls_kernel (wave per frame)
 constexpr int WCE_VARIANT_COUNT = 4;
 int set_variant(int which, int value);
 int launch_ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, void *stream);

@@ -459,6 +459,27 @@ __device__ __forceinline__ double2 quad_sum_c(double2 t)
     return cadd(t, make_double2(dpp_quad<0x4E>(t.x), dpp_quad<0x4E>(t.y)));  // quad_perm [2,3,0,1]
 }
 
+// REF pilot term w x r and the output u s, with contraction off: every REF
+// kernel (flat, tiles, and the config-4 element kernel) rounds them alike
+// whatever code surrounds them, so their outputs stay bit-identical.
+__device__ __forceinline__ double2 ref_term(double2 w, double2 x, double2 r)
+{
+#pragma clang fp contract(off)
+    const double2 c = make_double2(w.x * x.x - w.y * x.y, w.x * x.y + w.y * x.x);
+    return make_double2(c.x * r.x - c.y * r.y, c.x * r.y + c.y * r.x);
+}
+__device__ __forceinline__ double2 ref_sum4(double2 t0, double2 t1, double2 t2, double2 t3, double rb)
+{
+#pragma clang fp contract(off)
+    const double2 a = make_double2(t0.x + t1.x, t0.y + t1.y), b = make_double2(t2.x + t3.x, t2.y + t3.y);
+    return make_double2((a.x + b.x) * rb, (a.y + b.y) * rb);
+}
+__device__ __forceinline__ double2 ref_out(double2 u, double2 s)
+{
+#pragma clang fp contract(off)
+    return make_double2(u.x * s.x - u.y * s.y, u.x * s.y + u.y * s.x);
+}
+
 __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
                                                             uint32_t nfr)
 {
@@ -496,8 +517,9 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
                 uf[i] = ld2(a.cu, (f_begin + f) * a.cs + k);
             }
         }
-        const double2 sj = quad_sum_c(cmul(cmul(wp, xt), xr));   // w^T X rx over frame j's pilots
-        if (lane < 4 * FLAT_FR && pj == 0) s_tab[lane >> 2] = cscale(sj, rb);
+        const double2 sj = quad_sum_c(ref_term(wp, xt, xr));   // w^T X rx over frame j's pilots
+        if (lane < 4 * FLAT_FR && pj == 0) s_tab[lane >> 2] = ref_sum4(sj, make_double2(0, 0), make_double2(0, 0),
+                                                                      make_double2(0, 0), rb);
         wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < FLAT_U; ++i) {
@@ -505,10 +527,70 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
             const uint32_t f = e / NSC, k = e - f * NSC;
             const int jl = (int)(f - ff) < FLAT_FR ? (int)(f - ff) : FLAT_FR - 1;
             const double2 u = shared ? s_u[k] : uf[i];
-            if (e < E) st2(a.w, (f_begin + f) * a.ws + k, cmul(u, s_tab[jl]));
+            if (e < E) st2(a.w, (f_begin + f) * a.ws + k, ref_out(u, s_tab[jl]));
         }
         wave_lds_sync();   // s_tab is rewritten by the next chunk
     }
+}
+
+// =====================================================================
+// BASELINE configs[4] in main.c semantics (round 3): REF PS_MMSE with any of
+// LT_LS / PS_Linear / PS_Cubic / PS_Sinc and equalization, one pass over HBM
+// (main.c:66-212, WiFi_Equalization.m:1-9).  REF has no factorisation (Ryy =
+// 2 ow2 I), so the whole request is streaming: one (frame, subcarrier) element
+// per thread, no grid stride (ls_elem_kernel's store pattern).  Each thread
+// gathers its frame's 4 pilot pairs (the ~1.2 frames a wave covers share their
+// 64-B sectors, so a pilot load instruction touches ~2 of them) and serves
+// every output of its element from them: the pilot LS values h_p (main.c:
+// 82-84) feed PS_Linear/Cubic/Sinc, s = w^T X rx / b (over the same pilots)
+// gives H_MMSE = u s, rx_pre its LT_LS, and the 15 rx blocks of its subcarrier
+// (all loads issued before any use) the equalized symbols.  The arithmetic is
+// ls_kernel's (ls_lane / lt_ls_lane / ps_lane / ls_store_rv) and
+// mmse_ref_flat_kernel's (quad order ((t0 + t1) + (t2 + t3)) * (1 / b)), so the
+// outputs are bit-identical to the separate passes.  a.cs != 0: per-frame
+// factors u_f, w_f (WCE_MMSE_FRAME_COV).
+// =====================================================================
+template <bool EQ>
+__global__ __launch_bounds__(256) void ref_ls_elem_kernel(const State *__restrict__ st, SolveArgs a, LsArgs l,
+                                                          int64_t f_begin, uint32_t nfr)
+{
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= nfr * (uint32_t)NSC) return;
+    const uint32_t fl = e / NSC;
+    const int k = (int)(e - fl * NSC);
+    const int64_t f = f_begin + fl;
+    const bool shared = a.cs == 0;
+    // ---- every load first
+    const int64_t po = f * a.fs + (int64_t)a.blk * a.bs;
+    double2 xt[4], xr[4], wp[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        xt[p] = ld2(a.tx, po + PILOT[p]);
+        xr[p] = ld2(a.rx, po + PILOT[p]);
+        const int64_t wo = shared ? PILOT[p] : f * a.cs + PILOT[p];
+        wp[p] = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
+    }
+    const double2 uk = ld2(a.cu, shared ? k : f * a.cs + k);
+    const double2 rp = l.rx_pre ? ld2_nt(l.rx_pre, f * l.ps + k) : make_double2(0, 0);
+    double2 rv[NBLK];
+    if constexpr (EQ) {
+#pragma unroll
+        for (int b = 0; b < NBLK; b++) rv[b] = ld2_nt(l.rx, f * l.fs + k + b * l.bs);
+    }
+    const LsLane c = ls_lane(st, l.tx_pre, k);
+    // ---- PS_MMSE (REF): H = u s, s = w^T X rx / b over the 4 pilots
+    double2 tp[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) tp[p] = ref_term(wp[p], xt[p], xr[p]);
+    st2(a.w, f * a.ws + k, ref_out(uk, ref_sum4(tp[0], tp[1], tp[2], tp[3], 1.0 / st->bcoef)));
+    // ---- LS family + equalization
+    double2 h[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) h[p] = cdiv(xr[p], xt[p]);                 // main.c:82-84
+    const double2 hlt = lt_ls_lane<false>(c, l.rx_pre != nullptr, rp, k);
+    double2 hlin, hcub, hsnc;
+    ps_lane<false>(c, l.mask, h[0], h[1], h[2], h[3], hlin, hcub, hsnc);
+    ls_store_rv<EQ>(l, f, k, l.mask, hlt, hlin, hcub, hsnc, rv);
 }
 
 // =====================================================================
@@ -563,8 +645,8 @@ __global__ __launch_bounds__(256) void mmse_ref_tile_kernel(const State *__restr
         // order ((t0 + t1) + (t2 + t3)) so the result matches the chunked kernel
         double2 tp[4];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) tp[p] = cmul(cmul(wp[p], xt[p]), xr[p]);
-        s_tab[lane] = cscale(cadd(cadd(tp[0], tp[1]), cadd(tp[2], tp[3])), rb);
+        for (int p = 0; p < 4; ++p) tp[p] = ref_term(wp[p], xt[p], xr[p]);
+        s_tab[lane] = ref_sum4(tp[0], tp[1], tp[2], tp[3], rb);
         wave_lds_sync();
         const uint32_t nf = min((uint32_t)TILE_F, nfr - f0);
         const uint32_t ne = nf * NSC;
@@ -573,7 +655,7 @@ __global__ __launch_bounds__(256) void mmse_ref_tile_kernel(const State *__restr
 #pragma unroll 4
         for (uint32_t e = lane; e < ne; e += 64) {
             const double2 u = shared ? s_u[wk.k] : ld2(a.cu, (f_begin + f0 + wk.f) * a.cs + wk.k);
-            st2_nt(a.w, obase + (int64_t)wk.f * a.ws + wk.k, cmul(u, s_tab[wk.f]));
+            st2_nt(a.w, obase + (int64_t)wk.f * a.ws + wk.k, ref_out(u, s_tab[wk.f]));
             wk.next();
         }
         wave_lds_sync();   // s_tab is rewritten by the next tile
@@ -597,6 +679,8 @@ __global__ __launch_bounds__(256) void mmse_ref_tile_kernel(const State *__restr
 // step k is issued, hiding the pivot chain and the LDS round trip.
 // =====================================================================
 constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
+typedef double v4d __attribute__((ext_vector_type(4)));   // one v_mfma_f64_16x16x4 accumulator
+constexpr int KSTEPS = 14;   // 4-deep MFMA k-steps over 56 >= 53 subcarriers
 
 constexpr int CVS = 9;    // row stride (complex) of the panel transpose buffer
 
@@ -706,18 +790,21 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
 #define WCE_CHAIN_1LANE 1
 #endif
 // 1/sqrt(d) of a wave-uniform pivot d.  The kernel is power-capped, so the
-// 6-op chain runs on lane 0 alone (EXEC = 1 inside the asm) and comes back
-// as a scalar (v_readlane of lane 0): the same arithmetic as rsq_nr (one
+// 6-op chain runs on one lane alone (EXEC = that lane inside the asm) and
+// comes back as a scalar (v_readlane): the same arithmetic as rsq_nr (one
 // third-order step after v_rsq_f64), bit-identical, at 1/64 of its energy.
-// Lane 0 is read explicitly (not readfirstlane), so it is right under any EXEC.
+// The lane is the lowest ACTIVE one (s_ff1 of EXEC), so under divergent
+// control flow the asm never writes a lane that is switched off.
 __device__ __forceinline__ double rsq_uniform(double d)
 {
     if (!WCE_CHAIN_1LANE) return rsq_nr(d);
     double y, t, e;
     uint64_t sv;
     const double c38 = 0.375;
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    const int l0 = __builtin_ctzll(ex);
     asm("s_mov_b64 %[sv], exec\n\t"
-        "s_mov_b64 exec, 1\n\t"
+        "s_mov_b64 exec, %[m]\n\t"
         "v_rsq_f64 %[y], %[d]\n\t"
         "s_nop 1\n\t"
         "v_mul_f64 %[t], %[d], %[y]\n\t"
@@ -727,8 +814,8 @@ __device__ __forceinline__ double rsq_uniform(double d)
         "v_fma_f64 %[y], %[t], %[e], %[y]\n\t"
         "s_mov_b64 exec, %[sv]"
         : [y] "=&v"(y), [t] "=&v"(t), [e] "=&v"(e), [sv] "=&s"(sv)
-        : [d] "s"(d), [c] "s"(c38));
-    return readlane_f64(y, 0);   // lane 0 computed it, whatever EXEC was around the call
+        : [d] "s"(d), [c] "s"(c38), [m] "s"(ex & (0 - ex)));
+    return readlane_f64(y, l0);   // the lane that computed it
 }
 
 // A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
@@ -1041,6 +1128,8 @@ __device__ __forceinline__ void keep_where(bool sel, double2 &a, double2 c)
 #endif
 // rsel[lane L] = rs (wave-uniform, in SGPRs): one v_mov_b64 under EXEC = lane L
 // instead of v_cmp + two v_cndmask per step.  L is a constant after unrolling.
+// The mask is ANDed with the incoming EXEC (formed outside the asm, which
+// writes no SCC), so a lane switched off around the call is never written.
 __device__ __forceinline__ void keep_rsel_lane(double &rsel, int L, double rs)
 {
     if (!WCE_KEEP_EXEC) {
@@ -1053,9 +1142,9 @@ __device__ __forceinline__ void keep_rsel_lane(double &rsel, int L, double rs)
                  "v_mov_b64 %[r], %[v]\n\t"
                  "s_mov_b64 exec, %[sv]"
                  : [r] "+v"(rsel), [sv] "=&s"(sv)
-                 : [m] "s"(1ull << L), [v] "s"(rs));
+                 : [m] "s"((1ull << L) & __builtin_amdgcn_read_exec()), [v] "s"(rs));
 }
-// a = c on the lanes of mask m (a constant): two v_mov_b64 under EXEC
+// a = c on the lanes of mask m (a constant) that are active: two v_mov_b64 under EXEC
 __device__ __forceinline__ void keep_where_mask(uint64_t m, bool sel, double2 &a, double2 c)
 {
     if (!WCE_KEEP_EXEC) {
@@ -1069,7 +1158,7 @@ __device__ __forceinline__ void keep_where_mask(uint64_t m, bool sel, double2 &a
                  "v_mov_b64 %[ay], %[cy]\n\t"
                  "s_mov_b64 exec, %[sv]"
                  : [ax] "+v"(a.x), [ay] "+v"(a.y), [sv] "=&s"(sv)
-                 : [m] "s"(m), [cx] "v"(c.x), [cy] "v"(c.y));
+                 : [m] "s"(m & __builtin_amdgcn_read_exec()), [cx] "v"(c.x), [cy] "v"(c.y));
 }
 constexpr uint64_t lanes_q(int qq) { return 0x0101010101010101ull << qq; }   // lanes with q == qq
 
@@ -1204,27 +1293,49 @@ __device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s
     }
 }
 
+template <int KB>
+__device__ __forceinline__ void chol_panels_keep(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s,
+                                                 int p, int q, int lane, double &rsel)
+{
+    if constexpr (KB < RB - 1) {
+        chol_panel<KB, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+        chol_panels_keep<KB + 1>(A, P, R, s, p, q, lane, rsel);
+    }
+}
+
 // The dense-C factorisation (WCE_DENSE_CHOL): the headline's row-per-lane
 // Cholesky panels on Ryy bordered by conj(rx) (row 53), keeping L in the
 // block-cyclic registers for the back-substitution; s.rd = 1/sqrt(d_k).
-// Entering: A built (all 28 blocks, row 53 = conj(rx)).
+// Entering: A built (block rows/columns K0..6, row 53 = the conj right-hand
+// side).  K0 > 0 (the low-rank path, mmse_lr_kernel): the system occupies
+// rows 8 K0 .. 52 only and the panels before it are skipped.
+template <int K0 = 0>
 __device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane)
 {
-    double2 P[8];
-    to_rows<0>(A, P, s, p, q, lane);
-    const double r0 = rsq_nr(readlane_f64(P[0].x, 0));
-    double rsel = lane == 0 ? r0 : 0.0;
-    P[0] = cscale(P[0], r0);
-    wave_lds_sync();   // conv reads done before the publish (s.u is separate; order only)
-    s.u[0][lane] = P[0];
-    wave_lds_sync();
-    double2 R = WCE_DPP_PANEL ? s.u[0][lane & 7] : make_double2(0.0, 0.0);
-    chol_panel<0, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<1, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<2, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<3, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<4, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
-    chol_panel<5, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+    double rsel = 0.0;
+    if constexpr (K0 < RB - 1) {
+        double2 P[8];
+        to_rows<K0>(A, P, s, p, q, lane);
+        if constexpr (K0 > 0) {   // rows above the system: defined values (updated, never read)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) keep_where(lane < 8 * K0, P[c], make_double2(0.0, 0.0));
+        }
+        const double r0 = rsq_nr(readlane_f64(P[0].x, 8 * K0));
+        rsel = lane == 8 * K0 ? r0 : 0.0;
+        P[0] = cscale(P[0], r0);
+        wave_lds_sync();   // conv reads done before the publish (s.u is separate; order only)
+        s.u[0][lane] = P[0];
+        wave_lds_sync();
+        double2 R = WCE_DPP_PANEL ? s.u[0][8 * K0 + (lane & 7)] : make_double2(0.0, 0.0);
+        chol_panels_keep<K0>(A, P, R, s, p, q, lane, rsel);
+    } else {   // the system is block (6, 6) alone: pivot 48 opens the block-cyclic last panel
+        const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 0));
+        const double2 cs = cscale(A[RB - 1][RB - 1], rs);
+        if (q == 0) s.u[0][p + 8 * (RB - 1)] = cs;
+        keep_rsel_lane(rsel, 8 * (RB - 1), rs);
+        keep_where_mask(lanes_q(0), q == 0, A[RB - 1][RB - 1], cs);
+        wave_lds_sync();
+    }
     chol_last_keep(A, s, p, q, lane, rsel);
     wave_lds_sync();
     s.rd[lane] = lane < NSC ? rsel : 0.0;   // conv is dead: rd and z share its LDS
@@ -1538,6 +1649,206 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
     if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, w);
 }
 
+// =====================================================================
+// WCE_MMSE_COV, low-rank path (round 3).  C = U U^H with U = F V_r
+// sqrt(Lambda_r) (State::U, r columns, from the 80-bit eigendecomposition of
+// Rhh in wce_state.cpp).  With G = X U (53 x r):
+//     H = C X Ryy^-1 rx = U s,   s = U^H X Ryy^-1 rx,   Ryy = a G G^H + b I,
+// and by the push-through identity G^H (a G G^H + b I)^-1 = (a G^H G + b I)^-1 G^H
+//     s = t = (a G^H G + b I_r)^-1 G^H rx                      (real x),
+// while for complex x (U^H X = U^H X^H + U^H (X - X^H), b Ryy^-1 rx = rx - a G t)
+//     s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b.
+// The dense form (mmse_solve_kernel: z = Ryy^-1 rx, then C X z) carries the
+// components of z along C's null space, of size |rx|/b, which C X must
+// cancel: it loses ~eps cond(Ryy) on a rank-deficient C, 1e-10..1e-9 here
+// (DESIGN.md s2).  This form never creates them: the error stays at the
+// 1e-13 level for every rank (profiles/r03_cov_rank_probe.txt).
+//
+// The r x r Gram system reuses the dense solve's machinery: it is embedded
+// in the block-cyclic registers at block row K0 = (53 - r) / 8 (rows 8 K0 ..
+// 8 K0 + r - 1; rows up to 52 past r get Gram entries 0, i.e. pivot b and a
+// zero right-hand side, so t_j = 0 there), bordered by conj(G^H rx) in row 53
+// exactly where the dense solve keeps conj(rx); the panels before K0 and
+// their back-substitution blocks are skipped.  G^H G and the border row come
+// from v_mfma_f64_16x16x4 tiles of G~ = [X U | rx] (the border is the Gram
+// column j = 53 - 8 K0 of G~), staged through LDS into the register blocks.
+// =====================================================================
+#ifndef WCE_LR_WAVES_PER_SIMD   // K0 >= 2 (<= 122 VGPRs); 12 KB of LDS per wave caps a CU at 13 waves anyway
+#define WCE_LR_WAVES_PER_SIMD 4
+#endif
+// Gram column j of G~ at subcarrier k: x_k U[k][j] (U is zero past column
+// r - 1), rx_k at the border column j = 53 - 8 K0, 0 past it.
+template <int K0>
+__device__ __forceinline__ double2 lr_gcol(const State *__restrict__ st, const SolveLds &s, int k, int j)
+{
+    constexpr int RMAX = NSC - 8 * K0;
+    const double2 g = cmul(s.x[k], ld2(st->U, k * CLD + j));   // k, j < 64 (U zero-padded)
+    const double2 r = j == RMAX ? s.rx[k] : make_double2(0.0, 0.0);
+    return j < RMAX ? g : r;
+}
+
+constexpr int LR_TS = 17;   // row stride (complex) of a staged 16 x 16 Gram tile: conflict-free block reads
+
+// Gram tile (I, J) = rows 16 I .. 16 I + 15 x columns 16 J .. of G~^H G~,
+// then into the register blocks it covers: A = a Gamma + b I on rows < 53,
+// the border row 53 (conj(G^H rx)) and rows 54, 55 (0) as they are.
+template <int K0, int I, int J>
+__device__ __forceinline__ void lr_tile(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB], int lane,
+                                        int p, int q, double ac, double bc)
+{
+    const int ml = lane & 15, kl = lane >> 4;
+    v4d gr = {0, 0, 0, 0}, gi = {0, 0, 0, 0};
+#pragma unroll 2   // (fully unrolled, the 14 steps' operand loads are all hoisted: spills at K0 = 0)
+    for (int t = 0; t < KSTEPS; ++t) {
+        const int k = 4 * t + kl;
+        const double2 ga = lr_gcol<K0>(st, s, k, 16 * I + ml);
+        const double2 gb = (I == J) ? ga : lr_gcol<K0>(st, s, k, 16 * J + ml);
+        // conj(ga) gb = (ga.x gb.x + ga.y gb.y) + i (ga.x gb.y - ga.y gb.x)
+        gr = __builtin_amdgcn_mfma_f64_16x16x4f64(ga.x, gb.x, gr, 0, 0, 0);
+        gr = __builtin_amdgcn_mfma_f64_16x16x4f64(ga.y, gb.y, gr, 0, 0, 0);
+        gi = __builtin_amdgcn_mfma_f64_16x16x4f64(ga.x, gb.y, gi, 0, 0, 0);
+        gi = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga.y, gb.x, gi, 0, 0, 0);
+    }
+    double2 *T = s.conv;   // D[m = kl + 4 r][n = ml]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[(kl + 4 * r) * LR_TS + ml] = make_double2(gr[r], gi[r]);
+    wave_lds_sync();
+#pragma unroll
+    for (int da = 0; da < 2; ++da)
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+            const int aa = K0 + 2 * I + da, bb = K0 + 2 * J + db;   // constants after unrolling
+            if (aa < RB && bb <= aa) {
+                const int ai = aa < RB ? aa : RB - 1, bi = bb < RB ? bb : RB - 1;
+                const double2 v = T[(p + 8 * da) * LR_TS + q + 8 * db];
+                const bool gram = p + 8 * aa < NSC;
+                double2 e = cscale(v, ac);
+                e.x += (gram && aa == bb && p == q) ? bc : 0.0;
+                A[ai][bi] = make_double2(gram ? e.x : v.x, gram ? e.y : v.y);
+            }
+        }
+    wave_lds_sync();   // the next tile rewrites T
+}
+template <int K0, int I, int J>
+__device__ __forceinline__ void lr_gram(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB], int lane,
+                                        int p, int q, double ac, double bc)
+{
+    constexpr int NT = (8 * (RB - K0) + 15) / 16;   // tiles per side over block rows K0..6
+    if constexpr (I < NT) {
+        lr_tile<K0, I, J>(st, s, A, lane, p, q, ac, bc);
+        if constexpr (J < I) lr_gram<K0, I, J + 1>(st, s, A, lane, p, q, ac, bc);
+        else lr_gram<K0, I + 1, 0>(st, s, A, lane, p, q, ac, bc);
+    }
+}
+template <int BLK, int K0>
+__device__ __forceinline__ void back_blocks_from(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
+                                                 SolveLds &s, int p, int q, int lane)
+{
+    if constexpr (BLK >= K0) {
+        back_block<BLK>(A, P, rq, s, p, q, lane);
+        back_blocks_from<BLK - 1, K0>(A, P, rq, s, p, q, lane);
+    }
+}
+
+// One (frame, block): returns H_k on lane k (k < 53).
+template <int K0>
+__device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const SolveArgs &a, SolveLds &s, int64_t base)
+{
+    constexpr int RMAX = NSC - 8 * K0;
+    const int lane = threadIdx.x;
+    const int p = lane >> 3, q = lane & 7;
+    const bool act = lane < NSC;
+    const double ac = st->acoef, bc = st->bcoef;
+    double2 xl;
+    {
+        const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
+        const double2 r = act ? ld2(a.rx, base + lane) : make_double2(0, 0);
+        const bool inx = act && ((st->xmask >> lane) & 1ull);
+        xl = inx ? t : make_double2(0, 0);
+        s.x[lane] = xl;
+        s.rx[lane] = r;
+    }
+    wave_lds_sync();
+    double2 A[RB][RB];
+#pragma unroll
+    for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+        for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
+    lr_gram<K0, 0, 0>(st, s, A, lane, p, q, ac, bc);
+    dense_chol<K0>(A, s, p, q, lane);
+    double rq[RB];
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) rq[bb] = s.rd[q + 8 * bb];
+    double2 P[RB];
+    const bool brow = (p == NSC - 8 * (RB - 1));
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) P[bb] = brow ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
+    back_blocks_from<RB - 1, K0>(A, P, rq, s, p, q, lane);
+    wave_lds_sync();
+    // t_j = z[8 K0 + j]; y = U t on lane k (UT rows: coalesced)
+    const int r = min(st->cov_rank, RMAX);
+    const int kk = act ? lane : 0;
+    double2 y = make_double2(0.0, 0.0);
+#pragma unroll 4
+    for (int j = 0; j < r; ++j) {
+        const double2 u = ld2(st->UT, j * CLD + kk), t = s.z[8 * K0 + j];
+        y.x = fma(u.x, t.x, fma(-u.y, t.y, y.x));
+        y.y = fma(u.x, t.y, fma(u.y, t.x, y.y));
+    }
+    if (__ballot(act && xl.y != 0.0) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o rho] / b
+        const double2 rho = csub(s.rx[lane], cscale(cmul(xl, y), ac));   // b Ryy^-1 rx
+        s.blk[lane] = act ? make_double2(-2.0 * xl.y * rho.y, 2.0 * xl.y * rho.x) : make_double2(0, 0);
+        wave_lds_sync();
+        double2 c = make_double2(0.0, 0.0);   // lane j: c_j = sum_k conj(U[k][j]) v_k
+        const int jj = lane < r ? lane : 0;
+#pragma unroll 4
+        for (int k = 0; k < NSC; ++k) {
+            const double2 u = ld2(st->U, k * CLD + jj), v = s.blk[k];
+            c.x = fma(u.x, v.x, fma(u.y, v.y, c.x));
+            c.y = fma(u.x, v.y, fma(-u.y, v.x, c.y));
+        }
+        s.u[1][lane] = cscale(c, 1.0 / bc);
+        wave_lds_sync();
+#pragma unroll 4
+        for (int j = 0; j < r; ++j) {
+            const double2 u = ld2(st->UT, j * CLD + kk), t = s.u[1][j];
+            y.x = fma(u.x, t.x, fma(-u.y, t.y, y.x));
+            y.y = fma(u.x, t.y, fma(u.y, t.x, y.y));
+        }
+    }
+    return y;
+}
+
+// split (MATLAB averaging): one wave per (frame, block) writes H_b to row g
+// of a.w; avg_blocks_kernel forms the mean.
+// K0 = 0 (r > 45: a Gram system as large as Ryy itself) holds all 28
+// register blocks through the MFMA build: 181 VGPRs, 2 waves/SIMD; K0 = 1: 156
+constexpr int lr_waves(int k0) { return k0 == 0 ? 2 : (k0 == 1 ? 3 : WCE_LR_WAVES_PER_SIMD); }
+template <int K0>
+__global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    __shared__ SolveLds s;
+    const int64_t g = blockIdx.x;
+    const int64_t f = a.split ? g / a.nblk : g;
+    const int b = a.split ? (int)(g - f * a.nblk) : 0;
+    if (f >= a.n) return;
+    const double2 h = lr_solve<K0>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs);
+    if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, h);
+}
+
+// H[f] = (((X[4f] + X[4f+1]) + X[4f+2]) + X[4f+3]) / 4  (WiFi_channel_estimation_PS_MMSE.m:35)
+__global__ __launch_bounds__(256) void avg_blocks_kernel(const double *__restrict__ X, int64_t xs, double *H, int64_t hs,
+                                                         int64_t n)
+{
+    const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int k = threadIdx.x & 63;
+    if (f >= n || k >= NSC) return;
+    double2 acc = ld2(X, (4 * f) * xs + k);
+#pragma unroll
+    for (int b = 1; b < 4; ++b) acc = cadd(acc, ld2(X, (4 * f + b) * xs + k));
+    st2(H, f * hs + k, cscale(acc, 0.25));
+}
+
 // Config 5 fused: the MMSE solve of one frame, then -- with the wave's
 // registers free -- that frame's LS family and equalization from the same
 // resident data (pilots from LDS, rx blocks streamed).  The HBM traffic of the
@@ -1617,8 +1928,6 @@ __global__ __launch_bounds__(256) void fc_finish_kernel(SolveArgs a, const doubl
 // subcarrier i; complex = 4 real MFMAs.  W may alias H: every W fragment of a
 // tile is loaded before the first store of that tile.
 // =====================================================================
-typedef double v4d __attribute__((ext_vector_type(4)));
-constexpr int KSTEPS = 14;   // 56 >= 53
 constexpr int APPLY_WAVES = 4;
 
 // Y1[f] = M1 X[f] (and Y2[f] = M2 X[f]) for 16-frame tiles; M padded 64 x 64.
@@ -1805,14 +2114,21 @@ static inline int variant(int which) { return __atomic_load_n(&g_variant[which],
 
 // blocks of 4 waves for a tile kernel: one wave per tile up to the device's
 // resident-wave budget (CUs x waves per CU), grid-stride past it
+// CU count of the CURRENT device (callers hold a DeviceGuard for the ctx's
+// device), cached per device index: one process may drive several GPUs from
+// several threads, so the cache is an array of atomics, not one static int.
 static int cu_count()
 {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            cus = n;
-        if (cus <= 0) cus = 256;
+    constexpr int kMaxDev = 64;
+    static int cache[kMaxDev] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    int *slot = dev < kMaxDev ? &cache[dev] : nullptr;
+    int cus = slot ? __atomic_load_n(slot, __ATOMIC_RELAXED) : 0;
+    if (cus <= 0) {
+        int n = 0;
+        cus = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+        if (slot) __atomic_store_n(slot, cus, __ATOMIC_RELAXED);
     }
     return cus;
 }
@@ -1894,6 +2210,35 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     return hip_status(hipGetLastError());
 }
 
+int launch_mmse_lr(const State *st, int k0, const SolveArgs &a, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    const int64_t waves = a.split ? a.n * a.nblk : a.n;
+    if (waves > 0x7fffffffll) return WCE_EINVAL;
+    if (a.nblk > 1 && !a.split) return WCE_EINVAL;
+    const dim3 g((unsigned)waves), b(64);
+    hipStream_t s = (hipStream_t)stream;
+    switch (k0) {
+    case 0: hipLaunchKernelGGL(mmse_lr_kernel<0>, g, b, 0, s, st, a); break;
+    case 1: hipLaunchKernelGGL(mmse_lr_kernel<1>, g, b, 0, s, st, a); break;
+    case 2: hipLaunchKernelGGL(mmse_lr_kernel<2>, g, b, 0, s, st, a); break;
+    case 3: hipLaunchKernelGGL(mmse_lr_kernel<3>, g, b, 0, s, st, a); break;
+    case 4: hipLaunchKernelGGL(mmse_lr_kernel<4>, g, b, 0, s, st, a); break;
+    case 5: hipLaunchKernelGGL(mmse_lr_kernel<5>, g, b, 0, s, st, a); break;
+    case 6: hipLaunchKernelGGL(mmse_lr_kernel<6>, g, b, 0, s, st, a); break;
+    default: return WCE_EINVAL;
+    }
+    return hip_status(hipGetLastError());
+}
+
+int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream)
+{
+    if (n <= 0) return WCE_OK;
+    hipLaunchKernelGGL(avg_blocks_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, X, xs, H,
+                       hs, n);
+    return hip_status(hipGetLastError());
+}
+
 int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
@@ -1902,6 +2247,9 @@ int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t 
     return hip_status(hipGetLastError());
 }
 
+#ifndef WCE_REF_LS_FLAT   // A/B: 0 = REF + LS requests ride in mmse_solve_ls_kernel (one wave per frame)
+#define WCE_REF_LS_FLAT 1
+#endif
 int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
@@ -1909,6 +2257,15 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
     const dim3 g((unsigned)a.n), b(64);
     hipStream_t s = (hipStream_t)stream;
     const bool eq = (l.mask & WCE_EQUALIZE) && l.eq;
+    if (WCE_REF_LS_FLAT && a.ref_pilots && a.hout && !a.split && variant(WCE_VARIANT_REF_LS) == 0) {
+        for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {   // 53 * frames < 2^32 per launch
+            const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
+            const dim3 gb((unsigned)((nf * NSC + 255) / 256));
+            if (eq) hipLaunchKernelGGL(ref_ls_elem_kernel<true>, gb, dim3(256), 0, s, st, a, l, f0, (uint32_t)nf);
+            else hipLaunchKernelGGL(ref_ls_elem_kernel<false>, gb, dim3(256), 0, s, st, a, l, f0, (uint32_t)nf);
+        }
+        return hip_status(hipGetLastError());
+    }
 #define WCE_LAUNCH_SLS(R1, HOUT)                                                                        \
     do {                                                                                                \
         if (eq) hipLaunchKernelGGL((mmse_solve_ls_kernel<R1, HOUT, true>), g, b, 0, s, st, a, l);       \

@@ -16,6 +16,7 @@
 //   sinc table   main.c:135-143 + utils.c:727-733
 #include "wce_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -156,6 +157,7 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
 {
     if (mode != WCE_MMSE_REF && mode != WCE_MMSE_TEXTBOOK) return WCE_EINVAL;
     std::memset(st, 0, sizeof(State));
+    st->cov_k0 = -1;
     const int n = NSC;
     std::vector<cld> F(n * n), C(n * n);
     for (int i = 0; i < n * n; i++) F[i] = from(Fl[i]);
@@ -309,14 +311,129 @@ extern "C" int wce_debug_build_state(const double *tx_pre, const double *rx_pre,
 extern "C" size_t wce_state_size(void) { return sizeof(wce::State); }
 
 namespace wce {
+// Eigendecomposition of a Hermitian n x n matrix (row-major {re, im} long
+// double) by cyclic complex Jacobi rotations in 80-bit arithmetic: on return
+// lam[j] are the eigenvalues and column j of V (row-major) the eigenvector,
+// A = V diag(lam) V^H.  A diagonal input takes no rotation, so its eigenvalues
+// (a power-delay profile's exact zeros included) come back exactly.
+void host_hermitian_eig(const ldc *Ain, int n, long double *lam, ldc *V)
+{
+    std::vector<long double> ar(n * n), ai(n * n), vr(n * n, 0.0L), vi(n * n, 0.0L);
+    for (int i = 0; i < n * n; i++) { ar[i] = Ain[i].re; ai[i] = Ain[i].im; }
+    for (int i = 0; i < n; i++) { ai[i * n + i] = 0.0L; vr[i * n + i] = 1.0L; }
+    long double fro = 0.0L;
+    for (int i = 0; i < n * n; i++) fro += ar[i] * ar[i] + ai[i] * ai[i];
+    for (int sweep = 0; sweep < 60; sweep++) {
+        long double off = 0.0L;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) off += ar[p * n + q] * ar[p * n + q] + ai[p * n + q] * ai[p * n + q];
+        if (off <= fro * 1e-37L || off == 0.0L) break;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) {
+                const long double br = ar[p * n + q], bi = ai[p * n + q];
+                const long double m = hypotl(br, bi);
+                if (m == 0.0L) continue;
+                // D = diag(1, e^{-i phi}) makes A_pq = m real, then a real rotation R:
+                // G = D R = [[c, s], [-s e^{-i phi}, c e^{-i phi}]],  e^{i phi} = b / m
+                const long double er = br / m, ei = bi / m;
+                const long double app = ar[p * n + p], aqq = ar[q * n + q];
+                const long double tau = (aqq - app) / (2.0L * m);
+                const long double t = (tau >= 0 ? 1.0L : -1.0L) / (fabsl(tau) + sqrtl(1.0L + tau * tau));
+                const long double c = 1.0L / sqrtl(1.0L + t * t), s = t * c;
+                // G entries: gpp = c, gpq = s, gqp = -s conj(e), gqq = c conj(e)
+                const long double gqpr = -s * er, gqpi = s * ei, gqqr = c * er, gqqi = -c * ei;
+                for (int k = 0; k < n; k++) {   // columns: A[:, p], A[:, q] <- A G
+                    const long double xr = ar[k * n + p], xi = ai[k * n + p], yr = ar[k * n + q], yi = ai[k * n + q];
+                    ar[k * n + p] = c * xr + (yr * gqpr - yi * gqpi);
+                    ai[k * n + p] = c * xi + (yr * gqpi + yi * gqpr);
+                    ar[k * n + q] = s * xr + (yr * gqqr - yi * gqqi);
+                    ai[k * n + q] = s * xi + (yr * gqqi + yi * gqqr);
+                    const long double ur = vr[k * n + p], ui = vi[k * n + p], wr = vr[k * n + q], wi = vi[k * n + q];
+                    vr[k * n + p] = c * ur + (wr * gqpr - wi * gqpi);
+                    vi[k * n + p] = c * ui + (wr * gqpi + wi * gqpr);
+                    vr[k * n + q] = s * ur + (wr * gqqr - wi * gqqi);
+                    vi[k * n + q] = s * ui + (wr * gqqi + wi * gqqr);
+                }
+                for (int k = 0; k < n; k++) {   // rows: A[p, :], A[q, :] <- G^H A
+                    const long double xr = ar[p * n + k], xi = ai[p * n + k], yr = ar[q * n + k], yi = ai[q * n + k];
+                    ar[p * n + k] = c * xr + (gqpr * yr + gqpi * yi);
+                    ai[p * n + k] = c * xi + (gqpr * yi - gqpi * yr);
+                    ar[q * n + k] = s * xr + (gqqr * yr + gqqi * yi);
+                    ai[q * n + k] = s * xi + (gqqr * yi - gqqi * yr);
+                }
+                ar[p * n + q] = ai[p * n + q] = ar[q * n + p] = ai[q * n + p] = 0.0L;
+                ai[p * n + p] = ai[q * n + q] = 0.0L;
+            }
+    }
+    for (int j = 0; j < n; j++) lam[j] = ar[j * n + j];
+    for (int i = 0; i < n * n; i++) { V[i].re = vr[i]; V[i].im = vi[i]; }
+}
+
+// Eigenvalues of Rhh at or below this fraction of the largest are rounding
+// noise of an fp64 input (a rank-r matrix formed in double carries ~n eps
+// lambda_max in its null space) and are dropped from the factor U.
+constexpr long double kCovRankTol = 1.0L / (1ull << 46);
+// A full-rank C whose spectrum spans more than this keeps the low-rank (Gram)
+// path: the dense Ryy solve loses ~eps cond(Ryy) there.
+constexpr long double kCovDenseKappa = 1e5L;
+
 // WCE_MMSE_COV: the TEXTBOOK state with C = F Rhh F' from a caller's Rhh (80-bit products)
 int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
 {
     const int n = NSC;
     std::vector<cld> F(n * n), R(n * n), t1(n * n), C(n * n), FH(n * n);
+    // Rhh must be finite and Hermitian (to 1e-12 of its largest entry) ...
+    long double amax = 0.0L;
+    for (int i = 0; i < n * n; i++) {
+        if (!std::isfinite(Rhh[i].re) || !std::isfinite(Rhh[i].im)) return WCE_EINVAL;
+        amax = std::max(amax, (long double)std::max(std::fabs(Rhh[i].re), std::fabs(Rhh[i].im)));
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) {
+            const long double dr = (long double)Rhh[i * n + j].re - Rhh[j * n + i].re;
+            const long double di = (long double)Rhh[i * n + j].im + Rhh[j * n + i].im;
+            if (fabsl(dr) > 1e-12L * amax || fabsl(di) > 1e-12L * amax) return WCE_EINVAL;
+        }
     for (int i = 0; i < n * n; i++) {
         F[i] = from(Fl[i]);
         R[i] = mk((long double)Rhh[i].re, (long double)Rhh[i].im);
+    }
+    {   // ... and positive semidefinite: its Hermitian part's eigenvalues >= -1e-12 lambda_max
+        std::vector<ldc> Rh(n * n), V(n * n);
+        std::vector<long double> lam(n);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                Rh[i * n + j].re = 0.5L * ((long double)Rhh[i * n + j].re + Rhh[j * n + i].re);
+                Rh[i * n + j].im = 0.5L * ((long double)Rhh[i * n + j].im - Rhh[j * n + i].im);
+            }
+        host_hermitian_eig(Rh.data(), n, lam.data(), V.data());
+        long double lmax = 0.0L, lmin = 0.0L;
+        for (int j = 0; j < n; j++) { lmax = std::max(lmax, lam[j]); lmin = std::min(lmin, lam[j]); }
+        if (lmin < -1e-12L * lmax || (lmax == 0.0L && lmin < 0.0L)) return WCE_EINVAL;
+        // C = F Rhh F^H = U U^H, U = F V_r sqrt(Lambda_r), eigen-directions in
+        // descending order; the eigenvalues of C are 53 lambda (F^H F = 53 I)
+        std::vector<int> ord(n);
+        for (int j = 0; j < n; j++) ord[j] = j;
+        std::sort(ord.begin(), ord.end(), [&](int x, int y) { return lam[x] > lam[y]; });
+        int r = 0;
+        while (r < n && lam[ord[r]] > kCovRankTol * lmax && lmax > 0.0L) r++;
+        std::memset(st->U, 0, sizeof(st->U));
+        std::memset(st->UT, 0, sizeof(st->UT));
+        for (int j = 0; j < r; j++) {
+            const long double sl = sqrtl(lam[ord[j]]);
+            for (int k = 0; k < n; k++) {
+                cld u = mk(0, 0);
+                for (int t = 0; t < n; t++) u = u + F[k * n + t] * from(V[t * n + ord[j]]);
+                u = u * mk(sl, 0.0L);
+                st->U[2 * (k * CLD + j)] = st->UT[2 * (j * CLD + k)] = (double)__real__ u;
+                st->U[2 * (k * CLD + j) + 1] = st->UT[2 * (j * CLD + k) + 1] = (double)__imag__ u;
+            }
+        }
+        st->cov_rank = r;
+        st->cov_lmax = (double)(n * lmax);
+        st->cov_lmin = r ? (double)(n * lam[ord[r - 1]]) : 0.0;
+        const bool dense = r == n && lam[ord[0]] <= kCovDenseKappa * lam[ord[r - 1]];
+        st->cov_k0 = dense ? -1 : std::min((n - r) / 8, COV_K0_MAX);
     }
     for (int r = 0; r < n; r++)
         for (int c = 0; c < n; c++) {
@@ -359,4 +476,34 @@ extern "C" int wce_state_build(void *out, size_t bytes, const wce_complex *tx_pr
     host_lt_ls(txl, rxl, hlt);
     return host_build_state(static_cast<State *>(out), host_reference_F(), host_reference_invF(), hlt, txl, ow2,
                             mode);
+}
+
+// Host-only view of a WCE_MMSE_COV state blob (tests): the factor U (53 rows x
+// 64 columns {re, im}, zero past the rank), rank, solve form (cov_k0) and the
+// kept spectrum of C.
+extern "C" int wce_debug_cov_factor(const void *blob, size_t bytes, double *U, int *rank, int *k0, double *lmax,
+                                    double *lmin)
+{
+    using namespace wce;
+    if (!blob || bytes < sizeof(State)) return WCE_EINVAL;
+    const State *st = static_cast<const State *>(blob);
+    if (st->magic != STATE_MAGIC || st->mode != WCE_MMSE_COV) return WCE_EINVAL;
+    if (U) std::memcpy(U, st->U, sizeof(double) * 2 * NSC * CLD);
+    if (rank) *rank = st->cov_rank;
+    if (k0) *k0 = st->cov_k0;
+    if (lmax) *lmax = st->cov_lmax;
+    if (lmin) *lmin = st->cov_lmin;
+    return WCE_OK;
+}
+
+// Host-side check of a state blob (e.g. bytes received from another rank):
+// WCE_OK and its MMSE mode if it carries a valid state.
+extern "C" int wce_state_validate(const void *blob, size_t bytes, int *mode)
+{
+    using namespace wce;
+    if (!blob || bytes < sizeof(State)) return WCE_EINVAL;
+    const State *st = static_cast<const State *>(blob);
+    if (st->magic != STATE_MAGIC) return WCE_ESTATE;
+    if (mode) *mode = st->mode;
+    return WCE_OK;
 }

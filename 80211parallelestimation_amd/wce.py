@@ -100,11 +100,16 @@ ABI = {
     "wce_debug_set_border_dot": [c_void_p, c_int],
     "wce_debug_set_flat_chunk": [ctypes.c_int64],
     "wce_debug_set_variant": [c_int, c_int],
+    "wce_debug_set_cov_path": [c_void_p, c_int],
+    "wce_debug_cov_factor": [c_void_p, c_size_t, c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_double),
+                             POINTER(c_double)],
+    "wce_ctx_cov_info": [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_double), POINTER(c_double)],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
     "wce_state_build": [c_void_p, c_size_t, c_void_p, c_void_p, c_double, c_int],
     "wce_ctx_load_state": [c_void_p, c_void_p, c_size_t],
+    "wce_state_validate": [c_void_p, c_size_t, POINTER(c_int)],
     "wce_ctx_get_shared": [c_void_p, c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)],
     "wce_estimate": [c_void_p, POINTER(Frames), POINTER(Outputs), c_uint32, c_void_p],
     "wce_mmse_solve": [c_void_p, POINTER(Frames), c_void_p, c_int64, c_void_p],
@@ -320,6 +325,18 @@ class Context:
         """Capture one estimate call into a HIP graph (wce_plan_create)."""
         return Plan(self, frames, outputs, mask)
 
+    def cov_info(self):
+        """WCE_MMSE_COV: (rank r, low-rank path taken, lambda_max, lambda_min of the kept spectrum of C)."""
+        r, lr = c_int(), c_int()
+        lmax, lmin = c_double(), c_double()
+        _check(load().wce_ctx_cov_info(self.handle, ctypes.byref(r), ctypes.byref(lr), ctypes.byref(lmax),
+                                       ctypes.byref(lmin)), "cov_info")
+        return r.value, bool(lr.value), lmax.value, lmin.value
+
+    def set_cov_path(self, path: int):
+        """A/B: 0 = the state's choice, 1 = dense Ryy solve, 2 = low-rank Gram path."""
+        _check(load().wce_debug_set_cov_path(self.handle, path), "set_cov_path")
+
     def set_border_dot(self, on: bool):
         """A/B switch: rank-1 covariance via a second bordered row (default on)."""
         _check(_lib.wce_debug_set_border_dot(self.handle, int(bool(on))), "wce_debug_set_border_dot")
@@ -503,6 +520,24 @@ def state_blob(tx_pre, rx_pre, ow2, mode=MMSE_REF, Rhh=None) -> np.ndarray:
     _check(lib.wce_state_build(blob.ctypes.data_as(c_void_p), n, tp.ctypes.data_as(c_void_p),
                                rp.ctypes.data_as(c_void_p), float(ow2), mode), "wce_state_build")
     return blob
+
+
+def state_mode(blob: np.ndarray) -> int:
+    """The MMSE mode of a valid state blob (wce_state_validate); raises if the bytes hold no state."""
+    m = c_int()
+    _check(load().wce_state_validate(blob.ctypes.data_as(c_void_p), blob.nbytes, byref(m)), "wce_state_validate")
+    return m.value
+
+
+def cov_factor(blob: np.ndarray):
+    """A WCE_MMSE_COV state blob's low-rank factor: (U [53 x rank] with C = U U^H, rank, k0, lambda_max,
+    lambda_min); k0 = -1 when the dense Ryy solve runs, else the Gram system's first block row."""
+    U = np.zeros((NSC, 64), np.complex128)
+    r, k0 = c_int(), c_int()
+    lmax, lmin = c_double(), c_double()
+    _check(load().wce_debug_cov_factor(blob.ctypes.data_as(c_void_p), blob.nbytes, U.ctypes.data_as(c_void_p),
+                                       byref(r), byref(k0), byref(lmax), byref(lmin)), "wce_debug_cov_factor")
+    return U[:, :r.value].copy(), r.value, k0.value, lmax.value, lmin.value
 
 
 def ldc_to_complex(src, dst, n, stream=None):

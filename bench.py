@@ -87,15 +87,20 @@ class Dist:
             import torch
             import torch.distributed as dist
             self.torch, self.dist = torch, dist
+            # ranks > 0 wait in the barriers of the sharded legs while rank 0 runs
+            # its single-GPU legs (minutes at N = 1's sizes): an explicit,
+            # generous process-group timeout instead of the watchdog default
+            import datetime
+            tmo = datetime.timedelta(minutes=int(os.environ.get("WCE_DIST_TIMEOUT_MIN", "30")))
             if self.backend == "nccl":
                 torch.cuda.set_device(self.local)
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), timeout=tmo)
                 # first all-reduce now, long before any timed region: the
                 # first one in a process sets RCCL up lazily
                 self.barrier()
             else:
                 self.device = self.local % max(1, torch.cuda.device_count())
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=tmo)
 
     def barrier(self):
         if self.torch is None:
@@ -112,6 +117,17 @@ class Dist:
         t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def group_check(self) -> dict:
+        """Every rank's process group must span WORLD_SIZE ranks with this
+        rank at RANK (main_mpi.c:687-688's communicator, here the RCCL one):
+        each rank checks its own view, the verdict is the min over ranks."""
+        if self.torch is None:
+            return {"backend": None, "world_size_env": self.world, "group_size": 1, "all_ranks_agree": True}
+        ok = float(self.dist.get_world_size() == self.world and self.dist.get_rank() == self.rank)
+        agree = -self.max(-ok) == 1.0      # min over ranks
+        return {"backend": self.dist.get_backend(), "world_size_env": self.world,
+                "group_size": self.dist.get_world_size(), "all_ranks_agree": bool(agree)}
 
     def broadcast_state(self, wce, ctx):
         """One broadcast of the packed shared state from rank 0 (RCCL, device
@@ -441,12 +457,17 @@ def main():
             res["front_end"] = bench_front(wce, ctx, stream, B, reps)
             res["frame_cov"] = bench_frame_cov(wce, local_ctx, stream, B, reps)
             res["config5"] = bench_config5(wce, ctx, stream, args.c5_frames, reps)
+            res["cov_lowrank"] = bench_cov_lowrank(
+                wce, lambda R: wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], device=dev, Rhh=R), stream,
+                tx, rx, B, reps)
             res["small_batch"] = bench_small_batch(wce, ctx, stream)
             res["ldc_convert"] = bench_ldc_convert(wce, stream, reps)
             # REF past the MALL: 1,048,576 full frames (27 GB), last of the rank-0 legs
             ctx_ref = local_ctx(wce.MMSE_REF)
             res.setdefault("ref_mode", {})["b%d" % args.ls_frames] = bench_ref_large(wce, ctx_ref, stream,
                                                                                    args.ls_frames, reps)
+            # BASELINE configs[4] in main.c semantics at its full 1,048,576 frames (45 GB)
+            res["config5_ref"] = bench_config5_ref(wce, ctx_ref, stream, args.ls_frames, reps)
             del ctx_ref
 
         # BASELINE configs[3]: 1,048,576 frames in total, sharded over the
@@ -465,6 +486,7 @@ def main():
         if refc is not None:
             res["cpu_baseline"]["reference_code"] = refc
 
+    res["dist_check"] = dist.group_check()
     if dist.rank == 0:
         print(json.dumps(res), flush=True)
     dist.close()
@@ -562,7 +584,8 @@ def bench_config4(wce, ctx, dist, stream, hs, steps, total=1 << 20, prewarm_s=0.
     dt = dist.max(time.perf_counter() - t0) / steps
     return {"workload": "BASELINE configs[3]: PS_MMSE over 1,048,576 frames sharded over the ranks",
             "global_frames": total, "frames_per_gpu": count, "n_gpus": dist.world, "steps": steps,
-            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong"}
+            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "frames_per_s_per_gpu": total / dt / dist.world,
+            "scaling": "strong"}
 
 
 def ls_frames(wce, ctx, n, pilots_only=False):
@@ -864,6 +887,81 @@ def bench_config5(wce, ctx, stream, n, reps):
                       "achieved_GBs": bytes_frame * n / (t * 1e-3) / 1e9}
         del outs, eq
     return res
+
+
+def bench_config5_ref(wce, ctx_ref, stream, n, reps):
+    """BASELINE configs[4] in main.c semantics (round 3): REF PS_MMSE + LT_LS /
+    PS_Linear / PS_Cubic / PS_Sinc + equalization over n frames with per-frame
+    preambles, one HBM pass (ref_ls_elem_kernel: one (frame, subcarrier)
+    element per thread).  Bytes per frame, SURVEY 8(d): rx 15x53 + tx block 0 +
+    rx_pre in, 5 H + eq out = 31,376 (fp64) / 23,320 (LS + eq stored fp32); the
+    kernel reads only tx's 4 pilots of block 0, so it moves 784 B less
+    (30,592 / 22,536: its minimum I/O, the rate quoted as `achieved`)."""
+    s = stream.handle
+    tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+    ctx_ref.synth(tx, rx, pre, n, seed=0x80211, stream=s)
+    fr = ctx_ref.frames(tx, rx, n, rx_pre=pre)
+    res = {"workload": f"BASELINE configs[4], main.c semantics: REF PS_MMSE + LT_LS + PS_Linear/Cubic/Sinc + "
+                       f"equalization, per-frame preambles, {n} frames, one HBM pass (ref_ls_elem_kernel)",
+           "frames": n}
+    for label, f32, leg in (("fp64", False, "config5_ref"), ("mixed_fp64_solve_fp32_ls", True, "config5_ref_f32")):
+        dt = np.complex64 if f32 else np.complex128
+        outs = [wce.DeviceArray((n, N), dt) for _ in range(4)] + [wce.DeviceArray((n, N))]
+        eq = wce.DeviceArray((n, NBLK, N), dt)
+        o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32 if f32 else 0)
+        f = lambda: ctx_ref.estimate(fr, o, wce.ALL, s)
+        for _ in range(3):
+            f()
+        t = time_events(wce, stream, f, reps)
+        ob = 8 if f32 else 16
+        out_b = (4 * N + NBLK * N) * ob + N * 16
+        survey = (NBLK * N + N + N) * 16 + out_b            # 31,376 / 23,320
+        minimal = (NBLK * N + N + 4) * 16 + out_b            # tx: 4 pilots
+        ach = minimal * n / (t * 1e-3) / 1e9
+        k, src = pmc_leg(leg, n, out_b * n, tol=0.05)
+        bad = sum(ctx_ref.nonfinite_scan(h, n, f32=(f32 and i < 4), stream=s)[1] for i, h in enumerate(outs))
+        bad += ctx_ref.nonfinite_scan(eq, n * NBLK, f32=f32, stream=s)[1]
+        res[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3),
+                      "roofline": {"bound": "hbm", "kernel": "ref_ls_elem_kernel", "achieved": ach,
+                                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                                   "traffic": hbm_bytes(k) if k else None, "pmc_source": src,
+                                   "bytes_per_frame": minimal, "survey_bytes_per_frame": survey,
+                                   "achieved_on_survey_bytes": survey * n / (t * 1e-3) / 1e9},
+                      "nonfinite_outputs": bad}
+        del outs, eq
+    return res
+
+
+def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
+    """WCE_MMSE_COV with a power-delay profile of L taps (rank L, the channel
+    model of SURVEY 8(d)): the low-rank Gram path (mmse_lr_kernel), which
+    meets 1e-10 where the dense Ryy solve cannot.  Per-frame
+    rate on the headline's frames, beside the dense path forced on the same
+    ctx (wce_debug_set_cov_path) for comparison."""
+    s = stream.handle
+    H = wce.DeviceArray((B, N))
+    fr = wce.Context.frames(tx, rx, B)
+    o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+    out = {"workload": f"{B} frames, PS_MMSE, Rhh = L-tap exponential PDP (rank L)"}
+    for L in (4, 8, 16, 53):
+        p = np.exp(-0.5 * np.arange(L))
+        Rhh = np.zeros((N, N), np.complex128)
+        Rhh[np.arange(L), np.arange(L)] = p / p.sum() * 1.1e-4
+        c = make_ctx(Rhh)
+        r, lr, _, _ = c.cov_info()
+        f = lambda: c.estimate(fr, o, wce.PS_MMSE, s)
+        for _ in range(2):
+            f()
+        t = time_events(wce, stream, f, reps)
+        c.set_cov_path(1)
+        for _ in range(2):
+            f()
+        td = time_events(wce, stream, f, reps)
+        out[f"L{L}"] = {"rank": r, "path": "low-rank" if lr else "dense", "ms_per_step": t,
+                        "frames_per_s": B / (t * 1e-3), "dense_forced_ms_per_step": td,
+                        "dense_forced_frames_per_s": B / (td * 1e-3)}
+        del c
+    return out
 
 
 def bench_frame_cov(wce, make_ctx, stream, n, reps):

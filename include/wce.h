@@ -94,9 +94,21 @@ int wce_ctx_destroy(wce_ctx *ctx);
 
 /* WCE_MMSE_COV: Rhh is the 53 x 53 time-domain channel covariance (row-major,
  * Hermitian positive semidefinite, host); tx_pre/rx_pre still give H_LT for
- * LT_LS and equalization. */
+ * LT_LS and equalization.  Rhh is checked: WCE_EINVAL unless every entry is
+ * finite, Rhh = Rhh^H to 1e-12 of its largest entry, and its eigenvalues are
+ * >= -1e-12 of the largest.  The 80-bit eigendecomposition Rhh = V Lambda V^H
+ * (eigenvalues at or below 2^-46 of the largest -- the rounding level of an
+ * fp64 input -- count as zero) gives C = F Rhh F^H = U U^H, U = F V sqrt(Lambda),
+ * r columns.  The per-frame solve then runs in one of two forms:
+ *   low rank (r < 53, or a spectrum wider than 1e5): the r x r Gram system
+ *     (a G^H G + b I) t = G^H rx, G = X U, and H = U s -- accurate to ~1e-13
+ *     at any rank (the dense form loses ~eps cond(Ryy) there);
+ *   dense (r = 53 and a spectrum within 1e5): Cholesky of Ryy, then H = C W on MFMA. */
 int wce_ctx_create_cov(wce_ctx **ctx, int device, const wce_complex *tx_pre, const wce_complex *rx_pre,
                        const wce_complex *Rhh, double ow2);
+/* WCE_MMSE_COV context: the rank r, whether the low-rank path runs (1) or the
+ * dense one (0), and the largest / smallest kept eigenvalue of C (outputs may be NULL). */
+int wce_ctx_cov_info(wce_ctx *ctx, int *rank, int *low_rank, double *lambda_max, double *lambda_min);
 
 /* Device pointer and size of the packed shared state (C, H_LT, tx_pre, sinc
  * table, MMSE coefficients): the single buffer a multi-GPU run broadcasts
@@ -113,6 +125,10 @@ int wce_state_build(void *host_state, size_t bytes, const wce_complex *tx_pre, c
 int wce_state_build_cov(void *host_state, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
                         const wce_complex *Rhh, double ow2);
 int wce_ctx_load_state(wce_ctx *ctx, const void *host_state, size_t bytes);
+/* Host-only check of a state blob (e.g. bytes received from another rank):
+ * WCE_OK and its MMSE mode (may be NULL) if it holds a valid state, else
+ * WCE_EINVAL (too short) / WCE_ESTATE (no valid magic). */
+int wce_state_validate(const void *host_state, size_t bytes, int *mmse_mode);
 
 /* Copy back the shared vectors (host outputs, may be NULL): H_LT (53),
  * C (53*53 row-major), and the MMSE coefficients a, b. */

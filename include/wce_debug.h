@@ -11,6 +11,11 @@ int wce_debug_reference_invF(long double *out);
 /* the State wce_ctx_create builds: C (53*53 {re,im}), H_LT (53), sinc table (4*53), {a, b}, X mask */
 int wce_debug_build_state(const double *tx_pre, const double *rx_pre, double ow2, int mode, double *C,
                           double *h_lt, double *sinc, double *ab, unsigned long long *xmask);
+/* WCE_MMSE_COV state blob (wce_state_build_cov): the low-rank factor U
+ * (C = U U^H; 53 rows x 64 columns {re, im}, zero past the rank), the rank,
+ * the solve form (-1 dense, else the Gram system's first block row) and the
+ * largest / smallest kept eigenvalue of C.  Outputs may be NULL. */
+int wce_debug_cov_factor(const void *blob, size_t bytes, double *U, int *rank, int *k0, double *lmax, double *lmin);
 /* A/B switch for the config-5 fusion (LS family + equalization in the MMSE
  * solve's epilogue); on by default.  ctx is a wce_ctx* (include/wce.h). */
 struct wce_ctx;
@@ -29,8 +34,14 @@ int wce_debug_set_flat_chunk(long long frames);
  * default; 1 = 64-frame tiles; 2 = chunks, uncapped grid).  which 1: LT_LS +
  * PS_Linear in C semantics (0 = 512-element chunks, grid capped at 2,048
  * blocks; 1 = the same uncapped; 2 = one element per thread, default).
+ * which 2: REF PS_MMSE with LS outputs in one call (0 = one element per
+ * thread, ref_ls_elem_kernel, default; 1 = the wave-per-frame fused solve).
  * Process-wide; every variant gives bit-identical results (tests check it). */
 int wce_debug_set_variant(int which, int value);
+/* WCE_MMSE_COV solve form for A/B and accuracy probes: 0 = as the state
+ * chose (default), 1 = always the dense Ryy solve, 2 = always the low-rank
+ * Gram path (at the state's rank).  ctx is a wce_ctx*. */
+int wce_debug_set_cov_path(struct wce_ctx *ctx, int path);
 #ifdef __cplusplus
 }
 #endif

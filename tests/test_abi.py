@@ -133,10 +133,14 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
     F = np.exp(-2j * np.pi * np.outer(t, t).astype(np.longdouble) / 53).astype(np.clongdouble)
     ref = (F @ R.astype(np.clongdouble) @ F.conj().T).astype(np.complex128)
     assert np.max(np.abs(C - ref)) / np.max(np.abs(ref)) < 1e-14
-    a, b, ow2 = blob[-48:-24].view(np.float64)
-    mode, magic = blob[-16:-8].view(np.int32)
+    # State tail: a, b, ow2, xmask, mode, magic, then the low-rank factor
+    # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0
+    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8)]
+    a, b, ow2 = t[-40:-16].view(np.float64)
+    mode, magic = t[-8:].view(np.int32)
     assert (a, b, ow2, mode, magic) == (1.0, inp["ow2"], inp["ow2"], wce.MMSE_COV, 0x80211)
-    assert blob[-24:-16].view(np.uint64)[0] == (1 << 53) - 1    # X = diag(tx) over all 53
+    assert t[-16:-8].view(np.uint64)[0] == (1 << 53) - 1    # X = diag(tx) over all 53
+    assert wce.state_mode(blob) == wce.MMSE_COV
 
 
 @pytest.mark.gpu

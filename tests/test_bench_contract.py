@@ -113,3 +113,28 @@ def test_config5_sharded_consistent(line):
             assert c5["nonfinite_outputs"] == 0
         assert c5["global_frames"] == 1 << 20 and c5["scaling"] == "strong"
         assert abs(c5["frames_per_s"] - c5["global_frames"] / (c5["ms_per_step"] * 1e-3)) / c5["frames_per_s"] < 1e-6
+
+
+def test_multirank_rehearsal_self_explaining():
+    """The world-2 rehearsal of the N>1 line (gloo, two ranks on one GPU box:
+    the driver's torch.distributed.run launch with WCE_DIST_BACKEND=gloo)
+    carries the fields an N=8 reader needs: every rank's process group spans
+    WORLD_SIZE (dist_check, min over ranks) and configs[3]'s strong-scaling
+    rate per GPU beside its whole-job rate."""
+    lines = [ln for ln in open(_latest("r*_bench_2rank_gloo_rehearsal.json")) if ln.startswith("{")]
+    reh = json.loads(lines[-1])      # the rank-0 JSON line (gloo prints its own chatter first)
+    assert reh["n_gpus"] == 2
+    dc = reh.get("dist_check")
+    if dc is None:
+        pytest.skip("rehearsal predates dist_check (round < 3)")
+    assert dc["all_ranks_agree"] is True and dc["group_size"] == 2 == dc["world_size_env"]
+    c4 = reh["config4"]
+    assert c4["n_gpus"] == 2 and c4["scaling"] == "strong"
+    assert abs(c4["frames_per_s_per_gpu"] * 2 - c4["frames_per_s"]) / c4["frames_per_s"] < 1e-9
+
+
+def test_dist_check_in_headline_line(line):
+    dc = line.get("dist_check")
+    if dc is None:
+        pytest.skip("bench line predates dist_check (round < 3)")
+    assert dc["all_ranks_agree"] is True and dc["group_size"] == line["n_gpus"]

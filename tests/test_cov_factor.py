@@ -1,0 +1,113 @@
+"""WCE_MMSE_COV host state (CPU, no device): Rhh validation and the 80-bit
+low-rank factor C = F Rhh F^H = U U^H that the Gram path (mmse_lr_kernel)
+applies, plus a numpy restatement of that path's algebra against the long
+double unified solve -- the formulation checked without a GPU."""
+import numpy as np
+import pytest
+
+from oracle_py import N, normrel
+
+
+def pdp_rhh(L, decay):
+    p = np.exp(-decay * np.arange(L))
+    R = np.zeros((N, N), np.complex128)
+    R[np.arange(L), np.arange(L)] = p / p.sum() * 1.1e-4
+    return R
+
+
+@pytest.fixture(scope="module")
+def inp(golden):
+    return golden["inputs"]
+
+
+@pytest.mark.parametrize("L,decay,k0", [(1, 0.5, 6), (5, 0.5, 6), (6, 0.5, 5), (13, 0.5, 5), (16, 0.5, 4),
+                                        (29, 0.2, 3), (40, 0.1, 1), (45, 0.1, 1), (46, 0.1, 0), (52, 0.12, 0),
+                                        (53, 0.12, -1), (53, 0.5, 0)])
+def test_factor_rank_and_path(wce, oracle, inp, L, decay, k0):
+    R = pdp_rhh(L, decay)
+    U, r, kk, lmax, lmin = wce.cov_factor(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R))
+    assert (r, kk) == (L, k0)
+    F = oracle.fmatrix()
+    C = np.asarray(F @ oracle._ld(R) @ F.conj().T, np.complex128)
+    assert np.max(np.abs(U @ U.conj().T - C)) < 4e-15 * np.max(np.abs(C))
+    pd = np.diag(R).real * N                 # eigenvalues of C = F diag(p) F^H (F^H F = 53 I)
+    assert abs(lmax - pd.max()) < 1e-13 * pd.max() and abs(lmin - pd[:L].min()) < 1e-13 * pd[:L].min()
+
+
+def test_rotated_rhh_rank(wce, oracle, inp):
+    """Rank 5 in a random unitary basis, formed in fp64: the null space carries
+    only rounding (~1e-16 lambda_max), below the 2^-46 rank tolerance."""
+    rng = np.random.default_rng(5)
+    Q, _ = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+    d = np.zeros(N)
+    d[:5] = np.exp(-0.4 * np.arange(5))
+    R = (Q * d) @ Q.conj().T
+    U, r, k0, _, _ = wce.cov_factor(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R))
+    assert (r, k0) == (5, 6)
+    F = oracle.fmatrix()
+    C = np.asarray(F @ oracle._ld(R) @ F.conj().T, np.complex128)
+    assert np.max(np.abs(U @ U.conj().T - C)) < 1e-14 * np.max(np.abs(C))
+
+
+def test_invalid_rhh_rejected(wce, inp):
+    R = pdp_rhh(8, 0.5)
+    bad = {
+        "not Hermitian": R + 1e-9 * np.triu(np.ones((N, N)), 1),
+        "imaginary diagonal": R + 1e-9j * np.eye(N),
+        "indefinite": R - 1e-6 * np.eye(N),
+        "NaN": np.where(np.eye(N) > 0, np.nan, R),
+        "Inf": np.where(np.eye(N) > 0, np.inf, R),
+        "negative definite": -R,
+    }
+    for what, M in bad.items():
+        with pytest.raises(wce.WceError):
+            wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=M)
+        assert what
+
+
+def test_accepts_rounding_level_asymmetry_and_zero(wce, inp):
+    R = pdp_rhh(8, 0.5)
+    R2 = R.copy()
+    R2[0, 3] += 1e-14 * R.max()          # 1e-14 relative: within the 1e-12 Hermitian tolerance
+    U, r, k0, _, _ = wce.cov_factor(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R2))
+    assert r >= 8
+    U, r, k0, lmax, lmin = wce.cov_factor(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"],
+                                                         Rhh=np.zeros((N, N))))
+    assert (r, k0, lmax, lmin) == (0, 6, 0.0, 0.0)    # C = 0: H = 0 (Gram system b I, zero border)
+
+
+def _lowrank_np(U, tx, rx, a, b):
+    """The Gram path's algebra in fp64 (mmse_lr_kernel without its register layout)."""
+    G = tx[:, None] * U
+    M = a * (G.conj().T @ G) + b * np.eye(U.shape[1])
+    L = np.linalg.cholesky(M)
+    t = np.linalg.solve(L.conj().T, np.linalg.solve(L, G.conj().T @ rx))
+    y = U @ t
+    if np.any(tx.imag != 0):
+        v = (tx - tx.conj()) * (rx - a * tx * y)
+        y = y + U @ (U.conj().T @ v) / b
+    return y
+
+
+@pytest.mark.parametrize("L", [1, 4, 16, 40])
+def test_lowrank_algebra_vs_long_double(wce, oracle, inp, L):
+    R = pdp_rhh(L, 0.3)
+    U, r, _, _, _ = wce.cov_factor(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R))
+    F = oracle.fmatrix()
+    C = F @ oracle._ld(R) @ F.conj().T
+    rng = np.random.default_rng(L)
+    ow2 = inp["ow2"]
+    worst = 0.0
+    for i in range(24):
+        if i % 3 == 0:
+            tx = 8.8753 * rng.choice([-1.0, 1.0], N).astype(complex)
+        else:
+            tx = 8.8753 * (rng.choice([-1.0, 1.0], N) + 1j * rng.choice([-1.0, 1.0], N)) / np.sqrt(2)
+        tx[26] = 0
+        h = (rng.standard_normal(N) + 1j * rng.standard_normal(N)) * 0.007
+        h = np.fft.fft(np.fft.ifft(h) * (np.arange(N) < 6))       # a 6-tap channel of its own
+        rx = h * tx + np.sqrt(ow2 / 2) * (rng.standard_normal(N) + 1j * rng.standard_normal(N))
+        got = _lowrank_np(U, tx, rx, 1.0, ow2)
+        exp = oracle.mmse_unified(C, np.ones(N, np.uint8), 1.0, ow2, tx, rx)
+        worst = max(worst, float(normrel(got, exp)))
+    assert worst < 1e-11, worst

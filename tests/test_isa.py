@@ -29,3 +29,13 @@ def test_checker_flags_a_hazard():
     assert len(isa_check.dpp_hazards(bad)) == 1
     ok = "v_mov_b32 v122, v1\ns_nop 1\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
     assert isa_check.dpp_hazards(ok) == []
+
+
+def test_checker_flags_dpp_after_a_label():
+    """A DPP instruction at a branch target / loop header has predecessors the
+    straight-line scan cannot see: flagged unless 2 wait states follow the label."""
+    import isa_check
+    bad = "v_mov_b32 v1, v2\n.LBB0_3:\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
+    assert [p for _, p in isa_check.dpp_hazards(bad)] == [isa_check.LABEL]
+    ok = ".LBB0_3:\ns_nop 1\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
+    assert isa_check.dpp_hazards(ok) == []

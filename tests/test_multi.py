@@ -46,8 +46,8 @@ def _worker(rank, world, port, q):
         blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK) if rank == 0 else None
         got = multi.broadcast_state_host(dist, blob, n, src=0)
         local = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
-        magic = int(np.frombuffer(got[-16:-8].tobytes(), dtype=np.int32)[1])
-        q.put((rank, bool(np.array_equal(got, local)), magic, multi.weak_shard(65536, rank)))
+        mode = wce.state_mode(got)   # raises unless the bytes carry the state magic
+        q.put((rank, bool(np.array_equal(got, local)), mode, multi.weak_shard(65536, rank)))
     finally:
         dist.destroy_process_group()
 
@@ -66,9 +66,9 @@ def test_state_broadcast_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert [r[0] for r in res] == [0, 1]
-    for rank, same, magic, (first, count) in res:
+    for rank, same, mode, (first, count) in res:
         assert same
-        assert magic == 0x80211
+        assert mode == 1   # WCE_MMSE_TEXTBOOK
         assert (first, count) == (rank * 65536, 65536)
 
 
@@ -113,7 +113,8 @@ def _bench_dist_worker(rank, world, port, q):
         calls = []
         bench.prewarm_sync(d, _NullStream(), lambda: calls.append(1), 0.05)
         d.barrier()
-        q.put((rank, d.world, d.max(1.5 + rank), len(calls) > 0))
+        g = d.group_check()
+        q.put((rank, d.world, d.max(1.5 + rank), len(calls) > 0, g["group_size"], g["all_ranks_agree"]))
     finally:
         d.close()
 
@@ -132,4 +133,4 @@ def test_bench_dist_control_path_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res == [(0, 2, 2.5, True), (1, 2, 2.5, True)]
+    assert res == [(0, 2, 2.5, True, 2, True), (1, 2, 2.5, True, 2, True)]

@@ -27,18 +27,33 @@ def regs(tok: str):
     return set(range(int(m.group(1)), int(m.group(2)) + 1))
 
 
-def instructions(text: str):
+LABEL = "<label>"
+
+
+def instructions(text: str, labels=False):
+    """Instruction lines; with labels=True also the basic-block labels (as LABEL)."""
     for line in text.splitlines():
         t = line.split(";")[0].strip()
-        if not t or t.startswith(".") or t.endswith(":"):
+        if t.endswith(":"):   # labels (".LBB0_3:", "kernel:") before directives (".p2align")
+            if labels:
+                yield LABEL
+            continue
+        if not t or t.startswith("."):
             continue
         yield t
 
 
 def dpp_hazards(text: str):
-    """List of (dpp instruction, offending earlier instruction)."""
+    """List of (dpp instruction, offending earlier instruction).  A label is a
+    branch target or loop header whose predecessors this straight-line scan
+    cannot see: a DPP instruction fewer than 2 wait states after one is
+    reported (offender LABEL) unless those wait states come after the label."""
     out, prev = [], []   # prev: (wait states the instruction provides, text)
-    for ins in instructions(text):
+    for ins in instructions(text, labels=True):
+        if ins == LABEL:
+            prev.append((0, LABEL))
+            prev = prev[-8:]
+            continue
         op = ins.split()[0]
         if "_dpp" in op:
             ops = [o.strip() for o in ins[len(op):].split(",")]
@@ -46,6 +61,9 @@ def dpp_hazards(text: str):
             ws = 0
             for w, p in reversed(prev):
                 if ws >= 2:
+                    break
+                if p == LABEL:
+                    out.append((ins, LABEL))
                     break
                 pop = p.split()[0]
                 if pop.startswith("v_") and not pop.startswith(("v_readlane", "v_readfirstlane", "v_cmp")):
