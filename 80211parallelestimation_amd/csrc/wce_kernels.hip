@@ -2292,7 +2292,14 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 #ifndef WCE_APPLY_WG_PER_CU
 #define WCE_APPLY_WG_PER_CU 2
 #endif
-constexpr int ACS = 57;
+// Row stride (complex) of the staged C.  A read sc[i * ACS + 4 s + kl] (i =
+// 16 nt + (lane & 15), kl = lane >> 4) is a ds_read_b128, banked in four
+// 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... on 16-B slots
+// (ACS ml + kl) mod 16: ACS = 57 put 3 lanes of a group on one slot (8 LDS
+// cycles per read instead of 4: the 3.97 conflict cycles per LDS instruction
+// of r02_pmc_legs.json apply1m); 58 maps every group onto 16 distinct slots
+// (tools/lds_banks.py enumerates the strides).
+constexpr int ACS = 58;
 __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t n, int64_t g, int ml, int kl,
                                            double2 (&w)[KSTEPS])
 {

@@ -12,6 +12,8 @@ legs (bench.py field -> kernel, frames per launch):
   ls_pilots  (calibration)       ls_flat_kernel                1,048,576 (PS_Linear only: pilot reads)
   front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
   config5    config5_sharded     mmse_solve_ls_kernel<true,true,true>  1,048,576 (all 5 + eq, fp32 LS)
+  config5_ref(_f32) config5_ref   ref_ls_elem_kernel<true>      1,048,576 (REF + LS family + eq, fp64 / fp32 LS)
+  lowrank<L> cov_lowrank.L<L>    mmse_lr_kernel<K0>               65,536 (COV, L-tap PDP: rank L)
 """
 import argparse
 import importlib
@@ -35,7 +37,19 @@ LEGS = {
     "front_blocks": ("front_kernel<false>", 65536),
     "front_preamble": ("front_kernel<true>", 65536),
     "config5": ("mmse_solve_ls_kernel<true, true, true>", 1 << 20),
+    "config5_ref": ("ref_ls_elem_kernel<true>", 1 << 20),
+    "config5_ref_f32": ("ref_ls_elem_kernel<true>", 1 << 20),
+    "lowrank4": ("mmse_lr_kernel<6>", 65536),
+    "lowrank8": ("mmse_lr_kernel<5>", 65536),
+    "lowrank16": ("mmse_lr_kernel<4>", 65536),
 }
+
+
+def pdp_rank(L):
+    p = np.exp(-0.5 * np.arange(L))
+    R = np.zeros((N, N), np.complex128)
+    R[np.arange(L), np.arange(L)] = p / p.sum() * 1.1e-4
+    return R
 
 
 def pdp_rhh():
@@ -72,6 +86,25 @@ def main():
             W = wce.DeviceArray((n, N), zero=True)
             ctx.mmse_solve(fr, W, N)
             run = lambda: ctx.mmse_apply(W, H, n, N)
+    elif leg.startswith("lowrank"):
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rank(int(leg[7:])))
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211)
+        H = wce.DeviceArray((n, N), zero=True)
+        fr = ctx.frames(tx, rx, n)
+        run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
+                                   wce.PS_MMSE)
+    elif leg.startswith("config5_ref"):
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        f32 = leg.endswith("f32")
+        dt = np.complex64 if f32 else np.complex128
+        tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+        ctx.synth(tx, rx, pre, n, seed=0x80211)
+        outs = [wce.DeviceArray((n, N), dt) for _ in range(4)] + [wce.DeviceArray((n, N))]
+        eq = wce.DeviceArray((n, NBLK, N), dt)
+        o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32 if f32 else 0)
+        fr = ctx.frames(tx, rx, n, rx_pre=pre)
+        run = lambda: ctx.estimate(fr, o, wce.ALL)
     elif leg == "ref":
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
         tx, rx, fr = bench.ref_frames(wce, ctx, n)
