@@ -1740,6 +1740,69 @@ __device__ __forceinline__ void lr_gram(const State *__restrict__ st, SolveLds &
         else lr_gram<K0, I + 1, 0>(st, s, A, lane, p, q, ac, bc);
     }
 }
+// The same Gram blocks on the VALU, straight into the block-cyclic layout:
+// G~ is staged through LDS 8 subcarriers at a time (T[kk][j], j < 56 - 8 K0),
+// and lane (p, q) accumulates A[aa][bb] += conj(G~[k][p + 8 (aa - K0)])
+// G~[k][q + 8 (bb - K0)] for its blocks aa >= bb >= K0 only -- no upper
+// tiles, no padding columns, 4 FMAs per element and subcarrier, where the
+// MFMA tiles execute ~2-4x that (16 x 16 tiles over 56 - 8 K0 rows, both
+// triangles, 4 real MFMAs per complex product).  Operand reads: lanes that
+// share p (or q) read one address, so each ds_read_b128 touches <= 8 slots.
+constexpr int LR_KC = 8;   // subcarriers per staged chunk
+template <int K0>
+__device__ __forceinline__ void lr_gram_valu(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB],
+                                             int lane, int p, int q, double ac, double bc)
+{
+    constexpr int NC = 8 * (RB - K0);   // staged Gram columns (block rows K0..6)
+    constexpr int NB = RB - K0;
+    static_assert(LR_KC * NC <= 56 * CVS, "chunk fits the conv buffer");
+    double2 *T = s.conv;
+#pragma unroll
+    for (int aa = K0; aa < RB; ++aa)
+#pragma unroll
+        for (int bb = K0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
+#pragma unroll 1
+    for (int k0 = 0; k0 < 56; k0 += LR_KC) {
+#pragma unroll
+        for (int e = lane; e < LR_KC * NC; e += 64) {
+            const int kk = e / NC, j = e - kk * NC;
+            T[e] = lr_gcol<K0>(st, s, k0 + kk, j);
+        }
+        wave_lds_sync();
+#pragma unroll 2
+        for (int kk = 0; kk < LR_KC; ++kk) {
+            double2 rw[NB], cl[NB];
+#pragma unroll
+            for (int m = 0; m < NB; ++m) {
+                rw[m] = T[kk * NC + p + 8 * m];
+                cl[m] = T[kk * NC + q + 8 * m];
+            }
+#pragma unroll
+            for (int m = 0; m < NB; ++m)
+#pragma unroll
+                for (int n = 0; n <= m; ++n) {   // += conj(rw) cl
+                    double2 &acc = A[K0 + m][K0 + n];
+                    acc.x = fma(rw[m].x, cl[n].x, fma(rw[m].y, cl[n].y, acc.x));
+                    acc.y = fma(rw[m].x, cl[n].y, fma(-rw[m].y, cl[n].x, acc.y));
+                }
+        }
+        wave_lds_sync();   // the next chunk rewrites T
+    }
+#pragma unroll
+    for (int aa = K0; aa < RB; ++aa) {
+        const bool gram = p + 8 * aa < NSC;   // rows 53 (border), 54, 55 stay as they are
+#pragma unroll
+        for (int bb = K0; bb <= aa; ++bb) {
+            double2 e = cscale(A[aa][bb], ac);
+            e.x += (gram && aa == bb && p == q) ? bc : 0.0;
+            A[aa][bb] = make_double2(gram ? e.x : A[aa][bb].x, gram ? e.y : A[aa][bb].y);
+        }
+    }
+}
+#ifndef WCE_LR_GRAM_MFMA   // A/B: 1 = the Gram blocks from v_mfma_f64_16x16x4 tiles (lr_gram)
+#define WCE_LR_GRAM_MFMA 0
+#endif
+
 template <int BLK, int K0>
 __device__ __forceinline__ void back_blocks_from(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
                                                  SolveLds &s, int p, int q, int lane)
@@ -1774,7 +1837,8 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
     for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
         for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
-    lr_gram<K0, 0, 0>(st, s, A, lane, p, q, ac, bc);
+    if (WCE_LR_GRAM_MFMA) lr_gram<K0, 0, 0>(st, s, A, lane, p, q, ac, bc);
+    else lr_gram_valu<K0>(st, s, A, lane, p, q, ac, bc);
     dense_chol<K0>(A, s, p, q, lane);
     double rq[RB];
 #pragma unroll
@@ -1823,7 +1887,7 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
 // of a.w; avg_blocks_kernel forms the mean.
 // K0 = 0 (r > 45: a Gram system as large as Ryy itself) holds all 28
 // register blocks through the MFMA build: 181 VGPRs, 2 waves/SIMD; K0 = 1: 156
-constexpr int lr_waves(int k0) { return k0 == 0 ? 2 : (k0 == 1 ? 3 : WCE_LR_WAVES_PER_SIMD); }
+constexpr int lr_waves(int k0) { return k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD); }
 template <int K0>
 __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
 {

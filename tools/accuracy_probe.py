@@ -32,3 +32,36 @@ for label, hs in (("matched channel", hlt), ("unrelated channel", None)):
         out = ctx.estimate_host(txh, rxh, mask=wce.PS_MMSE)["ps_mmse"]
         err = orc.normrel(out, ref)
         print(f"{label:18s} {'bordered row' if on else 'back-subst + CW':16s} max {err.max():.2e}  median {np.median(err):.2e}")
+
+# ---- round 3: WCE_MMSE_COV rank sweep.  L-tap exponential power-delay
+# profiles (rank L; 53 taps = full rank at two spectral widths), frames with
+# their own channels (frame 0 = inputs.h), against the long double unified
+# solve with C = F Rhh F^H formed in 80 bits.  Both solve forms on the same
+# ctx: the low-rank Gram path (mmse_lr_kernel) and the dense Ryy solve
+# (wce_debug_set_cov_path), whichever the state chose marked with '*'.
+print("# WCE_MMSE_COV rank sweep: max / median norm-relative error vs the long double solve")
+B = 1025
+Fld = orc.fmatrix()
+for L, decay in ((1, 0.5), (4, 0.5), (6, 0.5), (8, 0.5), (16, 0.5), (24, 0.3), (40, 0.1), (53, 0.12), (53, 0.5)):
+    p = np.exp(-decay * np.arange(L))
+    R = np.zeros((53, 53), np.complex128)
+    R[np.arange(L), np.arange(L)] = p / p.sum() * 1.1e-4
+    c = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    r, lr, lmax, lmin = c.cov_info()
+    tx, rx = wce.DeviceArray((B, 15, 53)), wce.DeviceArray((B, 15, 53))
+    c.synth(tx, rx, None, B, seed=0xC0 + L)
+    wce.synchronize()
+    txh, rxh = tx.numpy(), rx.numpy()
+    txh[0], rxh[0] = inp["tx_symb"], inp["rx_symb"]
+    C = Fld @ orc._ld(R) @ Fld.conj().T
+    ref = np.stack([orc.mmse_unified(C, np.ones(53, np.uint8), 1.0, inp["ow2"], txh[f, 0], rxh[f, 0])
+                    for f in range(B)])
+    row = []
+    for path, name in ((2, "low-rank"), (1, "dense")):
+        c.set_cov_path(path)
+        err = orc.normrel(c.estimate_host(txh, rxh, mask=wce.PS_MMSE)["ps_mmse"], ref)
+        mark = "*" if (path == 2) == lr else " "
+        row.append(f"{name}{mark} max {err.max():.2e} median {np.median(err):.2e}")
+    print(f"L={L:2d} decay={decay:4.2f} rank={r:2d} spectrum {lmax / lmin if lmin else float('inf'):8.1e}: "
+          + "   ".join(row))
+    del c

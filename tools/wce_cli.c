@@ -176,6 +176,32 @@ int main(int argc, char **argv)
         free(back);
         free(hc);
     }
+    /* WCE_MMSE_COV with a model covariance: a 6-tap exponential power-delay
+     * profile (rank 6) takes the low-rank Gram path; an indefinite Rhh is refused */
+    {
+        static wce_complex R[WCE_NSC * WCE_NSC];
+        double norm = 0;
+        for (int t = 0; t < 6; t++) norm += exp(-0.5 * t);
+        for (int t = 0; t < 6; t++) R[t * WCE_NSC + t].re = 1.1e-4 * exp(-0.5 * t) / norm;
+        wce_ctx *cov;
+        CHECK(wce_ctx_create_cov(&cov, 0, tx_pre, rx_pre, R, ow2));
+        int rank = -1, lowrank = -1;
+        double lmax = 0, lmin = 0;
+        CHECK(wce_ctx_cov_info(cov, &rank, &lowrank, &lmax, &lmin));
+        if (rank != 6 || lowrank != 1) {
+            fprintf(stderr, "cov info: rank %d low-rank %d\n", rank, lowrank);
+            return 4;
+        }
+        float ms = time_it(stream, cov, &in, &out, WCE_EST_PS_MMSE, reps);
+        printf("  %-38s %9.3f ms  %.3e frames/s (rank %d, low-rank path)\n", "PS_MMSE, 6-tap PDP covariance", ms,
+               B / (ms * 1e-3), rank);
+        CHECK(wce_ctx_destroy(cov));
+        R[3 * WCE_NSC + 3].re = -1e-6;   /* indefinite: must be refused */
+        if (wce_ctx_create_cov(&cov, 0, tx_pre, rx_pre, R, ow2) != WCE_EINVAL) {
+            fprintf(stderr, "indefinite Rhh accepted\n");
+            return 5;
+        }
+    }
     /* spot check: LT_LS of frame 0 at DC must be 0 (main.c:74) */
     wce_complex h0[WCE_NSC];
     CHECK(wce_stream_synchronize(stream));
