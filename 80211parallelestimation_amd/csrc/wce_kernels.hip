@@ -1660,7 +1660,7 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
 //     s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b.
 // The dense form (mmse_solve_kernel: z = Ryy^-1 rx, then C X z) carries the
 // components of z along C's null space, of size |rx|/b, which C X must
-// cancel: it loses ~eps cond(Ryy) on a rank-deficient C, 1e-10..1e-9 here
+// cancel: it loses ~eps cond(Ryy) on a rank-deficient C, 2e-10 .. 1e-8 here
 // (DESIGN.md s2).  This form never creates them: the error stays at the
 // 1e-13 level for every rank (profiles/r03_cov_rank_probe.txt).
 //

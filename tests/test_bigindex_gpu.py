@@ -48,6 +48,9 @@ def _run(wce, ctx, fr, mask, f32=False):
     ("TEXTBOOK", "LT_LS|PS_LINEAR", False, "C"),     # ls_elem_kernel
     ("TEXTBOOK", "ALL", True, "C"),                  # fused solve + LS family + equalization, fp32 outputs
     ("COV", "PS_MMSE", False, "C"),                  # dense solve + MFMA apply
+    ("COV8", "PS_MMSE", False, "C"),                 # low-rank Gram path (8-tap PDP, mmse_lr_kernel<5>)
+    ("COV8", "PS_MMSE", False, "MATLAB"),            # low-rank, split per-block solves + block mean
+    ("REF", "ALL", True, "C"),                       # ref_ls_elem_kernel, fp32 LS / eq
     ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "C"),   # per-frame covariance: factor matvecs + solve
     ("TEXTBOOK", "LS_ALL", False, "MATLAB"),         # ls_kernel, MATLAB semantics (4-block averages)
     ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "MATLAB"),   # split per-block solves + fc_finish
@@ -57,6 +60,11 @@ def test_64bit_frame_indexing(layouts, mode, mask, f32, sem):
     if mode == "COV":
         p = np.exp(-0.12 * np.arange(N))
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4)
+    elif mode == "COV8":
+        p = np.zeros(N)
+        p[:8] = np.exp(-0.5 * np.arange(8))
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4)
+        assert ctx.cov_info()[:2] == (8, True)
     else:
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], getattr(wce, "MMSE_" + mode))
     m = 0

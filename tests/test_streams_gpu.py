@@ -22,7 +22,8 @@ def _batch(wce, ctx, n, seed):
 
 CASES = [("frame_cov", lambda wce: wce.PS_MMSE | wce.FRAME_COV, 0),
          ("matlab", lambda wce: wce.PS_MMSE, 1),
-         ("matlab_frame_cov", lambda wce: wce.PS_MMSE | wce.FRAME_COV, 1)]
+         ("matlab_frame_cov", lambda wce: wce.PS_MMSE | wce.FRAME_COV, 1),
+         ("matlab_cov_lowrank", lambda wce: wce.PS_MMSE, 1)]   # mmse_lr_kernel split + block mean
 
 
 def _call(wce, ctx, b, n, mask, sem, stream):
@@ -36,7 +37,13 @@ def _call(wce, ctx, b, n, mask, sem, stream):
 def test_streams_do_not_share_scratch(gpu_wce, golden, name, maskf, sem):
     wce = gpu_wce
     inp = golden["inputs"]
-    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK, device=0)
+    if name == "matlab_cov_lowrank":
+        p = np.zeros(N)
+        p[:6] = np.exp(-0.5 * np.arange(6))
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], device=0,
+                          Rhh=np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4)
+    else:
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK, device=0)
     mask = maskf(wce)
     sizes = [8192, 6000, 8192, 3001]               # different sizes: a shared buffer's layout would differ too
     batches = [_batch(wce, ctx, n, 100 + i) for i, n in enumerate(sizes)]
