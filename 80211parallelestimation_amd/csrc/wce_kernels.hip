@@ -1662,7 +1662,7 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
 // components of z along C's null space, of size |rx|/b, which C X must
 // cancel: it loses ~eps cond(Ryy) on a rank-deficient C, 2e-10 .. 1e-8 here
 // (DESIGN.md s2).  This form never creates them: the error stays at the
-// 1e-13 level for every rank (profiles/r03_cov_rank_probe.txt).
+// 1e-13 level for every rank (profiles/r03_accuracy_probe.txt).
 //
 // The r x r Gram system reuses the dense solve's machinery: it is embedded
 // in the block-cyclic registers at block row K0 = (53 - r) / 8 (rows 8 K0 ..

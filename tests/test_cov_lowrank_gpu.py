@@ -4,7 +4,7 @@
 A power-delay profile of L taps gives Rhh = diag(p_0..p_{L-1}, 0, ...): C has
 rank L, and at the synthetic frames' SNR Ryy = X C X^H + ow2 I has cond ~4e6.
 The dense form C X (Ryy^-1 rx) loses ~eps cond(Ryy) there (2e-10 .. 1e-8 in
-profiles/r03_cov_rank_probe.txt); the low-rank Gram path (mmse_lr_kernel, H =
+profiles/r03_accuracy_probe.txt); the low-rank Gram path (mmse_lr_kernel, H =
 U s) is checked here at every rank the state can choose, on 1,025 frames per
 profile with channels of their own (frame 0 = the inputs.h frame), against
 the long double unified solve (oracle_py.mmse_unified) with C = F Rhh F^H
