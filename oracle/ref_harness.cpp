@@ -108,6 +108,82 @@ void refh_mmse_repaired(ldc *tx_symbols, ldc *rx_symbols, ldc *Fflat, double ow2
     free(buf);
 }
 
+// WiFi_channel_estimation_PS_MMSE.m:26-33 (one block), composed from the
+// reference's own matrix routines: multiply() (utils.c:16-31) for every
+// product and inverse() (utils.c:141-170, the cofactor / unpivoted-Schur
+// inverse) for pinv(Ryy), all in its long double complex.  The reference has
+// no conjugate transpose (its hermitian() is re - im, utils.c:3-7), so the
+// .m file's ' is formed here, and the MATLAB ifft is conj(F) h / 53.
+//   C   : Rhh_in == NULL -> Rhh = ifft(H_LS) ifft(H_LS)' (TEXTBOOK); else the
+//         caller's 53 x 53 Rhh (WCE_MMSE_COV); C = F Rhh F'.
+//   Ryy = X4 C X4' + ow2 I, X4 = diag(tx);  H = F (Rhh F' X4) inv(Ryy) rx.
+// One step differs from calling inverse(Ryy) on all 53: a null subcarrier
+// (tx = 0, e.g. DC) leaves Ryy's row and column = ow2 e_i, and the cofactor
+// of a minor with that column but not that row is 0/0 in the unpivoted
+// Schur recursion (the NaN of main.c's PS_MMSE).  Ryy is block
+// diagonal there, so inverse() runs on the block of the other subcarriers
+// and the null's entry is 1 / ow2 -- the same inverse, exactly.
+void refh_mmse_formula(ldc *tx, ldc *rx, ldc *Fflat, double ow2, ldc *H_LS, ldc *Rhh_in, ldc *H_out)
+{
+    const int n = SAMPUTIL;
+    ldc *buf = (ldc *)calloc((size_t)n * n * 10 + 4 * n, sizeof(ldc));
+    ldc **F = rows(Fflat, n, n);
+    ldc **FH = rows(buf + 0 * n * n, n, n), **Fc = rows(buf + 1 * n * n, n, n);
+    ldc **Rhh = rows(buf + 2 * n * n, n, n), **C = rows(buf + 3 * n * n, n, n);
+    ldc **X4 = rows(buf + 4 * n * n, n, n), **X4H = rows(buf + 5 * n * n, n, n);
+    ldc **T1 = rows(buf + 6 * n * n, n, n), **Ryy = rows(buf + 7 * n * n, n, n);
+    ldc **Rhy = rows(buf + 8 * n * n, n, n), **invRyy = rows(buf + 9 * n * n, n, n);
+    ldc **hv = rows(buf + 10 * n * n, n, 1), **hls = rows(buf + 10 * n * n + n, n, 1);
+    ldc **rx1 = rows(buf + 10 * n * n + 2 * n, n, 1), **tmp = rows(buf + 10 * n * n + 3 * n, n, 1);
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < n; c++) {
+            FH[r][c] = conjl(F[c][r]);
+            Fc[r][c] = conjl(F[r][c]);
+            X4[r][c] = r == c ? tx[r] : 0.0L;
+            X4H[r][c] = r == c ? conjl(tx[r]) : 0.0L;
+        }
+    for (int r = 0; r < n; r++) { hls[r][0] = H_LS ? H_LS[r] : 0.0L; rx1[r][0] = rx[r]; }
+    if (Rhh_in) {
+        for (int i = 0; i < n * n; i++) Rhh[i / n][i % n] = Rhh_in[i];
+    } else {
+        multiply(Fc, n, n, hls, n, 1, hv);                       // ifft(H_LS, 53) * 53
+        for (int r = 0; r < n; r++) hv[r][0] = hv[r][0] / (long double)n;
+        for (int r = 0; r < n; r++)
+            for (int c = 0; c < n; c++) Rhh[r][c] = hv[r][0] * conjl(hv[c][0]);
+    }
+    multiply(Rhh, n, n, FH, n, n, T1);
+    multiply(F, n, n, T1, n, n, C);                              // C = F Rhh F'
+    multiply(X4, n, n, C, n, n, T1);
+    multiply(T1, n, n, X4H, n, n, Ryy);                          // X4 C X4'
+    for (int r = 0; r < n; r++) Ryy[r][r] = Ryy[r][r] + (long double)ow2;
+    int keep[SAMPUTIL], m = 0;
+    for (int r = 0; r < n; r++)
+        if (tx[r] != 0.0L) keep[m++] = r;
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < n; c++) invRyy[r][c] = 0.0L;
+    for (int r = 0; r < n; r++)
+        if (tx[r] == 0.0L) invRyy[r][r] = 1.0L / Ryy[r][r];
+    if (m > 0) {
+        ldc *sb = (ldc *)calloc((size_t)2 * m * m, sizeof(ldc));
+        ldc **S = rows(sb, m, m), **Si = rows(sb + (size_t)m * m, m, m);
+        for (int r = 0; r < m; r++)
+            for (int c = 0; c < m; c++) S[r][c] = Ryy[keep[r]][keep[c]];
+        inverse(S, m, Si);                                       // utils.c:141 on the coupled block
+        for (int r = 0; r < m; r++)
+            for (int c = 0; c < m; c++) invRyy[keep[r]][keep[c]] = Si[r][c];
+        free(S); free(Si); free(sb);
+    }
+    multiply(Rhh, n, n, FH, n, n, T1);
+    multiply(T1, n, n, X4, n, n, Rhy);                           // Rhy = Rhh F' X4
+    multiply(invRyy, n, n, rx1, n, 1, tmp);                      // inv(Ryy) rx
+    multiply(Rhy, n, n, tmp, n, 1, hv);
+    multiply(F, n, n, hv, n, 1, tmp);                            // F Rhy inv(Ryy) rx
+    for (int r = 0; r < n; r++) H_out[r] = tmp[r][0];
+    free(F); free(FH); free(Fc); free(Rhh); free(C); free(X4); free(X4H); free(T1); free(Ryy); free(Rhy);
+    free(invRyy); free(hv); free(hls); free(rx1); free(tmp);
+    free(buf);
+}
+
 // ---- CPU baselines timed by bench.py (the reference's own sequential code) ----
 // Frames are [n][53] long double complex.  Return wall seconds.
 

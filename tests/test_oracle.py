@@ -189,3 +189,30 @@ def test_front_end_preamble_matlab_pin(oracle, golden):
     d = m["rx_preamble2"] - m["rx_preamble1"]
     assert abs(float(ow2) - np.sum(np.abs(d) ** 2) / 128) < 1e-15 * abs(float(ow2))
     assert 0 < float(ow2) < 1e-3
+
+
+def test_mmse_formula_pins_vs_oracle(oracle, golden):
+    """WiFi_channel_estimation_PS_MMSE.m's formula computed by the reference's
+    own multiply() and cofactor inverse() (tests/golden/make_mmse_pins.py,
+    oracle/ref_harness.cpp:refh_mmse_formula) pins the oracle's restatements:
+    the TEXTBOOK closed form and the long double unified solve (WCE_MMSE_COV
+    with a rank-6 and a full-rank power-delay profile), at the noise powers
+    where the cofactor inverse is itself accurate (cond(Ryy) <= ~4e4)."""
+    import os
+    pins = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "mmse_formula_pins.npz")))
+    F = from_split(golden["ref"]["F"])
+    hls = from_split(pins["h_ls"])
+    assert normrel(hls, oracle.lt_ls(golden["inputs"]["tx_pre"], golden["inputs"]["rx_pre"])) == 0
+    c = F @ (F.conj() @ hls / N)
+    ones = np.ones(N, np.uint8)
+    worst = 0.0
+    for wi, ow2 in enumerate(pins["ow2"]):
+        for f in range(pins["frames_tx"].shape[0]):
+            t, r = pins["frames_tx"][f], pins["frames_rx"][f]
+            checks = [(pins["H_textbook"][wi, f], oracle.mmse_textbook_closed(c, t, r, ow2))]
+            for kind in ("pdp6", "pdp53"):
+                C = F @ oracle._ld(pins["rhh_" + kind]) @ F.conj().T
+                checks.append((pins["H_" + kind][wi, f], oracle.mmse_unified(C, ones, 1.0, ow2, t, r)))
+            for pin, want in checks:
+                worst = max(worst, float(normrel(from_split(pin), want)))
+    assert worst < 5e-12, worst   # measured 2.0e-12 (rank 6 at ow2 = 1e-5: the cofactor inverse's own error)
