@@ -1994,6 +1994,63 @@ __global__ __launch_bounds__(256) void fc_finish_kernel(SolveArgs a, const doubl
 // =====================================================================
 constexpr int APPLY_WAVES = 4;
 
+#ifndef WCE_APPLY_TAIL4   // output rows 48..52 on v_mfma_f64_4x4x4_4b (0: a fourth 16x16x4 row block, rows 48..63)
+#define WCE_APPLY_TAIL4 1
+#endif
+#ifndef WCE_MATVEC_TAIL4   // the same for matvec_kernel: off, its C comes from L2 and the 4x4 form reads twice
+#define WCE_MATVEC_TAIL4 0   // as much of it per tile (45.1 vs 41.6 us at 65,536 frames; equal at 131,072)
+#endif
+constexpr int APPLY_NT = WCE_APPLY_TAIL4 ? 3 : 4;   // 16-row output blocks on 16x16x4
+constexpr int MATVEC_NT = WCE_MATVEC_TAIL4 ? 3 : 4;
+
+// Output rows 48..52 of one 16-frame tile.  The last 16-row block holds 5
+// live rows, so 16x16x4 on it spends 11/16 of its cycles (1/6 of the tile's)
+// on padding; v_mfma_f64_4x4x4_4b_f64 has the same flop rate (16 cycles per
+// 512 flop, profiles/r02_ubench_mfma4.txt) at 4-row granularity: rows 48..55
+// cost half as much.  Its lane map, lane l = 16 r + 4 b + c: A holds A_b[c][r],
+// B holds B_b[r][c], D holds D_b[r][c] (blocks b independent).  Block b =
+// frames 4b .. 4b+3, so B_b[k][n] = W_{4b+n}[4s+k] is exactly the W fragment
+// lane l already holds for 16x16x4 (frame l&15, subcarrier 4s + (l>>4));
+// A_b[m][k] = C[i0+m][4s+k]: lane l reads C[i0 + (l&3)][4s + (l>>4)] (the
+// same in every block); D: lane l gets H_{frame l&15}[i0 + (l>>4)].  Two row
+// groups (48..51, 52..55), four independent chains so that no MFMA waits on
+// the previous one's result (~45 cycles dependent latency, 16 issue).
+template <bool QIN, bool PIPE, typename CLoad>
+__device__ __forceinline__ void tail_rows(CLoad cload, const double (&ar)[KSTEPS], const double (&ai)[KSTEPS],
+                                          double *Y, int64_t ys, int64_t f0, int64_t n, int lane)
+{
+    const int kl = lane >> 4, m4 = lane & 3;
+    double r0 = 0.0, i0 = 0.0, r1 = 0.0, i1 = 0.0;
+    double2 n0 = cload(48 + m4, kl), n1 = cload(52 + m4, kl);
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const double2 c0 = n0, c1 = n1;
+        // PIPE (C from LDS, apply_kernel): one k-step of C in flight; the
+        // compiler would otherwise hoist all 28 reads (112 VGPRs) and spill.
+        // matvec_kernel (C from L2, one tile per wave) wants them all issued early.
+        if (PIPE) asm volatile("" ::: "memory");
+        if (s + 1 < KSTEPS) {
+            n0 = cload(48 + m4, 4 * (s + 1) + kl);
+            n1 = cload(52 + m4, 4 * (s + 1) + kl);
+        }
+        r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ar[s], r0, 0, 0, 0);
+        r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ar[s], r1, 0, 0, 0);
+        i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, ar[s], i0, 0, 0, 0);
+        i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, ar[s], i1, 0, 0, 0);
+        if constexpr (!QIN) {
+            r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, -ai[s], r0, 0, 0, 0);
+            r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, -ai[s], r1, 0, 0, 0);
+            i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ai[s], i0, 0, 0, 0);
+            i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ai[s], i1, 0, 0, 0);
+        }
+    }
+    const int64_t fr = f0 + (lane & 15);
+    if (fr < n) {
+        st2(Y, fr * ys + 48 + kl, make_double2(r0, i0));
+        if (kl == 0) st2(Y, fr * ys + 52, make_double2(r1, i1));   // rows 53..55: padding, never stored
+    }
+}
+
 // Y1[f] = M1 X[f] (and Y2[f] = M2 X[f]) for 16-frame tiles; M padded 64 x 64.
 // QIN: the input is replaced by (re X - im X, 0) (main.c:188's real "conj").
 // NB > 1: the input of frame f is the mean of rows f*NB .. f*NB+NB-1 of X
@@ -2030,7 +2087,7 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
         const double *M = m == 0 ? M1 : M2;
         double *Y = m == 0 ? Y1 : Y2;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
+        for (int nt = 0; nt < MATVEC_NT; ++nt) {
             const int i = 16 * nt + ml;
             v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
 #pragma unroll
@@ -2050,6 +2107,8 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
                 }
             }
         }
+        if (WCE_MATVEC_TAIL4)
+            tail_rows<QIN, false>([&](int i, int j) { return ld2(M, i * CLD + j); }, ar, ai, Y, ys, f0, n, lane);
     }
 }
 
@@ -2345,11 +2404,13 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 // H = C W for the dense-C (COV) path, streaming form.  matvec_kernel runs one
 // 16-frame tile per wave and one wave round for a whole launch, so every wave
 // loads W, multiplies, then stores at the same time: the HBM and MFMA phases
-// never overlap.  Here C is staged once per workgroup in LDS (row stride 57
-// complex: the 16 rows a read touches start 4 banks apart) and each wave
+// never overlap.  Here C is staged once per workgroup in LDS (row stride
+// ACS = 58 complex, conflict-free: below) and each wave
 // walks a strided sequence of 16-frame tiles, loading tile t + 1's W while
 // its MFMAs run on tile t.  Same fragment maps and summation order as
-// matvec_kernel, so H is bit-identical.
+// matvec_kernel for rows 0..47; rows 48..52 on v_mfma_f64_4x4x4_4b
+// (tail_rows: 508 -> 465 us per 1,048,576 frames), whose results matched
+// the 16x16x4 form bit for bit on every A/B run (tools/ab_libs.py --leg apply).
 #ifndef WCE_APPLY_V2
 #define WCE_APPLY_V2 1
 #endif
@@ -2364,6 +2425,8 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 // of r02_pmc_legs.json apply1m); 58 maps every group onto 16 distinct slots
 // (tools/lds_banks.py enumerates the strides).
 constexpr int ACS = 58;
+// staged rows of C: 56 once rows 48..55 are the last ones read (tail_rows)
+constexpr int APPLY_ROWS = WCE_APPLY_TAIL4 ? 56 : 64;
 __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t n, int64_t g, int ml, int kl,
                                            double2 (&w)[KSTEPS])
 {
@@ -2378,8 +2441,8 @@ __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t 
 __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const double *__restrict__ M, const double *X,
                                                                         int64_t xs, double *Y, int64_t ys, int64_t n)
 {
-    __shared__ double2 sc[64 * ACS];
-    for (int e = threadIdx.x; e < 64 * 4 * KSTEPS; e += 256) {
+    __shared__ double2 sc[APPLY_ROWS * ACS];
+    for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
         const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
         sc[i * ACS + j] = ld2(M, i * CLD + j);   // M zero-padded 64 x 64
     }
@@ -2402,7 +2465,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
         if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);   // next tile, under this one's MFMAs
         const int64_t f0 = 16 * g;
 #pragma unroll 1
-        for (int nt = 0; nt < 4; ++nt) {
+        for (int nt = 0; nt < APPLY_NT; ++nt) {
             const int i = 16 * nt + ml;
             v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
 #pragma unroll
@@ -2421,6 +2484,8 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
                 }
             }
         }
+        if (WCE_APPLY_TAIL4)
+            tail_rows<false, true>([&](int i, int j) { return sc[i * ACS + j]; }, ar, ai, Y, ys, f0, n, lane);
     }
 }
 

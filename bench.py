@@ -190,6 +190,13 @@ def hbm_bytes(k, narrow_fetch_kib: float = 0.0):
     return (2.0 * (k["FETCH_SIZE"] - narrow_fetch_kib) + narrow_fetch_kib + k["WRITE_SIZE"]) * 1024.0
 
 
+def mfma_flops(k):
+    """Executed f64 MFMA flops of one dispatch: SQ_INSTS_VALU_MFMA_MOPS_F64
+    counts 512-flop units (4 per v_mfma_f64_16x16x4, 1 per v_mfma_f64_4x4x4_4b;
+    r02_pmc_legs.json apply1m: 58.72 M MOPS for 14.68 M 16x16x4)."""
+    return k["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512.0
+
+
 def power_clock(stream, step, seconds=2.5):
     """Board power and shader clock while the headline kernel runs back to
     back (untimed, after the timed region): `amd-smi metric` sampled from a
@@ -387,13 +394,15 @@ def main():
                "algorithmic_bytes": 2 * N * 16 * B}
         if ka:
             waves = 4 * ((B + 63) // 64)
-            mfma = ka["SQ_INSTS_VALU_MFMA_F64"]             # wave-level v_mfma_f64_16x16x4 per launch
+            mfma = ka["SQ_INSTS_VALU_MFMA_F64"]             # wave-level f64 MFMA instructions per launch
             app.update({"waves": waves, "mfma_insts_per_wave": mfma / waves,
                         "traffic": hbm_bytes(ka),
-                        "executed_tflops": mfma * 2 * 16 * 16 * 4 / (t_apply * 1e-3) / 1e12,
+                        "executed_tflops": mfma_flops(ka) / (t_apply * 1e-3) / 1e12,
                         "mfma_busy_frac_pmc": ka["SQ_VALU_MFMA_BUSY_CYCLES"] / (ka["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4),
-                        "note": "executed = 224 MFMA/wave x 2,048 flop: 56 x 64 zero-padded (53 x 53 useful, "
-                                "x1.276); busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
+                        "note": "executed = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 flop: per 16-frame tile 168 "
+                                "v_mfma_f64_16x16x4 (rows 0..47) + 112 v_mfma_f64_4x4x4_4b (rows 48..55), "
+                                "56 x 56 zero-padded (53 x 53 useful, x1.116); busy = SQ_VALU_MFMA_BUSY_CYCLES / "
+                                "(GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
         # the same product at 1,048,576 frames (the configs[3] batch): past 131,072
         # frames mmse_apply switches to apply_kernel (C staged in LDS, each wave
         # streaming 16-frame tiles with the next tile's W loaded under the MFMAs).
@@ -422,7 +431,7 @@ def main():
             app["frames_1M"].update({
                 "traffic": hbm_bytes(kb),
                 "mfma_insts": mf,
-                "executed_tflops": mf * 2 * 16 * 16 * 4 / (t_big * 1e-3) / 1e12,
+                "executed_tflops": mfma_flops(kb) / (t_big * 1e-3) / 1e12,
                 "mfma_busy_frac_pmc": kb["SQ_VALU_MFMA_BUSY_CYCLES"] / (kb["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4)})
         del Wb, Hb
         res["apply_kernel"] = app
