@@ -593,7 +593,7 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     }
     double *H = reinterpret_cast<double *>(out->ps_mmse);
     if (lr_k0 >= 0) {   // H = U s straight from the solve (split: H_b rows, then the block mean)
-        rc = wce::launch_mmse_lr(c->d_state, lr_k0, sa, stream);
+        rc = wce::launch_mmse_lr(c->d_state, lr_k0, c->cov_rank, sa, stream);
         if (rc) return fail(rc, "mmse_lr launch");
         if (split) rc = wce::launch_avg_blocks(ws, WS_LD, H, out->out_stride, n, stream);
         return rc ? fail(rc, "block average launch") : WCE_OK;

@@ -18,6 +18,8 @@ constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a
 
 // The frame-independent shared state: everything one rank broadcasts to the
 // others (one RCCL broadcast, 68 KB).  Complex values are {re, im} fp64.
+constexpr int LRL_RMAX = 8;                          // ranks on the lane-per-frame low-rank kernel
+constexpr int LRL_NP = LRL_RMAX * (LRL_RMAX + 1) / 2;  // packed lower-triangle entries of its Gram matrix
 struct State {
     double C[CLD * CLD * 2];   // MMSE covariance operator, row-major, zero-padded to 64 x 64
                                // (65,536 B): kernels index it without bounds checks
@@ -52,6 +54,10 @@ struct State {
     double cov_lmax, cov_lmin; // largest / smallest kept eigenvalue of C
     int32_t cov_rank;          // r = number of kept eigen-directions (0..53)
     int32_t cov_k0;            // -1 dense; else first block row of the embedded Gram system
+    // Ranks 1..LRL_RMAX (mmse_lr_lane_kernel): the Gram matrix is sum_k |x_k|^2 P_k
+    // with P_k[i][j] = conj(U[k][i]) U[k][j], i >= j, packed at i (i + 1) / 2 + j
+    // (80-bit products rounded once; zero for other ranks)
+    double Pk[NSC * LRL_NP * 2];
 };
 static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
 
@@ -141,7 +147,8 @@ int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t 
 int launch_synth(const State *st, const SynthArgs &a, void *stream);
 // WCE_MMSE_COV low-rank path: H (or, split, H_b per (frame, block) row) from
 // the Gram system embedded at block row k0 (State::cov_k0)
-int launch_mmse_lr(const State *st, int k0, const SolveArgs &a, void *stream);
+// (rank = State::cov_rank: ranks 1..LRL_RMAX run one frame per lane instead)
+int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream);
 // H[f] = mean of X rows 4f .. 4f+3 (MATLAB block average, left to right)
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
@@ -152,6 +159,9 @@ constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks (
                                       // 1 = the same uncapped, 2 = one element per thread (ls_elem_kernel, default)
 constexpr int WCE_VARIANT_REF_LS = 2;  // REF PS_MMSE + LS family (+ eq), C semantics: 0 = ref_ls_elem_kernel
                                       // (one element per thread, default), 1 = mmse_solve_ls_kernel (wave per frame)
+constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1..LRL_RMAX one frame per lane
+                                      // (mmse_lr_lane_kernel, default), 1 = every rank on mmse_lr_kernel
+                                      // (one frame per wave); the two agree to rounding (~1e-15), not bitwise
 constexpr int WCE_VARIANT_COUNT = 4;
 int set_variant(int which, int value);
 int launch_ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, void *stream);

@@ -1900,6 +1900,153 @@ __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *
     if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, h);
 }
 
+// ---------------------------------------------------------------------
+// The same low-rank MMSE for ranks 1..LRL_RMAX, ONE (frame, block) PER LANE.
+// At rank <= 8 the Gram system is tiny (36 complex entries), so a wave per
+// frame spends its time on latency: the embedded 8 x 8-block factorisation
+// runs whole pivot chains for a handful of live rows, and 12 KB of LDS per
+// wave caps a CU at 13 waves (0.147 ms per 65,536 frames at rank 4, 0.268 at
+// rank 8, against ~0.035 ms for the 167 MB the frames and H move).  Here the
+// shared factors are wave-uniform and every lane owns its frame outright:
+//   pass 1, k = 0..52:  Gamma += |x_k|^2 P_k   (P_k[i][j] = conj(U_ki) U_kj,
+//                       State::Pk, scalar loads), beta += conj(U_k) conj(x_k) rx_k
+//   (a Gamma + b I) t = beta: Cholesky + two triangular solves in registers
+//   complex x only (wave-uniform branch): s = t + U^H [(x - conj x) o
+//                       (rx - a x o (U t))] / b, one more pass over k
+//   pass 2, k = 0..52:  H_k = U_k s, stored straight from the lane.
+// Same algebra as mmse_lr_kernel (G = X U, border Gamma^H rx), summed in
+// another order: the two agree to ~1e-15 (tests/test_cov_lowrank_gpu.py).
+// No LDS, no cross-lane traffic; the frame's loads and stores are 16 B per
+// lane at the frame stride, consecutive k filling each 64-B sector in turn.
+// ---------------------------------------------------------------------
+#ifndef WCE_LR_LANE_UNROLL   // subcarriers per pass-1 iteration (loads in flight per lane) up to rank 4
+#define WCE_LR_LANE_UNROLL 4
+#endif
+template <int R>
+__global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    constexpr int NO = R * (R - 1) / 2;   // strictly-lower Gram entries
+    const int64_t units = a.split ? a.n * a.nblk : a.n;
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= units) return;
+    const int64_t f = a.split ? g / a.nblk : g;
+    const int b = a.split ? (int)(g - f * a.nblk) : 0;
+    const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
+    const double ac = st->acoef, bc = st->bcoef;
+    const uint64_t xm = st->xmask;
+    const double2 *__restrict__ P = reinterpret_cast<const double2 *>(st->Pk);
+    const double2 *__restrict__ U = reinterpret_cast<const double2 *>(st->U);
+    double gd[R];        // Gamma_ii (real)
+    double2 go[NO > 0 ? NO : 1];   // Gamma_ij, i > j, at i (i - 1) / 2 + j
+    double2 bt[R];       // beta = G^H rx
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        gd[i] = 0.0;
+        bt[i] = make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int e = 0; e < NO; ++e) go[e] = make_double2(0.0, 0.0);
+    bool cplx = false;
+    constexpr int UN = R <= 4 ? WCE_LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
+#pragma unroll UN
+    for (int k = 0; k < NSC; ++k) {
+        double2 x = ld2(a.tx, base + k);
+        const double2 r = ld2(a.rx, base + k);
+        if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+        cplx |= x.y != 0.0;
+        const double w = fma(x.x, x.x, x.y * x.y);
+        const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+        const double2 *Pk = P + k * LRL_NP;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const double2 u = U[k * CLD + i];   // beta_i += conj(u) v
+            bt[i].x = fma(u.x, v.x, fma(u.y, v.y, bt[i].x));
+            bt[i].y = fma(u.x, v.y, fma(-u.y, v.x, bt[i].y));
+            gd[i] = fma(w, Pk[i * (i + 1) / 2 + i].x, gd[i]);
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                const double2 pe = Pk[i * (i + 1) / 2 + j];
+                double2 &o = go[i * (i - 1) / 2 + j];
+                o.x = fma(w, pe.x, o.x);
+                o.y = fma(w, pe.y, o.y);
+            }
+        }
+    }
+    // A = a Gamma + b I = L L^H (lower L in place: ld = 1 / L_ii, lo = L_ij)
+    double ld[R];
+    double2 lo[NO > 0 ? NO : 1];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+            double2 acc = cscale(go[i * (i - 1) / 2 + j], ac);
+#pragma unroll
+            for (int m = 0; m < j; ++m) {   // acc -= L_im conj(L_jm)
+                const double2 x = lo[i * (i - 1) / 2 + m], y = lo[j * (j - 1) / 2 + m];
+                acc.x = fma(-x.x, y.x, fma(-x.y, y.y, acc.x));
+                acc.y = fma(-x.y, y.x, fma(x.x, y.y, acc.y));
+            }
+            lo[i * (i - 1) / 2 + j] = cscale(acc, ld[j]);
+        }
+        double d = fma(ac, gd[i], bc);
+#pragma unroll
+        for (int m = 0; m < i; ++m) {
+            const double2 x = lo[i * (i - 1) / 2 + m];
+            d = fma(-x.x, x.x, fma(-x.y, x.y, d));
+        }
+        ld[i] = 1.0 / sqrt(d);
+    }
+    // t = L^-H L^-1 beta
+    double2 t[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        double2 acc = bt[i];
+#pragma unroll
+        for (int m = 0; m < i; ++m) acc = csub(acc, cmul(lo[i * (i - 1) / 2 + m], t[m]));
+        t[i] = cscale(acc, ld[i]);
+    }
+#pragma unroll
+    for (int i = R - 1; i >= 0; --i) {
+        double2 acc = t[i];
+#pragma unroll
+        for (int m = i + 1; m < R; ++m) acc = csub(acc, cmul(cconj(lo[m * (m - 1) / 2 + i]), t[m]));
+        t[i] = cscale(acc, ld[i]);
+    }
+    if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
+        double2 c[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) c[i] = make_double2(0.0, 0.0);
+#pragma unroll 2
+        for (int k = 0; k < NSC; ++k) {
+            double2 x = ld2(a.tx, base + k);
+            const double2 r = ld2(a.rx, base + k);
+            if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+            double2 y = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int j = 0; j < R; ++j) y = cadd(y, cmul(U[k * CLD + j], t[j]));
+            const double2 rho = csub(r, cscale(cmul(x, y), ac));
+            const double2 v = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
+#pragma unroll
+            for (int j = 0; j < R; ++j) c[j] = cadd(c[j], cmul(cconj(U[k * CLD + j]), v));
+        }
+        const double rb = 1.0 / bc;
+#pragma unroll
+        for (int i = 0; i < R; ++i) t[i] = cadd(t[i], cscale(c[i], rb));
+    }
+    double *W = a.w + 2 * g * a.ws;
+#pragma unroll 4
+    for (int k = 0; k < NSC; ++k) {
+        double2 y = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double2 u = U[k * CLD + j];
+            y.x = fma(u.x, t[j].x, fma(-u.y, t[j].y, y.x));
+            y.y = fma(u.x, t[j].y, fma(u.y, t[j].x, y.y));
+        }
+        st2(W, k, y);
+    }
+}
+
 // H[f] = (((X[4f] + X[4f+1]) + X[4f+2]) + X[4f+3]) / 4  (WiFi_channel_estimation_PS_MMSE.m:35)
 __global__ __launch_bounds__(256) void avg_blocks_kernel(const double *__restrict__ X, int64_t xs, double *H, int64_t hs,
                                                          int64_t n)
@@ -2226,7 +2373,10 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 
 // A/B kernel variants, process-wide (wce_debug_set_variant): lets one process
 // time two kernels on the same buffers, interleaved.  Defaults = the product.
-static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, 0};
+#ifndef WCE_LR_WAVE_ONLY   // build-time default of WCE_VARIANT_LR (A/B builds: 1 = every rank on mmse_lr_kernel)
+#define WCE_LR_WAVE_ONLY 0
+#endif
+static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, WCE_LR_WAVE_ONLY};
 int set_variant(int which, int value)
 {
     if (which < 0 || which >= WCE_VARIANT_COUNT || value < 0 || value > 15) return WCE_EINVAL;
@@ -2333,14 +2483,28 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     return hip_status(hipGetLastError());
 }
 
-int launch_mmse_lr(const State *st, int k0, const SolveArgs &a, void *stream)
+int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
     const int64_t waves = a.split ? a.n * a.nblk : a.n;
     if (waves > 0x7fffffffll) return WCE_EINVAL;
     if (a.nblk > 1 && !a.split) return WCE_EINVAL;
-    const dim3 g((unsigned)waves), b(64);
     hipStream_t s = (hipStream_t)stream;
+    if (rank >= 1 && rank <= LRL_RMAX && variant(WCE_VARIANT_LR) == 0) {
+        const dim3 gl((unsigned)((waves + 255) / 256)), bl(256);
+        switch (rank) {
+        case 1: hipLaunchKernelGGL(mmse_lr_lane_kernel<1>, gl, bl, 0, s, st, a); break;
+        case 2: hipLaunchKernelGGL(mmse_lr_lane_kernel<2>, gl, bl, 0, s, st, a); break;
+        case 3: hipLaunchKernelGGL(mmse_lr_lane_kernel<3>, gl, bl, 0, s, st, a); break;
+        case 4: hipLaunchKernelGGL(mmse_lr_lane_kernel<4>, gl, bl, 0, s, st, a); break;
+        case 5: hipLaunchKernelGGL(mmse_lr_lane_kernel<5>, gl, bl, 0, s, st, a); break;
+        case 6: hipLaunchKernelGGL(mmse_lr_lane_kernel<6>, gl, bl, 0, s, st, a); break;
+        case 7: hipLaunchKernelGGL(mmse_lr_lane_kernel<7>, gl, bl, 0, s, st, a); break;
+        default: hipLaunchKernelGGL(mmse_lr_lane_kernel<8>, gl, bl, 0, s, st, a); break;
+        }
+        return hip_status(hipGetLastError());
+    }
+    const dim3 g((unsigned)waves), b(64);
     switch (k0) {
     case 0: hipLaunchKernelGGL(mmse_lr_kernel<0>, g, b, 0, s, st, a); break;
     case 1: hipLaunchKernelGGL(mmse_lr_kernel<1>, g, b, 0, s, st, a); break;

@@ -419,6 +419,8 @@ int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
         while (r < n && lam[ord[r]] > kCovRankTol * lmax && lmax > 0.0L) r++;
         std::memset(st->U, 0, sizeof(st->U));
         std::memset(st->UT, 0, sizeof(st->UT));
+        std::memset(st->Pk, 0, sizeof(st->Pk));
+        std::vector<cld> Ul((size_t)n * LRL_RMAX);   // U[k][j], j < LRL_RMAX, in 80 bits
         for (int j = 0; j < r; j++) {
             const long double sl = sqrtl(lam[ord[j]]);
             for (int k = 0; k < n; k++) {
@@ -427,8 +429,20 @@ int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
                 u = u * mk(sl, 0.0L);
                 st->U[2 * (k * CLD + j)] = st->UT[2 * (j * CLD + k)] = (double)__real__ u;
                 st->U[2 * (k * CLD + j) + 1] = st->UT[2 * (j * CLD + k) + 1] = (double)__imag__ u;
+                if (j < LRL_RMAX) Ul[(size_t)k * LRL_RMAX + j] = u;
             }
         }
+        if (r <= LRL_RMAX)   // P_k[i][j] = conj(U[k][i]) U[k][j], i >= j (mmse_lr_lane_kernel)
+            for (int k = 0; k < n; k++)
+                for (int i = 0; i < r; i++)
+                    for (int j = 0; j <= i; j++) {
+                        cld ui = Ul[(size_t)k * LRL_RMAX + i];
+                        __imag__ ui = -__imag__ ui;
+                        const cld v = ui * Ul[(size_t)k * LRL_RMAX + j];
+                        const int e = (k * LRL_NP + i * (i + 1) / 2 + j) * 2;
+                        st->Pk[e] = (double)__real__ v;
+                        st->Pk[e + 1] = i == j ? 0.0 : (double)__imag__ v;
+                    }
         st->cov_rank = r;
         st->cov_lmax = (double)(n * lmax);
         st->cov_lmin = r ? (double)(n * lam[ord[r - 1]]) : 0.0;

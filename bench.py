@@ -947,11 +947,15 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
 
 def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
     """WCE_MMSE_COV with a power-delay profile of L taps (rank L, the channel
-    model of SURVEY 8(d)): the low-rank Gram path (mmse_lr_kernel), which
-    meets 1e-10 where the dense Ryy solve cannot.  Per-frame
-    rate on the headline's frames, beside the dense path forced on the same
-    ctx (wce_debug_set_cov_path) for comparison."""
+    model of SURVEY 8(d)): the low-rank Gram path, which meets 1e-10 where
+    the dense Ryy solve cannot.  Ranks 1..8 run one frame per
+    lane (mmse_lr_lane_kernel: HBM-bound, 2,544 B per frame = tx + rx block
+    in, H out), higher ranks one frame per wave (mmse_lr_kernel).  Per-frame
+    rate on the headline's frames, beside the wave kernel (ranks <= 8) and
+    the dense path forced on the same ctx (wce_debug_set_variant /
+    wce_debug_set_cov_path) for comparison."""
     s = stream.handle
+    lib = wce.load()
     H = wce.DeviceArray((B, N))
     fr = wce.Context.frames(tx, rx, B)
     o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
@@ -966,13 +970,29 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
         for _ in range(2):
             f()
         t = time_events(wce, stream, f, reps)
+        lane = lr and 1 <= r <= 8
+        k0 = min((N - r) // 8, 6)
+        leg = {"rank": r, "path": "low-rank" if lr else "dense",
+               "kernel": f"mmse_lr_lane_kernel<{r}>" if lane else
+               (f"mmse_lr_kernel<{k0}>" if lr else "mmse_solve_kernel<false> + H = C W"),
+               "ms_per_step": t, "frames_per_s": B / (t * 1e-3)}
+        if lane:
+            leg["achieved_GBs"] = 3 * N * 16 * B / (t * 1e-3) / 1e9
+            leg["hbm_frac"] = leg["achieved_GBs"] / PEAK_HBM_GBS
+            assert lib.wce_debug_set_variant(3, 1) == 0    # the same ranks one frame per wave
+            try:
+                for _ in range(2):
+                    f()
+                tw = time_events(wce, stream, f, reps)
+            finally:
+                assert lib.wce_debug_set_variant(3, 0) == 0
+            leg.update({"wave_kernel": f"mmse_lr_kernel<{k0}>", "wave_kernel_ms_per_step": tw})
         c.set_cov_path(1)
         for _ in range(2):
             f()
         td = time_events(wce, stream, f, reps)
-        out[f"L{L}"] = {"rank": r, "path": "low-rank" if lr else "dense", "ms_per_step": t,
-                        "frames_per_s": B / (t * 1e-3), "dense_forced_ms_per_step": td,
-                        "dense_forced_frames_per_s": B / (td * 1e-3)}
+        leg.update({"dense_forced_ms_per_step": td, "dense_forced_frames_per_s": B / (td * 1e-3)})
+        out[f"L{L}"] = leg
         del c
     return out
 

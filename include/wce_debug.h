@@ -36,7 +36,10 @@ int wce_debug_set_flat_chunk(long long frames);
  * blocks; 1 = the same uncapped; 2 = one element per thread, default).
  * which 2: REF PS_MMSE with LS outputs in one call (0 = one element per
  * thread, ref_ls_elem_kernel, default; 1 = the wave-per-frame fused solve).
- * Process-wide; every variant gives bit-identical results (tests check it). */
+ * which 3: WCE_MMSE_COV low-rank path (0 = ranks 1..8 one frame per lane,
+ * mmse_lr_lane_kernel, default; 1 = every rank one frame per wave).
+ * Process-wide; variants 0..2 give bit-identical results, variant 3's two
+ * kernels sum in different orders and agree to rounding (tests check both). */
 int wce_debug_set_variant(int which, int value);
 /* WCE_MMSE_COV solve form for A/B and accuracy probes: 0 = as the state
  * chose (default), 1 = always the dense Ryy solve, 2 = always the low-rank

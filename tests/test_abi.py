@@ -134,8 +134,9 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
     ref = (F @ R.astype(np.clongdouble) @ F.conj().T).astype(np.complex128)
     assert np.max(np.abs(C - ref)) / np.max(np.abs(ref)) < 1e-14
     # State tail: a, b, ow2, xmask, mode, magic, then the low-rank factor
-    # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0
-    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8)]
+    # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0 and
+    # the lane kernel's P_k (53 x 36 complex)
+    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 53 * 36 * 16)]
     a, b, ow2 = t[-40:-16].view(np.float64)
     mode, magic = t[-8:].view(np.int32)
     assert (a, b, ow2, mode, magic) == (1.0, inp["ow2"], inp["ow2"], wce.MMSE_COV, 0x80211)

@@ -217,3 +217,43 @@ def test_profiling_entry_rejects_lowrank(gpu_wce, golden):
     W = gpu_wce.DeviceArray((B, N))
     with pytest.raises(gpu_wce.WceError):
         ctx.mmse_solve(ctx.frames(tx, rx, B), W)
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
+    """Ranks 1..8 run one frame per lane (mmse_lr_lane_kernel): BPSK and QPSK
+    frames against the long double solve, and against the wave-per-frame Gram
+    kernel (variant WCE_VARIANT_LR = 1) on the same frames, C and MATLAB
+    semantics, 515 frames (a partial last workgroup of lanes)."""
+    inp = golden["inputs"]
+    lib = gpu_wce.load()
+    R = pdp_rhh(L, 0.4)
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    assert ctx.cov_info()[:2] == (L, True)
+    B = 515
+    tx, rx = synth(ctx, gpu_wce, B, seed=0x1A0 + L)
+    rng = np.random.default_rng(L)
+    txq = constellation(rng, "qpsk", tx.shape)
+    txq[:, :, 26] = 0
+    rxq = channel_frames(rng, txq, inp["ow2"])
+    C = c_ld(oracle, R)
+    try:
+        for t, r in ((tx, rx), (txq, rxq)):
+            got = {}
+            for v in (0, 1):
+                assert lib.wce_debug_set_variant(3, v) == 0
+                got[v] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE)["ps_mmse"]
+                got[v, "m"] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE, semantics=gpu_wce.SEM_MATLAB)["ps_mmse"]
+            sel = np.r_[0:30, B - 10:B]
+            err = normrel(got[0][sel], solve_ld(oracle, C, t[sel, 0], r[sel, 0], inp["ow2"]))
+            assert err.max() < TOL, err.max()
+            per = [solve_ld(oracle, C, t[sel, b], r[sel, b], inp["ow2"]) for b in range(4)]
+            errm = normrel(got[0, "m"][sel], (((per[0] + per[1]) + per[2]) + per[3]) / 4)
+            assert errm.max() < TOL, errm.max()
+            # the two kernels: the same algebra summed in another order (rank 1
+            # carries the most rounding, ~1e-11 from the long double solve, r03 probe)
+            d = max(normrel(got[0], got[1]).max(), normrel(got[0, "m"], got[1, "m"]).max())
+            print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, lane vs wave kernel {d:.2e}")
+            assert d < TOL
+    finally:
+        assert lib.wce_debug_set_variant(3, 0) == 0
