@@ -1919,19 +1919,105 @@ __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *
 // No LDS, no cross-lane traffic; the frame's loads and stores are 16 B per
 // lane at the frame stride, consecutive k filling each 64-B sector in turn.
 // ---------------------------------------------------------------------
-#ifndef WCE_LR_LANE_UNROLL   // subcarriers per pass-1 iteration (loads in flight per lane) up to rank 4
+// Memory, two forms (launch_mmse_lr picks by batch size):
+//  - direct (STAGED = false): each lane loads its frame's 16 B per subcarrier
+//    and stores H the same way, 4 subcarriers (one 64-B sector) per unrolled
+//    step.  Best while the grid is small: 0.052 ms at rank 4 for 65,536
+//    frames.  But every instruction touches 64 sectors, and at 1,048,576
+//    frames the CU's 16 resident waves keep ~130 KB of partly-read sectors
+//    live, past L1 and close to an XCD's L2: 1.28 ms there (2.1 TB/s).
+//  - staged (STAGED = true): the wave moves its 64 frames through LDS in
+//    chunks of 4 subcarriers, coalesced (16 frames x 64 B per instruction),
+//    each chunk's loads issued one chunk ahead into registers; every lane then
+//    reads its own frame's 4 values from LDS (row stride 5 complex:
+//    conflict-free), and H goes out the same way in reverse.  0.93 ms at
+//    1,048,576 frames, but 0.061 ms at 65,536 (the staging's fixed cost).
+#ifndef WCE_LR_LANE_UNROLL   // direct form: subcarriers per pass-1 step (loads in flight per lane) up to rank 4
 #define WCE_LR_LANE_UNROLL 4
 #endif
-template <int R>
-__global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a)
+constexpr int LRL_KC = 4;                         // subcarriers per chunk
+constexpr int LRL_NCH = (NSC + LRL_KC - 1) / LRL_KC;   // 14 chunks (k = 52..55: only 52 is live)
+constexpr int LRL_LS = 5;                         // LDS row stride (complex) per frame
+struct LrLaneLds {
+    double2 x[64 * LRL_LS];
+    double2 r[64 * LRL_LS];
+};
+// the wave's chunk c of tx / rx as 4 x 16 B per lane: element e = lane + 64 m
+// is frame e >> 2 of the wave, subcarrier 4 c + (e & 3)
+struct LrChunk {
+    double2 x[4], r[4];
+};
+__device__ __forceinline__ void lrl_load(LrChunk &q, const SolveArgs &a, const int64_t (&eb)[4], uint32_t live,
+                                         int c, int lane)
+{
+    const int k = LRL_KC * c + (lane & 3);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const bool ok = ((live >> m) & 1u) && k < NSC;
+        q.x[m] = ok ? ld2(a.tx, eb[m] + k) : make_double2(0.0, 0.0);
+        q.r[m] = ok ? ld2(a.rx, eb[m] + k) : make_double2(0.0, 0.0);
+    }
+}
+__device__ __forceinline__ void lrl_stage(LrLaneLds &s, const LrChunk &q, int lane)
+{
+    asm volatile("" ::: "memory");   // after the previous chunk's reads (LDS runs a wave's ops in order)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int fl = (lane >> 2) + 16 * m;
+        s.x[fl * LRL_LS + (lane & 3)] = q.x[m];
+        s.r[fl * LRL_LS + (lane & 3)] = q.r[m];
+    }
+    asm volatile("" ::: "memory");
+}
+// pass-1 / correction-pass sweep over k: f(k, x_k, rx_k) in order k = 0..52
+template <bool STAGED, int UN, typename Fn>
+__device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, const int64_t (&eb)[4], uint32_t live,
+                                          int64_t base, bool own, int lane, Fn fn)
+{
+    if constexpr (STAGED) {
+        LrChunk q;
+        lrl_load(q, a, eb, live, 0, lane);
+#pragma unroll 1
+        for (int c = 0; c < LRL_NCH; ++c) {
+            lrl_stage(*sp, q, lane);
+            if (c + 1 < LRL_NCH) lrl_load(q, a, eb, live, c + 1, lane);   // one chunk ahead
+#pragma unroll
+            for (int kk = 0; kk < LRL_KC; ++kk) {
+                const int k = LRL_KC * c + kk;
+                if (kk > 0 && k >= NSC) break;   // (uniform) the last chunk holds k = 52 only
+                fn(k, sp->x[lane * LRL_LS + kk], sp->r[lane * LRL_LS + kk]);
+            }
+        }
+    } else {
+#pragma unroll UN
+        for (int k = 0; k < NSC; ++k)
+            fn(k, own ? ld2(a.tx, base + k) : make_double2(0.0, 0.0), own ? ld2(a.rx, base + k) : make_double2(0.0, 0.0));
+    }
+}
+template <int R, bool STAGED>
+__device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const SolveArgs &a, LrLaneLds *sp)
 {
     constexpr int NO = R * (R - 1) / 2;   // strictly-lower Gram entries
+    const int lane = threadIdx.x & 63;
     const int64_t units = a.split ? a.n * a.nblk : a.n;
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= units) return;
-    const int64_t f = a.split ? g / a.nblk : g;
-    const int b = a.split ? (int)(g - f * a.nblk) : 0;
-    const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
+    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);   // the wave's first (frame, block) unit
+    const int64_t g = g0 + lane;
+    const bool own = g < units;
+    if (!STAGED && !own) return;   // (the staged form's whole wave stages and stores)
+    auto ubase = [&](int64_t u) {   // (frame, block) unit -> element offset of its block
+        const int64_t f = a.split ? u / a.nblk : u;
+        const int b = a.split ? (int)(u - f * a.nblk) : 0;
+        return f * a.fs + (int64_t)(a.blk + b) * a.bs;
+    };
+    const int64_t base = own ? ubase(g) : 0;
+    int64_t eb[4];   // STAGED: the unit element lane + 64 m stages
+    uint32_t live = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int64_t u = g0 + (lane >> 2) + 16 * m;
+        live |= (u < units ? 1u : 0u) << m;
+        eb[m] = STAGED && u < units ? ubase(u) : 0;
+    }
     const double ac = st->acoef, bc = st->bcoef;
     const uint64_t xm = st->xmask;
     const double2 *__restrict__ P = reinterpret_cast<const double2 *>(st->Pk);
@@ -1948,10 +2034,7 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
     for (int e = 0; e < NO; ++e) go[e] = make_double2(0.0, 0.0);
     bool cplx = false;
     constexpr int UN = R <= 4 ? WCE_LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
-#pragma unroll UN
-    for (int k = 0; k < NSC; ++k) {
-        double2 x = ld2(a.tx, base + k);
-        const double2 r = ld2(a.rx, base + k);
+    lrl_sweep<STAGED, UN>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
         if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
         cplx |= x.y != 0.0;
         const double w = fma(x.x, x.x, x.y * x.y);
@@ -1971,7 +2054,7 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
                 o.y = fma(w, pe.y, o.y);
             }
         }
-    }
+    });
     // A = a Gamma + b I = L L^H (lower L in place: ld = 1 / L_ii, lo = L_ij)
     double ld[R];
     double2 lo[NO > 0 ? NO : 1];
@@ -2013,13 +2096,10 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
         t[i] = cscale(acc, ld[i]);
     }
     if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
-        double2 c[R];
+        double2 cc[R];
 #pragma unroll
-        for (int i = 0; i < R; ++i) c[i] = make_double2(0.0, 0.0);
-#pragma unroll 2
-        for (int k = 0; k < NSC; ++k) {
-            double2 x = ld2(a.tx, base + k);
-            const double2 r = ld2(a.rx, base + k);
+        for (int i = 0; i < R; ++i) cc[i] = make_double2(0.0, 0.0);
+        lrl_sweep<STAGED, 2>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
             if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
             double2 y = make_double2(0.0, 0.0);
 #pragma unroll
@@ -2027,15 +2107,14 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
             const double2 rho = csub(r, cscale(cmul(x, y), ac));
             const double2 v = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
 #pragma unroll
-            for (int j = 0; j < R; ++j) c[j] = cadd(c[j], cmul(cconj(U[k * CLD + j]), v));
-        }
+            for (int j = 0; j < R; ++j) cc[j] = cadd(cc[j], cmul(cconj(U[k * CLD + j]), v));
+        });
         const double rb = 1.0 / bc;
 #pragma unroll
-        for (int i = 0; i < R; ++i) t[i] = cadd(t[i], cscale(c[i], rb));
+        for (int i = 0; i < R; ++i) t[i] = cadd(t[i], cscale(cc[i], rb));
     }
-    double *W = a.w + 2 * g * a.ws;
-#pragma unroll 4
-    for (int k = 0; k < NSC; ++k) {
+    // H_k = U_k s
+    auto hk = [&](int k) {
         double2 y = make_double2(0.0, 0.0);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -2043,8 +2122,45 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
             y.x = fma(u.x, t[j].x, fma(-u.y, t[j].y, y.x));
             y.y = fma(u.x, t[j].y, fma(u.y, t[j].x, y.y));
         }
-        st2(W, k, y);
+        return y;
+    };
+    if constexpr (STAGED) {   // each lane its frame's 4 subcarriers of a chunk into LDS, then 16 frames x 64 B per store
+        int64_t ob[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ob[m] = (g0 + (lane >> 2) + 16 * m) * a.ws;
+#pragma unroll 1
+        for (int c = 0; c < LRL_NCH; ++c) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int kk = 0; kk < LRL_KC; ++kk) {
+                const int k = LRL_KC * c + kk;
+                if (kk > 0 && k >= NSC) break;
+                sp->x[lane * LRL_LS + kk] = hk(k);
+            }
+            asm volatile("" ::: "memory");
+            const int k = LRL_KC * c + (lane & 3);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const double2 y = sp->x[((lane >> 2) + 16 * m) * LRL_LS + (lane & 3)];
+                if (((live >> m) & 1u) && k < NSC) st2(a.w, ob[m] + k, y);
+            }
+        }
+    } else {
+        double *W = a.w + 2 * g * a.ws;
+#pragma unroll 4
+        for (int k = 0; k < NSC; ++k) st2(W, k, hk(k));
     }
+}
+template <int R>
+__global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    lr_lane_body<R, false>(st, a, nullptr);   // (no LDS)
+}
+template <int R>
+__global__ __launch_bounds__(64) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    __shared__ LrLaneLds s;
+    lr_lane_body<R, true>(st, a, &s);
 }
 
 // H[f] = (((X[4f] + X[4f+1]) + X[4f+2]) + X[4f+3]) / 4  (WiFi_channel_estimation_PS_MMSE.m:35)
@@ -2373,6 +2489,9 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 
 // A/B kernel variants, process-wide (wce_debug_set_variant): lets one process
 // time two kernels on the same buffers, interleaved.  Defaults = the product.
+#ifndef WCE_LR_STAGE_FROM   // mmse_lr_lane_kernel: the LDS-staged form past this many (frame, block) units
+#define WCE_LR_STAGE_FROM 262144
+#endif
 #ifndef WCE_LR_WAVE_ONLY   // build-time default of WCE_VARIANT_LR (A/B builds: 1 = every rank on mmse_lr_kernel)
 #define WCE_LR_WAVE_ONLY 0
 #endif
@@ -2490,18 +2609,22 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
     if (waves > 0x7fffffffll) return WCE_EINVAL;
     if (a.nblk > 1 && !a.split) return WCE_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    if (rank >= 1 && rank <= LRL_RMAX && variant(WCE_VARIANT_LR) == 0) {
-        const dim3 gl((unsigned)((waves + 255) / 256)), bl(256);
+    const int lv = variant(WCE_VARIANT_LR);
+    if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
+        // direct form up to 262,144 units (the grid fits the CUs' wave slots a
+        // few times over), the LDS-staged form past it (profiles/r03_ab_lowrank_lane.txt)
+        const bool staged = lv == 3 || (lv == 0 && waves > (int64_t)WCE_LR_STAGE_FROM);
+        const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((waves + 255) / 256)), bd(256);
+#define WCE_LRL(RR)                                                                                         \
+    case RR:                                                                                                \
+        if (staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a);               \
+        else hipLaunchKernelGGL(mmse_lr_lane_kernel<RR>, gd, bd, 0, s, st, a);                              \
+        break;
         switch (rank) {
-        case 1: hipLaunchKernelGGL(mmse_lr_lane_kernel<1>, gl, bl, 0, s, st, a); break;
-        case 2: hipLaunchKernelGGL(mmse_lr_lane_kernel<2>, gl, bl, 0, s, st, a); break;
-        case 3: hipLaunchKernelGGL(mmse_lr_lane_kernel<3>, gl, bl, 0, s, st, a); break;
-        case 4: hipLaunchKernelGGL(mmse_lr_lane_kernel<4>, gl, bl, 0, s, st, a); break;
-        case 5: hipLaunchKernelGGL(mmse_lr_lane_kernel<5>, gl, bl, 0, s, st, a); break;
-        case 6: hipLaunchKernelGGL(mmse_lr_lane_kernel<6>, gl, bl, 0, s, st, a); break;
-        case 7: hipLaunchKernelGGL(mmse_lr_lane_kernel<7>, gl, bl, 0, s, st, a); break;
-        default: hipLaunchKernelGGL(mmse_lr_lane_kernel<8>, gl, bl, 0, s, st, a); break;
+            WCE_LRL(1) WCE_LRL(2) WCE_LRL(3) WCE_LRL(4) WCE_LRL(5) WCE_LRL(6) WCE_LRL(7)
+            default: WCE_LRL(8)
         }
+#undef WCE_LRL
         return hip_status(hipGetLastError());
     }
     const dim3 g((unsigned)waves), b(64);

@@ -224,7 +224,9 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
     """Ranks 1..8 run one frame per lane (mmse_lr_lane_kernel): BPSK and QPSK
     frames against the long double solve, and against the wave-per-frame Gram
     kernel (variant WCE_VARIANT_LR = 1) on the same frames, C and MATLAB
-    semantics, 515 frames (a partial last workgroup of lanes)."""
+    semantics, 515 frames (a partial last wave of lanes).  The lane kernel's
+    direct and LDS-staged forms (variants 2, 3; the batch size picks one)
+    agree to rounding."""
     inp = golden["inputs"]
     lib = gpu_wce.load()
     R = pdp_rhh(L, 0.4)
@@ -240,10 +242,13 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
     try:
         for t, r in ((tx, rx), (txq, rxq)):
             got = {}
-            for v in (0, 1):
+            for v in (0, 1, 3):
                 assert lib.wce_debug_set_variant(3, v) == 0
                 got[v] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE)["ps_mmse"]
                 got[v, "m"] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE, semantics=gpu_wce.SEM_MATLAB)["ps_mmse"]
+            # direct vs LDS-staged form: same sums in the same order (the compiler may
+            # contract a product into an FMA differently in the two instantiations)
+            assert max(normrel(got[0], got[3]).max(), normrel(got[0, "m"], got[3, "m"]).max()) < 1e-12
             sel = np.r_[0:30, B - 10:B]
             err = normrel(got[0][sel], solve_ld(oracle, C, t[sel, 0], r[sel, 0], inp["ow2"]))
             assert err.max() < TOL, err.max()
