@@ -1923,16 +1923,16 @@ __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *
 //  - direct (STAGED = false): each lane loads its frame's 16 B per subcarrier
 //    and stores H the same way, 4 subcarriers (one 64-B sector) per unrolled
 //    step.  Best while the grid is small: 0.052 ms at rank 4 for 65,536
-//    frames.  But every instruction touches 64 sectors, and at 1,048,576
-//    frames the CU's 16 resident waves keep ~130 KB of partly-read sectors
-//    live, past L1 and close to an XCD's L2: 1.28 ms there (2.1 TB/s).
+//    frames.  But every instruction touches 64 sectors, and from 131,072
+//    frames on the resident waves keep enough partly-read sectors live to
+//    thrash the caches: 0.143 ms at 131,072, 1.28 ms at 1,048,576 (2.1 TB/s).
 //  - staged (STAGED = true): the wave moves its 64 frames through LDS in
 //    chunks of 4 subcarriers, coalesced (16 frames x 64 B per instruction),
 //    each chunk's loads issued one chunk ahead into registers; every lane then
 //    reads its own frame's 4 values from LDS (row stride 5 complex:
-//    conflict-free), and H goes out the same way in reverse.  0.93 ms at
-//    1,048,576 frames, but 0.061 ms at 65,536 (the staging's fixed cost).
-#ifndef WCE_LR_LANE_UNROLL   // direct form: subcarriers per pass-1 step (loads in flight per lane) up to rank 4
+//    conflict-free), and H goes out the same way in reverse.  0.110 ms at
+//    131,072 frames, 0.95 ms at 1,048,576, but 0.061 ms at 65,536.
+#ifndef WCE_LR_LANE_UNROLL   // direct form without the look-ahead: subcarriers per step up to rank 4
 #define WCE_LR_LANE_UNROLL 4
 #endif
 constexpr int LRL_KC = 4;                         // subcarriers per chunk
@@ -1989,21 +1989,30 @@ __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, con
             }
         }
     } else {
+#ifdef WCE_LR_ABLATE_LOADS   // timing-only build: one sector of the frame, reused for every k
+        const double2 x0 = ld2(a.tx, base), r0 = ld2(a.rx, base);
+#pragma unroll UN
+        for (int k = 0; k < NSC; ++k) fn(k, x0, r0);
+#else
 #pragma unroll UN
         for (int k = 0; k < NSC; ++k)
             fn(k, own ? ld2(a.tx, base + k) : make_double2(0.0, 0.0), own ? ld2(a.rx, base + k) : make_double2(0.0, 0.0));
+#endif
     }
 }
 template <int R, bool STAGED>
-__device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const SolveArgs &a, LrLaneLds *sp)
+__device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const SolveArgs &a, LrLaneLds *sp,
+                                             int fpw)
 {
     constexpr int NO = R * (R - 1) / 2;   // strictly-lower Gram entries
     const int lane = threadIdx.x & 63;
     const int64_t units = a.split ? a.n * a.nblk : a.n;
-    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);   // the wave's first (frame, block) unit
+    // the wave's first (frame, block) unit; the direct form may run fpw < 64
+    // units per wave (lanes past fpw idle) to put more waves on a small batch
+    const int64_t g0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * fpw;
     const int64_t g = g0 + lane;
-    const bool own = g < units;
-    if (!STAGED && !own) return;   // (the staged form's whole wave stages and stores)
+    const bool own = lane < fpw && g < units;
+    if (!STAGED && !own) return;   // (a staging wave moves all 64 lanes' data)
     auto ubase = [&](int64_t u) {   // (frame, block) unit -> element offset of its block
         const int64_t f = a.split ? u / a.nblk : u;
         const int b = a.split ? (int)(u - f * a.nblk) : 0;
@@ -2015,7 +2024,7 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         const int64_t u = g0 + (lane >> 2) + 16 * m;
-        live |= (u < units ? 1u : 0u) << m;
+        live |= ((lane >> 2) + 16 * m < fpw && u < units ? 1u : 0u) << m;
         eb[m] = STAGED && u < units ? ubase(u) : 0;
     }
     const double ac = st->acoef, bc = st->bcoef;
@@ -2147,20 +2156,24 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
         }
     } else {
         double *W = a.w + 2 * g * a.ws;
+#ifdef WCE_LR_ABLATE_STORES   // timing-only build: H_0 alone
+        st2(W, 0, hk(0));
+#else
 #pragma unroll 4
         for (int k = 0; k < NSC; ++k) st2(W, k, hk(k));
+#endif
     }
 }
 template <int R>
-__global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a)
+__global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a, int fpw)
 {
-    lr_lane_body<R, false>(st, a, nullptr);   // (no LDS)
+    lr_lane_body<R, false>(st, a, nullptr, fpw);   // (no LDS)
 }
 template <int R>
 __global__ __launch_bounds__(64) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ LrLaneLds s;
-    lr_lane_body<R, true>(st, a, &s);
+    lr_lane_body<R, true>(st, a, &s, 64);
 }
 
 // H[f] = (((X[4f] + X[4f+1]) + X[4f+2]) + X[4f+3]) / 4  (WiFi_channel_estimation_PS_MMSE.m:35)
@@ -2489,8 +2502,14 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 
 // A/B kernel variants, process-wide (wce_debug_set_variant): lets one process
 // time two kernels on the same buffers, interleaved.  Defaults = the product.
+#ifndef WCE_LR_FPW   // mmse_lr_lane_kernel (direct): units per wave at or below WCE_LR_FPW_BELOW units
+#define WCE_LR_FPW 64
+#endif
+#ifndef WCE_LR_FPW_BELOW
+#define WCE_LR_FPW_BELOW 131072
+#endif
 #ifndef WCE_LR_STAGE_FROM   // mmse_lr_lane_kernel: the LDS-staged form past this many (frame, block) units
-#define WCE_LR_STAGE_FROM 262144
+#define WCE_LR_STAGE_FROM 98304   // rank 4: direct 51.6 vs staged ~60 us at 65,536; 142.6 vs 109.5 at 131,072
 #endif
 #ifndef WCE_LR_WAVE_ONLY   // build-time default of WCE_VARIANT_LR (A/B builds: 1 = every rank on mmse_lr_kernel)
 #define WCE_LR_WAVE_ONLY 0
@@ -2611,14 +2630,18 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
     hipStream_t s = (hipStream_t)stream;
     const int lv = variant(WCE_VARIANT_LR);
     if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
-        // direct form up to 262,144 units (the grid fits the CUs' wave slots a
-        // few times over), the LDS-staged form past it (profiles/r03_ab_lowrank_lane.txt)
+        // direct form up to 98,304 units, the LDS-staged form past it: the direct
+        // form's scattered sectors start to thrash the caches at 131,072
+        // (profiles/r03_ab_lowrank_lane.txt)
         const bool staged = lv == 3 || (lv == 0 && waves > (int64_t)WCE_LR_STAGE_FROM);
-        const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((waves + 255) / 256)), bd(256);
+        // direct form: fewer units per wave on a small batch (latency-bound at one wave per SIMD)
+        const int fpw = waves <= (int64_t)WCE_LR_FPW_BELOW ? WCE_LR_FPW : 64;
+        const int64_t dw = (waves + fpw - 1) / fpw;
+        const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((dw + 3) / 4)), bd(256);
 #define WCE_LRL(RR)                                                                                         \
     case RR:                                                                                                \
         if (staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a);               \
-        else hipLaunchKernelGGL(mmse_lr_lane_kernel<RR>, gd, bd, 0, s, st, a);                              \
+        else hipLaunchKernelGGL(mmse_lr_lane_kernel<RR>, gd, bd, 0, s, st, a, fpw);                         \
         break;
         switch (rank) {
             WCE_LRL(1) WCE_LRL(2) WCE_LRL(3) WCE_LRL(4) WCE_LRL(5) WCE_LRL(6) WCE_LRL(7)
