@@ -111,3 +111,31 @@ def test_lowrank_algebra_vs_long_double(wce, oracle, inp, L):
         exp = oracle.mmse_unified(C, np.ones(N, np.uint8), 1.0, ow2, tx, rx)
         worst = max(worst, float(normrel(got, exp)))
     assert worst < 1e-11, worst
+
+
+@pytest.mark.parametrize("L,rot", [(1, False), (5, False), (8, False), (5, True), (13, False)])
+def test_lane_gram_factors(wce, oracle, inp, L, rot):
+    """State::Pk, the rank <= 8 lane kernel's per-subcarrier Gram factors
+    P_k[i][j] = conj(U_ki) U_kj (i >= j, packed at i (i + 1) / 2 + j, formed
+    from the 80-bit U and rounded once): consistent with the state's own U to
+    rounding, real on the diagonal, and all zero past rank 8."""
+    R = pdp_rhh(L, 0.5)
+    if rot:
+        rng = np.random.default_rng(9)
+        Q, _ = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+        R = (Q * np.diag(R).real) @ Q.conj().T
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    U, r, _, _, _ = wce.cov_factor(blob)
+    assert r == L
+    P = blob[len(blob) - N * 36 * 16:].view(np.complex128).reshape(N, 36)   # the State's last member
+    if L > 8:
+        assert not np.any(P)
+        return
+    ref = np.zeros((N, 36), np.complex128)
+    for i in range(L):
+        for j in range(i + 1):
+            ref[:, i * (i + 1) // 2 + j] = np.conj(U[:, i]) * U[:, j]
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(P - ref)) < 4e-16 * scale * 4
+    assert not np.any(P[:, [i * (i + 1) // 2 + i for i in range(8)]].imag)
+    assert not np.any(P[:, L * (L + 1) // 2:])
