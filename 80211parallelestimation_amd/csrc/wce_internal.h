@@ -160,7 +160,8 @@ constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks (
 constexpr int WCE_VARIANT_REF_LS = 2;  // REF PS_MMSE + LS family (+ eq), C semantics: 0 = ref_ls_elem_kernel
                                       // (one element per thread, default), 1 = mmse_solve_ls_kernel (wave per frame)
 constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1..LRL_RMAX one frame per lane
-                                      // (mmse_lr_lane_kernel, direct or LDS-staged by batch size; default),
+                                      // (mmse_lr_lane_kernel, direct or LDS-staged by batch size), ranks 9..16
+                                      // 16 lanes per frame (mmse_lr_quad_kernel); default
                                       // 1 = every rank on mmse_lr_kernel (one frame per wave), 2 = lane kernel
                                       // direct, 3 = lane kernel staged; the lane and wave kernels agree to
                                       // rounding (~1e-15), not bitwise; the lane kernel's two forms bitwise

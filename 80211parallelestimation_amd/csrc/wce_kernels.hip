@@ -2176,6 +2176,210 @@ __global__ __launch_bounds__(64) void mmse_lr_lane_staged_kernel(const State *__
     lr_lane_body<R, true>(st, a, &s, 64);
 }
 
+// ---------------------------------------------------------------------
+// Ranks 9..16: 16 LANES PER (frame, block), 4 per wave (mmse_lr_quad_kernel).
+// A rank-16 Gram system no longer fits one lane's registers (136 complex
+// entries), and a wave per frame spends most of its time on the 53-row
+// machinery around a 16-row system (0.447 ms per 65,536 frames at rank 16).
+// Here lane i of a 16-lane DPP row holds row i of the system:
+//   pass 1, k = 0..52:  Gamma[i][:] += w_k conj(U_ki) U_k:   (U_k: scalar loads,
+//                       conj(U_ki): the lane's own), beta_i += conj(U_ki) conj(x_k) rx_k
+//   Cholesky on the rows: pivot c's scale and column by row_newbcast:c inside
+//                       the 16-lane row (DPP, no LDS), the trailing rows updated
+//                       by each lane for its own row
+//   z = L^-1 beta by broadcasts; t = L^-H z by 16-lane DPP sums (column c of L
+//                       is spread over the rows, one element per lane)
+//   complex x (a wave-uniform branch): the correction term from the lane's 4
+//                       subcarriers k = i, i + 16, ..., summed over the row
+//   H_k = U_k s for the lane's 4 subcarriers: 16 lanes store 256 B of one frame.
+// Same algebra as mmse_lr_kernel, summed in another order (~1e-15).
+// ---------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+template <int N>
+__device__ __forceinline__ double2 row_bcast(double2 v)   // lane N of each 16-lane row, to the row
+{
+    return make_double2(dpp_f64<0x150 + N>(v.x), dpp_f64<0x150 + N>(v.y));
+}
+__device__ __forceinline__ double row16_sum(double v)   // over a 16-lane row, the same bits in every lane
+{
+    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);   // row_half_mirror
+    v += dpp_f64<0x140>(v);   // row_mirror
+    return v;
+}
+__device__ __forceinline__ double2 row16_sum(double2 v) { return make_double2(row16_sum(v.x), row16_sum(v.y)); }
+
+__device__ __forceinline__ double2 row_bcast_n(double2 v, int n)   // n a constant after unrolling
+{
+    switch (n) {
+    case 0: return row_bcast<0>(v);
+    case 1: return row_bcast<1>(v);
+    case 2: return row_bcast<2>(v);
+    case 3: return row_bcast<3>(v);
+    case 4: return row_bcast<4>(v);
+    case 5: return row_bcast<5>(v);
+    case 6: return row_bcast<6>(v);
+    case 7: return row_bcast<7>(v);
+    case 8: return row_bcast<8>(v);
+    case 9: return row_bcast<9>(v);
+    case 10: return row_bcast<10>(v);
+    case 11: return row_bcast<11>(v);
+    case 12: return row_bcast<12>(v);
+    case 13: return row_bcast<13>(v);
+    case 14: return row_bcast<14>(v);
+    default: return row_bcast<15>(v);
+    }
+}
+template <int R, int C>
+__device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
+{
+    if constexpr (C < R) {
+        const double d = row_bcast<C>(Ar[C]).x;   // pivot (C, C), from lane C of the row
+        const double rs = rsq_nr(d);
+        Ar[C] = cscale(Ar[C], rs);                 // L[i][C] (for i >= C)
+        ldi = i == C ? rs : ldi;                   // 1 / L_ii
+#pragma unroll
+        for (int j = C + 1; j < R; ++j) {          // A[i][j] -= L[i][C] conj(L[j][C])
+            const double2 lj = row_bcast_n(Ar[C], j);
+            cmsub_conj(Ar[j], Ar[C], lj);
+        }
+        lrq_chol<R, C + 1>(Ar, ldi, i);
+    }
+}
+
+#ifndef WCE_LR_QUAD   // ranks 9..16 on mmse_lr_quad_kernel (0: mmse_lr_kernel)
+#define WCE_LR_QUAD 1
+#endif
+template <int R>
+__global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    const int i = threadIdx.x & 15;   // the row of the R x R system this lane holds
+    const int64_t units = a.split ? a.n * a.nblk : a.n;
+    const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // (frame, block) unit of the row
+    if (g >= units) return;   // whole 16-lane rows
+    const int64_t f = a.split ? g / a.nblk : g;
+    const int b = a.split ? (int)(g - f * a.nblk) : 0;
+    const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
+    const double ac = st->acoef, bc = st->bcoef;
+    const uint64_t xm = st->xmask;
+    const double2 *__restrict__ U = reinterpret_cast<const double2 *>(st->U);
+    const double2 *__restrict__ UT = reinterpret_cast<const double2 *>(st->UT);
+    const bool row = i < R;
+    double2 Ar[R];   // row i of Gamma, then of a Gamma + b I, then of L
+#pragma unroll
+    for (int j = 0; j < R; ++j) Ar[j] = make_double2(0.0, 0.0);
+    double2 bt = make_double2(0.0, 0.0);
+    bool cplx = false;
+#pragma unroll 1
+    for (int k = 0; k < NSC; ++k) {
+        double2 x = ld2(a.tx, base + k);   // the same 16 B in the row's 16 lanes
+        const double2 r = ld2(a.rx, base + k);
+        if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+        cplx |= x.y != 0.0;
+        const double w = fma(x.x, x.x, x.y * x.y);
+        const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+        const double2 ui = row ? U[k * CLD + i] : make_double2(0.0, 0.0);
+        bt.x = fma(ui.x, v.x, fma(ui.y, v.y, bt.x));   // += conj(u_i) v
+        bt.y = fma(ui.x, v.y, fma(-ui.y, v.x, bt.y));
+        const double2 wi = make_double2(w * ui.x, -w * ui.y);   // w conj(u_i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double2 uj = U[k * CLD + j];   // wave-uniform: scalar loads
+            Ar[j].x = fma(wi.x, uj.x, fma(-wi.y, uj.y, Ar[j].x));
+            Ar[j].y = fma(wi.x, uj.y, fma(wi.y, uj.x, Ar[j].y));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {   // a Gamma + b I; rows past R: the identity (never read)
+        Ar[j] = cscale(Ar[j], ac);
+        Ar[j].x += (i == j || (!row && j == 0)) ? bc : 0.0;
+    }
+    double ldi = 1.0;
+    lrq_chol<R, 0>(Ar, ldi, i);
+    // z = L^-1 beta: lane i keeps z_i
+    double2 z = bt;
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+        const double2 zc = row_bcast_n(cscale(z, ldi), c);   // z_c = (beta_c - ...) / L_cc, from lane c
+        if (i == c) z = zc;
+        else if (i > c) z = csub(z, cmul(Ar[c], zc));
+    }
+    // t = L^-H z: t_c = (z_c - sum_{m > c} conj(L[m][c]) t_m) / L_cc, the sum over the row's lanes
+    double2 t = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int c = R - 1; c >= 0; --c) {
+        const double2 term = i > c && row ? cmul(cconj(Ar[c]), t) : make_double2(0.0, 0.0);
+        const double2 sum = row16_sum(term);
+        if (i == c) t = cscale(csub(z, sum), ldi);
+    }
+    double *W = a.w + 2 * g * a.ws;
+    if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
+        double2 vk[4], rk[4];   // the correction's v_k at the lane's subcarriers k = i + 16 m
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = i + 16 * m;
+            const int kc = k < NSC ? k : 0;
+            double2 x = ld2(a.tx, base + kc);
+            const double2 r = ld2(a.rx, base + kc);
+            if (!((xm >> kc) & 1ull) || k >= NSC) x = make_double2(0.0, 0.0);
+            vk[m] = x;   // (x_k for now; v_k below)
+            rk[m] = r;
+        }
+        double2 uy[4] = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
+#pragma unroll
+        for (int j = 0; j < R; ++j) {   // (U t)_k, t_j broadcast once per j
+            const double2 tj = row_bcast_n(t, j);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int k = i + 16 * m;
+                uy[m] = cadd(uy[m], cmul(UT[j * CLD + (k < NSC ? k : 0)], tj));
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double2 x = vk[m];
+            const double2 rho = csub(rk[m], cscale(cmul(x, uy[m]), ac));
+            vk[m] = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
+        }
+        const double rb = 1.0 / bc;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {   // c_j = sum_k conj(U_kj) v_k over the row; lane j keeps t_j + c_j / b
+            double2 cp = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int k = i + 16 * m;
+                cp = cadd(cp, cmul(cconj(UT[j * CLD + (k < NSC ? k : 0)]), vk[m]));
+            }
+            const double2 cj = row16_sum(cp);
+            if (i == j) t = cadd(t, cscale(cj, rb));
+        }
+    }
+    double2 y[4];   // H_k = U_k s at k = i + 16 m: t_j broadcast once per j
+#pragma unroll
+    for (int m = 0; m < 4; ++m) y[m] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const double2 tj = row_bcast_n(t, j);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = i + 16 * m;
+            const double2 u = UT[j * CLD + (k < NSC ? k : 0)];
+            y[m].x = fma(u.x, tj.x, fma(-u.y, tj.y, y[m].x));
+            y[m].y = fma(u.x, tj.y, fma(u.y, tj.x, y[m].y));
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)   // the row stores 256 B of its frame per m
+        if (i + 16 * m < NSC) st2(W, i + 16 * m, y[m]);
+}
+
 // H[f] = (((X[4f] + X[4f+1]) + X[4f+2]) + X[4f+3]) / 4  (WiFi_channel_estimation_PS_MMSE.m:35)
 __global__ __launch_bounds__(256) void avg_blocks_kernel(const double *__restrict__ X, int64_t xs, double *H, int64_t hs,
                                                          int64_t n)
@@ -2648,6 +2852,20 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
             default: WCE_LRL(8)
         }
 #undef WCE_LRL
+        return hip_status(hipGetLastError());
+    }
+    if (WCE_LR_QUAD && rank > LRL_RMAX && rank <= 16 && lv == 0) {
+        const dim3 gq((unsigned)((waves + 15) / 16)), bq(256);
+        switch (rank) {
+        case 9: hipLaunchKernelGGL(mmse_lr_quad_kernel<9>, gq, bq, 0, s, st, a); break;
+        case 10: hipLaunchKernelGGL(mmse_lr_quad_kernel<10>, gq, bq, 0, s, st, a); break;
+        case 11: hipLaunchKernelGGL(mmse_lr_quad_kernel<11>, gq, bq, 0, s, st, a); break;
+        case 12: hipLaunchKernelGGL(mmse_lr_quad_kernel<12>, gq, bq, 0, s, st, a); break;
+        case 13: hipLaunchKernelGGL(mmse_lr_quad_kernel<13>, gq, bq, 0, s, st, a); break;
+        case 14: hipLaunchKernelGGL(mmse_lr_quad_kernel<14>, gq, bq, 0, s, st, a); break;
+        case 15: hipLaunchKernelGGL(mmse_lr_quad_kernel<15>, gq, bq, 0, s, st, a); break;
+        default: hipLaunchKernelGGL(mmse_lr_quad_kernel<16>, gq, bq, 0, s, st, a); break;
+        }
         return hip_status(hipGetLastError());
     }
     const dim3 g((unsigned)waves), b(64);

@@ -37,9 +37,10 @@ int wce_debug_set_flat_chunk(long long frames);
  * which 2: REF PS_MMSE with LS outputs in one call (0 = one element per
  * thread, ref_ls_elem_kernel, default; 1 = the wave-per-frame fused solve).
  * which 3: WCE_MMSE_COV low-rank path (0 = ranks 1..8 one frame per lane,
- * mmse_lr_lane_kernel, its direct or LDS-staged form by batch size, default;
- * 1 = every rank one frame per wave; 2 / 3 = the lane kernel's direct /
- * staged form at any size).
+ * mmse_lr_lane_kernel, its direct or LDS-staged form by batch size, and
+ * ranks 9..16 16 lanes per frame, mmse_lr_quad_kernel, default; 1 = every
+ * rank one frame per wave; 2 / 3 = the lane kernel's direct / staged form at
+ * any size, ranks past 8 one frame per wave).
  * Process-wide; variants 0..2 give bit-identical results, variant 3's two
  * kernels sum in different orders and agree to rounding (tests check both). */
 int wce_debug_set_variant(int which, int value);

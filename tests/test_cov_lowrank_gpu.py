@@ -262,3 +262,39 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
             assert d < TOL
     finally:
         assert lib.wce_debug_set_variant(3, 0) == 0
+
+
+@pytest.mark.parametrize("L", [9, 10, 12, 13, 16])
+def test_quad_kernel_mid_ranks(gpu_wce, golden, oracle, L):
+    """Ranks 9..16 run 16 lanes per frame (mmse_lr_quad_kernel): BPSK and QPSK
+    frames against the long double solve and against the wave-per-frame Gram
+    kernel (variant WCE_VARIANT_LR = 1), C and MATLAB semantics, 515 frames
+    (a partial last row group of the last wave)."""
+    inp = golden["inputs"]
+    lib = gpu_wce.load()
+    R = pdp_rhh(L, 0.3)
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    assert ctx.cov_info()[:2] == (L, True)
+    B = 515
+    tx, rx = synth(ctx, gpu_wce, B, seed=0x2B0 + L)
+    rng = np.random.default_rng(L)
+    txq = constellation(rng, "qam16", tx.shape)
+    txq[:, :, 26] = 0
+    rxq = channel_frames(rng, txq, inp["ow2"])
+    C = c_ld(oracle, R)
+    try:
+        for t, r in ((tx, rx), (txq, rxq)):
+            got = {}
+            for v in (0, 1):
+                assert lib.wce_debug_set_variant(3, v) == 0
+                got[v] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE)["ps_mmse"]
+                got[v, "m"] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE, semantics=gpu_wce.SEM_MATLAB)["ps_mmse"]
+            sel = np.r_[0:30, B - 10:B]
+            err = normrel(got[0][sel], solve_ld(oracle, C, t[sel, 0], r[sel, 0], inp["ow2"]))
+            per = [solve_ld(oracle, C, t[sel, b], r[sel, b], inp["ow2"]) for b in range(4)]
+            errm = normrel(got[0, "m"][sel], (((per[0] + per[1]) + per[2]) + per[3]) / 4)
+            d = max(normrel(got[0], got[1]).max(), normrel(got[0, "m"], got[1, "m"]).max())
+            print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, quad vs wave kernel {d:.2e}")
+            assert err.max() < TOL and errm.max() < TOL and d < TOL
+    finally:
+        assert lib.wce_debug_set_variant(3, 0) == 0
