@@ -41,7 +41,7 @@ LEGS = {
     "config5_ref_f32": ("ref_ls_elem_kernel<true>", 1 << 20),
     "lowrank4": ("mmse_lr_lane_kernel<4>", 65536),
     "lowrank8": ("mmse_lr_lane_kernel<8>", 65536),
-    "lowrank16": ("mmse_lr_kernel<4>", 65536),
+    "lowrank16": ("mmse_lr_quad_kernel<16>", 65536),
 }
 
 
