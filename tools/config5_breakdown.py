@@ -40,4 +40,4 @@ for d in dirs:
             ctx.estimate(fr, o, mask, st.handle)
         e1.record(st)
         ms = e0.elapsed_ms(e1) / 10
-        print(f"{os.path.basename(d.rstrip('/')):14s} {label:14s} {ms:7.3f} ms  {B / ms / 1e3:.3e} frames/s")
+        print(f"{os.path.basename(d.rstrip('/')):14s} {label:14s} {ms:7.3f} ms  {B / (ms * 1e-3):.3e} frames/s")
