@@ -2474,6 +2474,10 @@ __global__ __launch_bounds__(256) void fc_finish_kernel(SolveArgs a, const doubl
 // =====================================================================
 constexpr int APPLY_WAVES = 4;
 
+#ifndef WCE_APPLY_3M   // H = C W with three real MFMA products per complex product (apply_tile_acc3, matvec_kernel)
+#define WCE_APPLY_3M 1
+#endif
+
 #ifndef WCE_APPLY_TAIL4   // output rows 48..52 on v_mfma_f64_4x4x4_4b (0: a fourth 16x16x4 row block, rows 48..63)
 #define WCE_APPLY_TAIL4 1
 #endif
@@ -2570,14 +2574,27 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
         for (int nt = 0; nt < MATVEC_NT; ++nt) {
             const int i = 16 * nt + ml;
             v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
+            if (!QIN && WCE_APPLY_3M) {   // apply_tile_acc3's chains and order: bit-identical to apply_kernel
+                v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
 #pragma unroll
-            for (int s = 0; s < KSTEPS; ++s) {
-                const int j = 4 * s + kl;
-                const double2 c = ld2(M, i * CLD + j);   // zero-padded 64 x 64
-                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
-                if constexpr (!QIN) accr = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[s], c.y, accr, 0, 0, 0);
-                acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
-                if constexpr (!QIN) acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
+                for (int s = 0; s < KSTEPS; ++s) {
+                    const double2 c = ld2(M, i * CLD + 4 * s + kl);   // zero-padded 64 x 64
+                    p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, p1, 0, 0, 0);
+                    p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, p2, 0, 0, 0);
+                    p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s] + ai[s], c.x + c.y, p3, 0, 0, 0);
+                }
+                accr = p1 - p2;
+                acci = (p3 - p1) - p2;
+            } else {
+#pragma unroll
+                for (int s = 0; s < KSTEPS; ++s) {
+                    const int j = 4 * s + kl;
+                    const double2 c = ld2(M, i * CLD + j);   // zero-padded 64 x 64
+                    accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
+                    if constexpr (!QIN) accr = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[s], c.y, accr, 0, 0, 0);
+                    acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
+                    if constexpr (!QIN) acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
+                }
             }
             if (i < NSC) {
 #pragma unroll
@@ -2966,13 +2983,265 @@ __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t 
     }
 }
 
+#ifndef WCE_APPLY_PF   // C fragment reads issued this many k-steps ahead, across the 16-row blocks (0: per block, 1 ahead)
+#define WCE_APPLY_PF 2
+#endif
+// Rows 0..47 of one tile as one flat sequence of 3 x 14 k-steps, C's LDS
+// fragment for step t + PF read at step t.  Left to itself the compiler
+// issues each k-step's ds_read_b128 right before its 4 MFMAs and waits on it
+// (lgkmcnt(0) every 4 MFMAs), so the MFMA pipe idles for an LDS round trip
+// per k-step unless the SIMD's other wave fills it.  A scheduling barrier
+// per step pins every read at its step (otherwise the scheduler moves each
+// read back next to its first use).  Same products, same summation order: bit-identical.
+template <int PF>
+__device__ __forceinline__ void apply_rows_pf(const double2 *sc, const double (&ar)[KSTEPS], const double (&ai)[KSTEPS],
+                                              double *Y, int64_t ys, int64_t f0, int64_t n, int ml, int kl)
+{
+    constexpr int NS = APPLY_NT * KSTEPS;
+    double2 cb[PF];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) cb[t] = sc[(16 * (t / KSTEPS) + ml) * ACS + 4 * (t % KSTEPS) + kl];
+    v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const int nt = t / KSTEPS, s = t % KSTEPS;
+        const double2 c = cb[t % PF];
+        if (t + PF < NS) cb[t % PF] = sc[(16 * ((t + PF) / KSTEPS) + ml) * ACS + 4 * ((t + PF) % KSTEPS) + kl];
+        __builtin_amdgcn_sched_barrier(0);
+        // the two chains alternate (no MFMA waits on its predecessor's result);
+        // -ai by the f64 MFMA's A-negate bit (blgp = 1: neg:[1,0,0]), not a VALU xor
+        accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, accr, 0, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == KSTEPS - 1) {
+            const int i = 16 * nt + ml;
+            if (i < NSC) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t fr = f0 + kl + 4 * r;
+                    if (fr < n) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
+                }
+            }
+            accr = v4d{0, 0, 0, 0};
+            acci = v4d{0, 0, 0, 0};
+        }
+    }
+}
+
+#ifndef WCE_APPLY_DEFER   // a tile's H stores issued at the start of the next tile (after its W has landed)
+#define WCE_APPLY_DEFER 0
+#endif
+// gfx950 has one vmcnt for loads and stores, which may complete out of
+// order, so the wait for the next tile's W (loaded a whole tile ahead) is a
+// vmcnt(0): it also waits for every H store of the tile just finished, issued
+// a few hundred cycles earlier.  Deferred, a tile's results stay in registers
+// (52 VGPRs) and are stored right after that wait, one tile before the next
+// wait that covers them.
+struct ApplyAcc {
+    v4d r[APPLY_NT], i[APPLY_NT];   // rows 16 nt + ml, frames kl + 4 r
+    double tr0, ti0, tr1, ti1;       // tail: row 48 + kl and row 52, frame ml
+};
+template <int PF>
+__device__ __forceinline__ void apply_tile_acc(const double2 *sc, const double (&ar)[KSTEPS], const double (&ai)[KSTEPS],
+                                               int ml, int kl, ApplyAcc &o)
+{
+    constexpr int NS = APPLY_NT * KSTEPS;
+    double2 cb[PF];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) cb[t] = sc[(16 * (t / KSTEPS) + ml) * ACS + 4 * (t % KSTEPS) + kl];
+#pragma unroll
+    for (int nt = 0; nt < APPLY_NT; ++nt) o.r[nt] = o.i[nt] = v4d{0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const int nt = t / KSTEPS, s = t % KSTEPS;
+        const double2 c = cb[t % PF];
+        if (t + PF < NS) cb[t % PF] = sc[(16 * ((t + PF) / KSTEPS) + ml) * ACS + 4 * ((t + PF) % KSTEPS) + kl];
+        __builtin_amdgcn_sched_barrier(0);
+        o.r[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, o.r[nt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        o.i[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, o.i[nt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        o.r[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, o.r[nt], 0, 0, 1);   // -ai c.y
+        __builtin_amdgcn_sched_barrier(0);
+        o.i[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, o.i[nt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // rows 48..55 on v_mfma_f64_4x4x4_4b (tail_rows' maps and order)
+    const int m4 = ml & 3;
+    double r0 = 0.0, i0 = 0.0, r1 = 0.0, i1 = 0.0;
+    double2 n0 = sc[(48 + m4) * ACS + kl], n1 = sc[(52 + m4) * ACS + kl];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const double2 c0 = n0, c1 = n1;
+        asm volatile("" ::: "memory");
+        if (s + 1 < KSTEPS) {
+            n0 = sc[(48 + m4) * ACS + 4 * (s + 1) + kl];
+            n1 = sc[(52 + m4) * ACS + 4 * (s + 1) + kl];
+        }
+        r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ar[s], r0, 0, 0, 0);
+        r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ar[s], r1, 0, 0, 0);
+        i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, ar[s], i0, 0, 0, 0);
+        i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, ar[s], i1, 0, 0, 0);
+        r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, -ai[s], r0, 0, 0, 0);
+        r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, -ai[s], r1, 0, 0, 0);
+        i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ai[s], i0, 0, 0, 0);
+        i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ai[s], i1, 0, 0, 0);
+    }
+    o.tr0 = r0; o.ti0 = i0; o.tr1 = r1; o.ti1 = i1;
+}
+// The same tile with three real products per complex one instead of four
+// (Gauss): P1 = Σ Re w Re c, P2 = Σ Im w Im c, P3 = Σ (Re w + Im w)(Re c + Im c),
+// Re h = P1 - P2, Im h = P3 - P1 - P2.  25% fewer MFMA cycles; Re c + Im c is
+// a third LDS plane (scs, staged once), Re w + Im w one VALU add per k-step.
+// Exact on integers (tests/test_parity_gpu.py); on real data Im h carries
+// ~eps (|Re w| + |Im w|)(|Re c| + |Im c|) per term instead of
+// ~eps (|Re w Im c| + |Im w Re c|): the same order.
+// NOW: each 16-row block's results are stored as soon as they are final
+// (the deferred form holds 52 more VGPRs, which with three chains spills).
+template <int PF, bool NOW>
+__device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double *scs, const double (&ar)[KSTEPS],
+                                                const double (&ai)[KSTEPS], int ml, int kl, ApplyAcc &o,
+                                                double *Y = nullptr, int64_t ys = 0, int64_t f0 = 0, int64_t n = 0)
+{
+    constexpr int NS = APPLY_NT * KSTEPS;
+    double2 cb[PF];
+    double cbs[PF];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+        const int e = (16 * (t / KSTEPS) + ml) * ACS + 4 * (t % KSTEPS) + kl;
+        cb[t] = sc[e];
+        cbs[t] = scs[e];
+    }
+    v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
+#ifdef WCE_APPLY_ABLATE_MFMA   // timing-only build: loads and stores alone (H = sums of the tile's W)
+    if (NOW) {
+        double sr = 0.0, si = 0.0;
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) { sr += ar[s]; si += ai[s]; }
+#pragma unroll
+        for (int nt = 0; nt < APPLY_NT; ++nt) {
+            const int i = 16 * nt + ml;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t fr = f0 + kl + 4 * r;
+                if (fr < n) st2(Y, fr * ys + i, make_double2(sr + r, si + nt));
+            }
+        }
+        const int64_t fr = f0 + ml;
+        if (fr < n) {
+            st2(Y, fr * ys + 48 + kl, make_double2(sr, si));
+            if (kl == 0) st2(Y, fr * ys + 52, make_double2(si, sr));
+        }
+        return;
+    }
+#endif
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+        const int nt = t / KSTEPS, s = t % KSTEPS;
+        const double2 c = cb[t % PF];
+        const double cs = cbs[t % PF];
+        if (t + PF < NS) {
+            const int e = (16 * ((t + PF) / KSTEPS) + ml) * ACS + 4 * ((t + PF) % KSTEPS) + kl;
+            cb[t % PF] = sc[e];
+            cbs[t % PF] = scs[e];
+        }
+        const double as = ar[s] + ai[s];
+        __builtin_amdgcn_sched_barrier(0);
+        p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, p1, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, p2, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(as, cs, p3, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == KSTEPS - 1) {
+            if (NOW) {
+                const v4d hr = p1 - p2, hi = (p3 - p1) - p2;
+                const int i = 16 * nt + ml;
+                if (i < NSC) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t fr = f0 + kl + 4 * r;
+                        if (fr < n) st2(Y, fr * ys + i, make_double2(hr[r], hi[r]));
+                    }
+                }
+            } else {
+                o.r[nt] = p1 - p2;
+                o.i[nt] = (p3 - p1) - p2;
+            }
+            p1 = p2 = p3 = v4d{0, 0, 0, 0};
+        }
+    }
+    // rows 48..55 on v_mfma_f64_4x4x4_4b (tail_rows' maps), three chains per row group
+    const int m4 = ml & 3;
+    double a0 = 0.0, b0 = 0.0, g0 = 0.0, a1 = 0.0, b1 = 0.0, g1 = 0.0;
+    double2 n0 = sc[(48 + m4) * ACS + kl], n1 = sc[(52 + m4) * ACS + kl];
+    double ns0 = scs[(48 + m4) * ACS + kl], ns1 = scs[(52 + m4) * ACS + kl];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const double2 c0 = n0, c1 = n1;
+        const double cs0 = ns0, cs1 = ns1;
+        asm volatile("" ::: "memory");
+        if (s + 1 < KSTEPS) {
+            n0 = sc[(48 + m4) * ACS + 4 * (s + 1) + kl];
+            n1 = sc[(52 + m4) * ACS + 4 * (s + 1) + kl];
+            ns0 = scs[(48 + m4) * ACS + 4 * (s + 1) + kl];
+            ns1 = scs[(52 + m4) * ACS + 4 * (s + 1) + kl];
+        }
+        const double as = ar[s] + ai[s];
+        a0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ar[s], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ar[s], a1, 0, 0, 0);
+        b0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, ai[s], b0, 0, 0, 0);
+        b1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, ai[s], b1, 0, 0, 0);
+        g0 = __builtin_amdgcn_mfma_f64_4x4x4f64(cs0, as, g0, 0, 0, 0);
+        g1 = __builtin_amdgcn_mfma_f64_4x4x4f64(cs1, as, g1, 0, 0, 0);
+    }
+    o.tr0 = a0 - b0; o.ti0 = (g0 - a0) - b0;
+    o.tr1 = a1 - b1; o.ti1 = (g1 - a1) - b1;
+    if (NOW) {
+        const int64_t fr = f0 + ml;
+        if (fr < n) {
+            st2(Y, fr * ys + 48 + kl, make_double2(o.tr0, o.ti0));
+            if (kl == 0) st2(Y, fr * ys + 52, make_double2(o.tr1, o.ti1));
+        }
+    }
+}
+
+__device__ __forceinline__ void apply_tile_store(const ApplyAcc &o, double *Y, int64_t ys, int64_t f0, int64_t n,
+                                                 int ml, int kl)
+{
+#pragma unroll
+    for (int nt = 0; nt < APPLY_NT; ++nt) {
+        const int i = 16 * nt + ml;
+        if (i < NSC) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t fr = f0 + kl + 4 * r;
+                if (fr < n) st2(Y, fr * ys + i, make_double2(o.r[nt][r], o.i[nt][r]));
+            }
+        }
+    }
+    const int64_t fr = f0 + ml;
+    if (fr < n) {
+        st2(Y, fr * ys + 48 + kl, make_double2(o.tr0, o.ti0));
+        if (kl == 0) st2(Y, fr * ys + 52, make_double2(o.tr1, o.ti1));   // rows 53..55: padding, never stored
+    }
+}
+
 __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const double *__restrict__ M, const double *X,
                                                                         int64_t xs, double *Y, int64_t ys, int64_t n)
 {
     __shared__ double2 sc[APPLY_ROWS * ACS];
+    __shared__ double scs[WCE_APPLY_3M ? APPLY_ROWS * ACS : 1];   // Re c + Im c (3M form)
     for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
         const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
-        sc[i * ACS + j] = ld2(M, i * CLD + j);   // M zero-padded 64 x 64
+        const double2 c = ld2(M, i * CLD + j);   // M zero-padded 64 x 64
+        sc[i * ACS + j] = c;
+        if (WCE_APPLY_3M) scs[i * ACS + j] = c.x + c.y;
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -2983,6 +3252,30 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
     if (g >= ng) return;
     double2 wn[KSTEPS];
     apply_load(X, xs, n, g, ml, kl, wn);
+#if WCE_APPLY_DEFER
+    static_assert(WCE_APPLY_TAIL4, "the deferred form holds the 4x4x4 tail rows");
+    ApplyAcc acc;
+    int64_t fprev = -1;
+    for (; g < ng; g += stride) {
+        double ar[KSTEPS], ai[KSTEPS];
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            ar[s] = wn[s].x;
+            ai[s] = wn[s].y;
+            asm volatile("" ::"v"(ar[s]), "v"(ai[s]));   // W_g complete HERE, before the stores below are issued
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (fprev >= 0) apply_tile_store(acc, Y, ys, fprev, n, ml, kl);   // W_g has landed; W aliasing Y: tile fprev's W was read a tile ago
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);
+        __builtin_amdgcn_sched_barrier(0);
+        if (WCE_APPLY_3M) apply_tile_acc3<WCE_APPLY_PF ? WCE_APPLY_PF : 5, false>(sc, scs, ar, ai, ml, kl, acc);
+        else apply_tile_acc<WCE_APPLY_PF ? WCE_APPLY_PF : 5>(sc, ar, ai, ml, kl, acc);
+        fprev = 16 * g;
+    }
+    apply_tile_store(acc, Y, ys, fprev, n, ml, kl);
+    return;
+#endif
     for (; g < ng; g += stride) {
         double ar[KSTEPS], ai[KSTEPS];
 #pragma unroll
@@ -2992,6 +3285,16 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
         }
         if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);   // next tile, under this one's MFMAs
         const int64_t f0 = 16 * g;
+#if WCE_APPLY_3M
+        {
+            ApplyAcc unused;
+            apply_tile_acc3<WCE_APPLY_PF ? WCE_APPLY_PF : 2, true>(sc, scs, ar, ai, ml, kl, unused, Y, ys, f0, n);
+        }
+        continue;
+#endif
+#if WCE_APPLY_PF
+        apply_rows_pf<WCE_APPLY_PF>(sc, ar, ai, Y, ys, f0, n, ml, kl);
+#else
 #pragma unroll 1
         for (int nt = 0; nt < APPLY_NT; ++nt) {
             const int i = 16 * nt + ml;
@@ -3012,6 +3315,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
                 }
             }
         }
+#endif
         if (WCE_APPLY_TAIL4)
             tail_rows<false, true>([&](int i, int j) { return sc[i * ACS + j]; }, ar, ai, Y, ys, f0, n, lane);
     }

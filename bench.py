@@ -399,10 +399,11 @@ def main():
                         "traffic": hbm_bytes(ka),
                         "executed_tflops": mfma_flops(ka) / (t_apply * 1e-3) / 1e12,
                         "mfma_busy_frac_pmc": ka["SQ_VALU_MFMA_BUSY_CYCLES"] / (ka["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4),
-                        "note": "executed = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 flop: per 16-frame tile 168 "
-                                "v_mfma_f64_16x16x4 (rows 0..47) + 112 v_mfma_f64_4x4x4_4b (rows 48..55), "
-                                "56 x 56 zero-padded (53 x 53 useful, x1.116); busy = SQ_VALU_MFMA_BUSY_CYCLES / "
-                                "(GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
+                        "note": "executed = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 flop; 3M (Gauss) form, three real "
+                                "products per complex one: per 16-frame tile 168 v_mfma_f64_16x16x4 (4 row blocks "
+                                "of 16, 3 chains x 14 k-steps), 64 x 56 zero-padded (53 x 53 useful); achieved "
+                                "counts the 4-product 8 n^2 flop of the contract; busy = "
+                                "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
         # the same product at 1,048,576 frames (the configs[3] batch): past 131,072
         # frames mmse_apply switches to apply_kernel (C staged in LDS, each wave
         # streaming 16-frame tiles with the next tile's W loaded under the MFMAs).
@@ -416,9 +417,13 @@ def main():
             ctx3.mmse_apply(Wb, Hb, nbig, N, s)
         t_big = time_events(wce, stream, lambda: ctx3.mmse_apply(Wb, Hb, nbig, N, s), reps)
         ach_big = FLOP_APPLY * nbig / (t_big * 1e-3) / 1e12
-        app["frames_1M"] = {"kernel": "apply_kernel (streaming, C in LDS)", "frames": nbig, "avg_launch_ms": t_big,
+        app["frames_1M"] = {"kernel": "apply_kernel (streaming, C in LDS, 3M form)", "frames": nbig,
+                            "avg_launch_ms": t_big,
                             "achieved_tflops": ach_big, "frac_fp64_peak": ach_big / PEAK_FP64_TFLOPS,
                             "achieved_GBs": 2 * N * 16 * nbig / (t_big * 1e-3) / 1e9,
+                            "frac_hbm_peak": 2 * N * 16 * nbig / (t_big * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                            "memory_floor_note": "the same loads and stores without the MFMAs take 0.380 ms "
+                                                 "(4.68 TB/s, profiles/r03_ab_apply_3m.txt)",
                             "algorithmic_bytes": 2 * N * 16 * nbig}
         # its MFMA counters from same-size launches (tools/pmc_legs.sh apply1m);
         # the grid is capped at 2 workgroups per CU, so check the output bytes:
