@@ -175,6 +175,36 @@ def test_mfma_apply_exact_integers(gpu_wce, golden):
         assert np.array_equal(got[:, N:], W[:, N:]), B      # the padding is never written
 
 
+def test_apply_kernels_agree_bitwise(gpu_wce, golden):
+    """H = C W on real (non-integer) data: the streaming apply_kernel (batches
+    from 131,072 frames) and matvec_kernel (smaller batches) run the same three
+    Gauss chains (3M form) in the same order, so a frame's H does not depend on
+    the batch size; both within 1e-12 of numpy's W C^T."""
+    inp = golden["inputs"]
+    rng = np.random.default_rng(5)
+    pdp = np.exp(-0.12 * np.arange(N))
+    Rhh = np.diag(pdp / pdp.sum()).astype(np.complex128) * 1.1e-4
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=Rhh)
+    lib = gpu_wce.load()
+    C = (rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N))) / 7.0
+    Cpad = np.zeros((64, 64), np.complex128)
+    Cpad[:N, :N] = C
+    ptr, _ = ctx.state()
+    assert lib.wce_memcpy_htod(ptr, Cpad.ctypes.data_as(ctypes.c_void_p), Cpad.nbytes) == 0
+    big, small = 16 * 4 * 2048 + 16, 4096 + 5
+    W = rng.standard_normal((big, N)) + 1j * rng.standard_normal((big, N))
+    dW = gpu_wce.DeviceArray.from_numpy(W)
+    dHb, dHs = gpu_wce.DeviceArray((big, N), zero=True), gpu_wce.DeviceArray((small, N), zero=True)
+    ctx.mmse_apply(dW, dHb, big)      # apply_kernel
+    ctx.mmse_apply(dW, dHs, small)    # matvec_kernel
+    gpu_wce.synchronize()
+    hb, hs = dHb.numpy(), dHs.numpy()
+    assert np.array_equal(hb[:small], hs)
+    want = W[:small] @ C.T
+    err = np.abs(hs - want).max(axis=1) / np.abs(want).max(axis=1)
+    assert err.max() < 1e-12, err.max()
+
+
 def test_strided_layout_and_block(gpu_wce, golden, oracle):
     """Non-default strides and OFDM block != 0 read the right subcarriers."""
     inp = golden["inputs"]

@@ -56,9 +56,12 @@ row("`matvec_kernel` as `H = C·W` (f64 MFMA, COV mode, 65,536 frames = 4,096 wa
        if "executed_tflops" in ap else "no same-size PMC"))
 if "frames_1M" in ap:
     ab = ap["frames_1M"]
-    row("`apply_kernel` as `H = C·W`, 1,048,576 frames (streaming: C in LDS, next tile's W loaded under the MFMAs)",
-        f"{ab['avg_launch_ms'] * 1e3:.0f} µs; {ab['achieved_tflops']:.1f} TFLOP/s algorithmic = "
-        f"{100 * ab['frac_fp64_peak']:.0f}% of FP64 peak; {ab['achieved_GBs'] / 1000:.2f} TB/s of W in + H out"
+    row("`apply_kernel` as `H = C·W`, 1,048,576 frames (streaming: C in LDS, next tile's W loaded under the MFMAs; "
+        "3M form, three real MFMA products per complex one)",
+        f"{ab['avg_launch_ms'] * 1e3:.0f} µs; {ab['achieved_GBs'] / 1000:.2f} TB/s of W in + H out"
+        + (f" = {100 * ab['frac_hbm_peak']:.0f}% of 8 TB/s (its load/store stream alone: 380 µs)" if "frac_hbm_peak" in ab else "")
+        + f"; {ab['achieved_tflops']:.1f} TFLOP/s algorithmic (8 n² per frame) = "
+        f"{100 * ab['frac_fp64_peak']:.0f}% of FP64 peak"
         + (f"; {ab['executed_tflops']:.1f} TFLOP/s executed, MFMA pipe busy {100 * ab['mfma_busy_frac_pmc']:.0f}% (PMC of "
            f"same-size launches); traffic {ab['traffic'] / 1e6:.0f} MB vs {ab['algorithmic_bytes'] / 1e6:.0f} MB"
            if "executed_tflops" in ab else ""))
