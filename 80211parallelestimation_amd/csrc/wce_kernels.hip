@@ -1935,6 +1935,15 @@ __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *
 #ifndef WCE_LR_LANE_UNROLL   // direct form without the look-ahead: subcarriers per step up to rank 4
 #define WCE_LR_LANE_UNROLL 4
 #endif
+#ifndef WCE_LR_LDS_P   // direct form: P_k and U staged in LDS per workgroup instead of scalar loads, for the ranks whose bit is set
+#define WCE_LR_LDS_P 0x110   // ranks 4 and 8 (measured per rank, profiles/r03_ab_lowrank_ldsp.txt)
+#endif
+#ifndef WCE_LR_PF_LO   // direct form, pass 1: tx / rx loads this many subcarriers ahead, ranks 1..4 (0: UNROLL form)
+#define WCE_LR_PF_LO 0
+#endif
+#ifndef WCE_LR_PF_HI   // the same for ranks 5..8
+#define WCE_LR_PF_HI 0
+#endif
 constexpr int LRL_KC = 4;                         // subcarriers per chunk
 constexpr int LRL_NCH = (NSC + LRL_KC - 1) / LRL_KC;   // 14 chunks (k = 52..55: only 52 is live)
 constexpr int LRL_LS = 5;                         // LDS row stride (complex) per frame
@@ -1970,7 +1979,7 @@ __device__ __forceinline__ void lrl_stage(LrLaneLds &s, const LrChunk &q, int la
     asm volatile("" ::: "memory");
 }
 // pass-1 / correction-pass sweep over k: f(k, x_k, rx_k) in order k = 0..52
-template <bool STAGED, int UN, typename Fn>
+template <bool STAGED, int UN, int PF = 0, typename Fn>
 __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, const int64_t (&eb)[4], uint32_t live,
                                           int64_t base, bool own, int lane, Fn fn)
 {
@@ -1988,6 +1997,31 @@ __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, con
                 fn(k, sp->x[lane * LRL_LS + kk], sp->r[lane * LRL_LS + kk]);
             }
         }
+    } else if constexpr (PF > 0) {
+        // direct form, loads PF subcarriers ahead: at 65,536 frames a launch is
+        // one wave per SIMD (64 frames per wave), so nothing else hides a load's
+        // round trip; issued just in time, pass 1 waits one per subcarrier
+        double2 xb[PF], rb[PF];
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            xb[j] = own ? ld2(a.tx, base + j) : make_double2(0.0, 0.0);
+            rb[j] = own ? ld2(a.rx, base + j) : make_double2(0.0, 0.0);
+        }
+#pragma unroll 1
+        for (int k0 = 0; k0 < NSC; k0 += PF) {
+#pragma unroll
+            for (int j = 0; j < PF; ++j) {
+                const int k = k0 + j;
+                if (k < NSC) {   // (uniform)
+                    const double2 x = xb[j], r = rb[j];
+                    if (k + PF < NSC) {
+                        xb[j] = own ? ld2(a.tx, base + k + PF) : make_double2(0.0, 0.0);
+                        rb[j] = own ? ld2(a.rx, base + k + PF) : make_double2(0.0, 0.0);
+                    }
+                    fn(k, x, r);
+                }
+            }
+        }
     } else {
 #ifdef WCE_LR_ABLATE_LOADS   // timing-only build: one sector of the frame, reused for every k
         const double2 x0 = ld2(a.tx, base), r0 = ld2(a.rx, base);
@@ -2000,9 +2034,11 @@ __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, con
 #endif
     }
 }
-template <int R, bool STAGED>
+// Pl / Ul (WCE_LR_LDS_P, direct form): the workgroup's LDS copies of P_k
+// (R (R + 1) / 2 entries per k) and U (R per k); else State::Pk / State::U
+template <int R, bool STAGED, bool LP = false>
 __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const SolveArgs &a, LrLaneLds *sp,
-                                             int fpw)
+                                             int fpw, const double2 *Pl = nullptr, const double2 *Ul = nullptr)
 {
     constexpr int NO = R * (R - 1) / 2;   // strictly-lower Gram entries
     const int lane = threadIdx.x & 63;
@@ -2029,8 +2065,10 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
     }
     const double ac = st->acoef, bc = st->bcoef;
     const uint64_t xm = st->xmask;
-    const double2 *__restrict__ P = reinterpret_cast<const double2 *>(st->Pk);
-    const double2 *__restrict__ U = reinterpret_cast<const double2 *>(st->U);
+    constexpr int NPR = R * (R + 1) / 2;
+    const double2 *__restrict__ P = LP ? Pl : reinterpret_cast<const double2 *>(st->Pk);
+    const double2 *__restrict__ U = LP ? Ul : reinterpret_cast<const double2 *>(st->U);
+    constexpr int pld = LP ? NPR : LRL_NP, uld = LP ? R : CLD;
     double gd[R];        // Gamma_ii (real)
     double2 go[NO > 0 ? NO : 1];   // Gamma_ij, i > j, at i (i - 1) / 2 + j
     double2 bt[R];       // beta = G^H rx
@@ -2043,15 +2081,16 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
     for (int e = 0; e < NO; ++e) go[e] = make_double2(0.0, 0.0);
     bool cplx = false;
     constexpr int UN = R <= 4 ? WCE_LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
-    lrl_sweep<STAGED, UN>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
+    constexpr int PF = R <= 4 ? WCE_LR_PF_LO : WCE_LR_PF_HI;
+    lrl_sweep<STAGED, UN, PF>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
         if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
         cplx |= x.y != 0.0;
         const double w = fma(x.x, x.x, x.y * x.y);
         const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
-        const double2 *Pk = P + k * LRL_NP;
+        const double2 *Pk = P + k * pld;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            const double2 u = U[k * CLD + i];   // beta_i += conj(u) v
+            const double2 u = U[k * uld + i];   // beta_i += conj(u) v
             bt[i].x = fma(u.x, v.x, fma(u.y, v.y, bt[i].x));
             bt[i].y = fma(u.x, v.y, fma(-u.y, v.x, bt[i].y));
             gd[i] = fma(w, Pk[i * (i + 1) / 2 + i].x, gd[i]);
@@ -2112,11 +2151,11 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
             if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
             double2 y = make_double2(0.0, 0.0);
 #pragma unroll
-            for (int j = 0; j < R; ++j) y = cadd(y, cmul(U[k * CLD + j], t[j]));
+            for (int j = 0; j < R; ++j) y = cadd(y, cmul(U[k * uld + j], t[j]));
             const double2 rho = csub(r, cscale(cmul(x, y), ac));
             const double2 v = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
 #pragma unroll
-            for (int j = 0; j < R; ++j) cc[j] = cadd(cc[j], cmul(cconj(U[k * CLD + j]), v));
+            for (int j = 0; j < R; ++j) cc[j] = cadd(cc[j], cmul(cconj(U[k * uld + j]), v));
         });
         const double rb = 1.0 / bc;
 #pragma unroll
@@ -2127,7 +2166,7 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
         double2 y = make_double2(0.0, 0.0);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const double2 u = U[k * CLD + j];
+            const double2 u = U[k * uld + j];
             y.x = fma(u.x, t[j].x, fma(-u.y, t[j].y, y.x));
             y.y = fma(u.x, t[j].y, fma(u.y, t[j].x, y.y));
         }
@@ -2167,7 +2206,29 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
 template <int R>
 __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a, int fpw)
 {
+#if WCE_LR_LDS_P
+    if constexpr (((WCE_LR_LDS_P >> R) & 1) != 0) {
+    // P_k and U through LDS: their scalar loads each wait a round trip per k
+    // (18 s_load_dwordx16 per k at rank 8, and rank 8's 30 KB of P_k does not
+    // stay in the scalar cache), fully exposed at one wave per SIMD.  Per rank
+    // at 65,536 frames: rank 8 98.0 -> 68.7 us, rank 4 54.9 -> 50.3 us, but
+    // ranks 3, 5, 6, 7 slower (52.6 -> 59.0, 62.6 -> 93.7, 65.4 -> 67.1,
+    // 74.8 -> 84.7: the LDS reads cost VGPRs and the compiler's schedule
+    // changes with them), rank 1, 2 equal; bit-identical everywhere
+    constexpr int NPR = R * (R + 1) / 2;
+    __shared__ double2 sP[NSC * NPR], sU[NSC * R];
+    const double2 *Pg = reinterpret_cast<const double2 *>(st->Pk);
+    const double2 *Ug = reinterpret_cast<const double2 *>(st->U);
+    for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x) sP[e] = Pg[(e / NPR) * LRL_NP + e % NPR];
+    for (int e = threadIdx.x; e < NSC * R; e += blockDim.x) sU[e] = Ug[(e / R) * CLD + e % R];
+    __syncthreads();
+    lr_lane_body<R, false, true>(st, a, nullptr, fpw, sP, sU);
+    } else {
+        lr_lane_body<R, false>(st, a, nullptr, fpw);
+    }
+#else
     lr_lane_body<R, false>(st, a, nullptr, fpw);   // (no LDS)
+#endif
 }
 template <int R>
 __global__ __launch_bounds__(64) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
