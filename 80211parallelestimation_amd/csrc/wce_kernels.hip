@@ -2230,11 +2230,28 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
     lr_lane_body<R, false>(st, a, nullptr, fpw);   // (no LDS)
 #endif
 }
+#ifndef WCE_LR_STAGED_LDS_P   // staged form: 4-wave workgroups sharing one LDS copy of P_k and U, for the ranks whose bit is set
+#define WCE_LR_STAGED_LDS_P 0x1fe   // every rank: 1,048,576 frames, rank 8 1476 -> 951 us, 7 1343 -> 875, 6 1189 -> 845,
+                                    // 5 894 -> 840, 2 952 -> 934, 4 equal (profiles/r03_ab_lowrank_ldsp.txt)
+#endif
+constexpr int lr_staged_threads(int r) { return ((WCE_LR_STAGED_LDS_P >> r) & 1) ? 256 : 64; }
 template <int R>
-__global__ __launch_bounds__(64) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
+__global__ __launch_bounds__(lr_staged_threads(R)) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
 {
-    __shared__ LrLaneLds s;
-    lr_lane_body<R, true>(st, a, &s, 64);
+    if constexpr (lr_staged_threads(R) == 256) {
+        constexpr int NPR = R * (R + 1) / 2;
+        __shared__ double2 sP[NSC * NPR], sU[NSC * R];
+        __shared__ LrLaneLds s[4];
+        const double2 *Pg = reinterpret_cast<const double2 *>(st->Pk);
+        const double2 *Ug = reinterpret_cast<const double2 *>(st->U);
+        for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x) sP[e] = Pg[(e / NPR) * LRL_NP + e % NPR];
+        for (int e = threadIdx.x; e < NSC * R; e += blockDim.x) sU[e] = Ug[(e / R) * CLD + e % R];
+        __syncthreads();
+        lr_lane_body<R, true, true>(st, a, &s[threadIdx.x >> 6], 64, sP, sU);
+    } else {
+        __shared__ LrLaneLds s;
+        lr_lane_body<R, true>(st, a, &s, 64);
+    }
 }
 
 // ---------------------------------------------------------------------
@@ -2791,7 +2808,9 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 #define WCE_LR_FPW_BELOW 131072
 #endif
 #ifndef WCE_LR_STAGE_FROM   // mmse_lr_lane_kernel: the LDS-staged form past this many (frame, block) units
-#define WCE_LR_STAGE_FROM 98304   // rank 4: direct 51.6 vs staged ~60 us at 65,536; 142.6 vs 109.5 at 131,072
+#define WCE_LR_STAGE_FROM 0   // round 3, with P_k / U shared in LDS (WCE_LR_STAGED_LDS_P) the staged form wins at every size:
+                             // 65,536 frames rank 4 52.1 -> 37.2 us, 5 63.1 -> 40.8, 6 65.8 -> 46.8, 7 75.4 -> 53.0, 8 68.1 -> 64.4
+                             // (before the LDS sharing: rank 4 direct 51.6 vs staged ~60 at 65,536, so 98,304 then)
 #endif
 #ifndef WCE_LR_WAVE_ONLY   // build-time default of WCE_VARIANT_LR (A/B builds: 1 = every rank on mmse_lr_kernel)
 #define WCE_LR_WAVE_ONLY 0
@@ -2920,9 +2939,12 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
         const int fpw = waves <= (int64_t)WCE_LR_FPW_BELOW ? WCE_LR_FPW : 64;
         const int64_t dw = (waves + fpw - 1) / fpw;
         const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((dw + 3) / 4)), bd(256);
+        const dim3 gs4((unsigned)((waves + 255) / 256)), bs4(256);   // staged, 4-wave workgroups (WCE_LR_STAGED_LDS_P)
 #define WCE_LRL(RR)                                                                                         \
     case RR:                                                                                                \
-        if (staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a);               \
+        if (staged && lr_staged_threads(RR) == 256)                                                         \
+            hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs4, bs4, 0, s, st, a);                      \
+        else if (staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a);          \
         else hipLaunchKernelGGL(mmse_lr_lane_kernel<RR>, gd, bd, 0, s, st, a, fpw);                         \
         break;
         switch (rank) {

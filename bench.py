@@ -954,7 +954,8 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
     """WCE_MMSE_COV with a power-delay profile of L taps (rank L, the channel
     model of SURVEY 8(d)): the low-rank Gram path, which meets 1e-10 where
     the dense Ryy solve cannot.  Ranks 1..8 run one frame per
-    lane (mmse_lr_lane_kernel; 2,544 B per frame move: tx + rx block in, H
+    lane (mmse_lr_lane_staged_kernel: frames staged through LDS, P_k / U
+    shared per workgroup in LDS; 2,544 B per frame move: tx + rx block in, H
     out), ranks 9..16 16 lanes per frame (mmse_lr_quad_kernel), higher ranks
     one frame per wave (mmse_lr_kernel).  Per-frame rate on the headline's
     frames, beside the wave kernel (ranks <= 16) and
@@ -980,7 +981,7 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
         quad = lr and 9 <= r <= 16
         k0 = min((N - r) // 8, 6)
         leg = {"rank": r, "path": "low-rank" if lr else "dense",
-               "kernel": f"mmse_lr_lane_kernel<{r}>" if lane else f"mmse_lr_quad_kernel<{r}>" if quad else
+               "kernel": f"mmse_lr_lane_staged_kernel<{r}>" if lane else f"mmse_lr_quad_kernel<{r}>" if quad else
                (f"mmse_lr_kernel<{k0}>" if lr else "mmse_solve_kernel<false> + H = C W"),
                "ms_per_step": t, "frames_per_s": B / (t * 1e-3)}
         if lane or quad:

@@ -13,7 +13,7 @@ legs (bench.py field -> kernel, frames per launch):
   front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
   config5    config5_sharded     mmse_solve_ls_kernel<true,true,true>  1,048,576 (all 5 + eq, fp32 LS)
   config5_ref(_f32) config5_ref   ref_ls_elem_kernel<true>      1,048,576 (REF + LS family + eq, fp64 / fp32 LS)
-  lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_kernel<L> (L <= 8) / mmse_lr_kernel<K0>  65,536 (COV, L-tap PDP: rank L)
+  lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_staged_kernel<L> (L <= 8) / mmse_lr_kernel<K0>  65,536 (COV, L-tap PDP: rank L)
 """
 import argparse
 import importlib
@@ -39,8 +39,8 @@ LEGS = {
     "config5": ("mmse_solve_ls_kernel<true, true, true>", 1 << 20),
     "config5_ref": ("ref_ls_elem_kernel<true>", 1 << 20),
     "config5_ref_f32": ("ref_ls_elem_kernel<true>", 1 << 20),
-    "lowrank4": ("mmse_lr_lane_kernel<4>", 65536),
-    "lowrank8": ("mmse_lr_lane_kernel<8>", 65536),
+    "lowrank4": ("mmse_lr_lane_staged_kernel<4>", 65536),
+    "lowrank8": ("mmse_lr_lane_staged_kernel<8>", 65536),
     "lowrank16": ("mmse_lr_quad_kernel<16>", 65536),
 }
 
