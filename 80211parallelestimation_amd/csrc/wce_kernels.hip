@@ -2335,19 +2335,34 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
 #ifndef WCE_LR_QUAD   // ranks 9..16 on mmse_lr_quad_kernel (0: mmse_lr_kernel)
 #define WCE_LR_QUAD 1
 #endif
+#ifndef WCE_LR_QUAD_LDS_U   // pass 1's U_k from an LDS copy per workgroup instead of scalar loads: slower here
+#define WCE_LR_QUAD_LDS_U 0   // (rank 16 237 -> 271 us at 65,536 frames, 3.82 -> 4.39 ms at 1M; profiles/r03_ab_lowrank_ldsp.txt):
+#endif                        // U (13.6 KB at rank 16) stays in the scalar cache, and 3 waves/SIMD hide its latency
 template <int R>
 __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restrict__ st, SolveArgs a)
 {
     const int i = threadIdx.x & 15;   // the row of the R x R system this lane holds
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // (frame, block) unit of the row
+#if WCE_LR_QUAD_LDS_U
+    __shared__ double2 sU[NSC * R];
+    {
+        const double2 *Ug = reinterpret_cast<const double2 *>(st->U);
+        for (int e = threadIdx.x; e < NSC * R; e += blockDim.x) sU[e] = Ug[(e / R) * CLD + e % R];
+        __syncthreads();
+    }
+    const double2 *__restrict__ U1 = sU;
+    constexpr int uld = R;
+#else
+    const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);
+    constexpr int uld = CLD;
+#endif
     if (g >= units) return;   // whole 16-lane rows
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
     const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
     const double ac = st->acoef, bc = st->bcoef;
     const uint64_t xm = st->xmask;
-    const double2 *__restrict__ U = reinterpret_cast<const double2 *>(st->U);
     const double2 *__restrict__ UT = reinterpret_cast<const double2 *>(st->UT);
     const bool row = i < R;
     double2 Ar[R];   // row i of Gamma, then of a Gamma + b I, then of L
@@ -2363,13 +2378,13 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         cplx |= x.y != 0.0;
         const double w = fma(x.x, x.x, x.y * x.y);
         const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
-        const double2 ui = row ? U[k * CLD + i] : make_double2(0.0, 0.0);
+        const double2 ui = row ? U1[k * uld + i] : make_double2(0.0, 0.0);
         bt.x = fma(ui.x, v.x, fma(ui.y, v.y, bt.x));   // += conj(u_i) v
         bt.y = fma(ui.x, v.y, fma(-ui.y, v.x, bt.y));
         const double2 wi = make_double2(w * ui.x, -w * ui.y);   // w conj(u_i)
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const double2 uj = U[k * CLD + j];   // wave-uniform: scalar loads
+            const double2 uj = U1[k * uld + j];   // wave-uniform: scalar loads (or an LDS broadcast)
             Ar[j].x = fma(wi.x, uj.x, fma(-wi.y, uj.y, Ar[j].x));
             Ar[j].y = fma(wi.x, uj.y, fma(wi.y, uj.x, Ar[j].y));
         }
