@@ -2234,9 +2234,12 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
 #define WCE_LR_STAGED_LDS_P 0x1fe   // every rank: 1,048,576 frames, rank 8 1476 -> 951 us, 7 1343 -> 875, 6 1189 -> 845,
                                     // 5 894 -> 840, 2 952 -> 934, 4 equal (profiles/r03_ab_lowrank_ldsp.txt)
 #endif
+#ifndef WCE_LR_STAGED_MINWG   // 4-wave workgroups per CU asked of the register allocator, ranks >= 7, batches past one wave per SIMD
+#define WCE_LR_STAGED_MINWG 2   // 1,048,576 frames: rank 7 898 -> 858 us, rank 8 955 -> 896 (2 waves/SIMD instead of 1; rank 8
+#endif                          // spills 52 B); at 65,536 frames (one wave per SIMD anyway) rank 8 63.3 -> 67.5, so MW = 1 there
 constexpr int lr_staged_threads(int r) { return ((WCE_LR_STAGED_LDS_P >> r) & 1) ? 256 : 64; }
-template <int R>
-__global__ __launch_bounds__(lr_staged_threads(R)) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
+template <int R, int MW = 1>
+__global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
 {
     if constexpr (lr_staged_threads(R) == 256) {
         constexpr int NPR = R * (R + 1) / 2;
@@ -2955,9 +2958,12 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
         const int64_t dw = (waves + fpw - 1) / fpw;
         const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((dw + 3) / 4)), bd(256);
         const dim3 gs4((unsigned)((waves + 255) / 256)), bs4(256);   // staged, 4-wave workgroups (WCE_LR_STAGED_LDS_P)
+        const bool many = waves > 64 * 4 * (int64_t)cu_count();       // more than one 64-unit wave per SIMD
 #define WCE_LRL(RR)                                                                                         \
     case RR:                                                                                                \
-        if (staged && lr_staged_threads(RR) == 256)                                                         \
+        if (staged && lr_staged_threads(RR) == 256 && RR >= 7 && WCE_LR_STAGED_MINWG > 1 && many)          \
+            hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
+        else if (staged && lr_staged_threads(RR) == 256)                                                    \
             hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs4, bs4, 0, s, st, a);                      \
         else if (staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a);          \
         else hipLaunchKernelGGL(mmse_lr_lane_kernel<RR>, gd, bd, 0, s, st, a, fpw);                         \
