@@ -183,17 +183,15 @@ int wce_ctx_mark_ready(wce_ctx *c)
 {
     if (!c) return fail(WCE_EINVAL, "null ctx");
     DeviceGuard g(c->device);
-    int32_t magic = 0;
     HIPCHECK(hipDeviceSynchronize(), "sync");
-    HIPCHECK(hipMemcpy(&magic, reinterpret_cast<char *>(c->d_state) + offsetof(State, magic), sizeof(magic),
-                       hipMemcpyDeviceToHost), "read state magic");
-    if (magic != wce::STATE_MAGIC) return fail(WCE_ESTATE, "state buffer does not hold a valid state");
-    HIPCHECK(hipMemcpy(&c->mode, reinterpret_cast<char *>(c->d_state) + offsetof(State, mode), sizeof(c->mode),
-                       hipMemcpyDeviceToHost), "read state mode");
-    HIPCHECK(hipMemcpy(&c->cov_rank, reinterpret_cast<char *>(c->d_state) + offsetof(State, cov_rank),
-                       sizeof(c->cov_rank), hipMemcpyDeviceToHost), "read state rank");
-    HIPCHECK(hipMemcpy(&c->cov_k0, reinterpret_cast<char *>(c->d_state) + offsetof(State, cov_k0), sizeof(c->cov_k0),
-                       hipMemcpyDeviceToHost), "read state path");
+    std::unique_ptr<State> h(new (std::nothrow) State);
+    if (!h) return fail(WCE_ENOMEM, "alloc");
+    HIPCHECK(hipMemcpy(h.get(), c->d_state, sizeof(State), hipMemcpyDeviceToHost), "read state");
+    if (!wce::state_ok(h.get()))
+        return fail(WCE_ESTATE, "state buffer does not hold a valid state of this build (magic, layout, size, mode, rank)");
+    c->mode = h->mode;
+    c->cov_rank = h->cov_rank;
+    c->cov_k0 = h->cov_k0;
     c->ready = true;
     return WCE_OK;
 }
@@ -201,13 +199,14 @@ int wce_ctx_mark_ready(wce_ctx *c)
 int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
 {
     if (!c || !host_state || bytes < sizeof(State)) return fail(WCE_EINVAL, "bad state blob");
-    if (static_cast<const State *>(host_state)->magic != wce::STATE_MAGIC)
-        return fail(WCE_ESTATE, "state blob has no valid magic");
+    const State *st = static_cast<const State *>(host_state);
+    if (!wce::state_ok(st))
+        return fail(WCE_ESTATE, "state blob is not a valid state of this build (magic, layout, size, mode, rank)");
     DeviceGuard g(c->device);
     HIPCHECK(hipMemcpy(c->d_state, host_state, sizeof(State), hipMemcpyHostToDevice), "upload state");
-    c->mode = static_cast<const State *>(host_state)->mode;
-    c->cov_k0 = static_cast<const State *>(host_state)->cov_k0;
-    c->cov_rank = static_cast<const State *>(host_state)->cov_rank;
+    c->mode = st->mode;
+    c->cov_k0 = st->cov_k0;
+    c->cov_rank = st->cov_rank;
     c->ready = true;
     return WCE_OK;
 }
@@ -266,6 +265,15 @@ extern "C" int wce_debug_set_cov_path(wce_ctx *c, int path)
     if (path < 0 || path > 2) return fail(WCE_EINVAL, "cov path: 0 auto, 1 dense, 2 low-rank");
     c->cov_path = path;
     return WCE_OK;
+}
+
+extern "C" const char *wce_debug_lr_kernel(wce_ctx *c, long long units)
+{
+    if (!c || !c->ready || c->mode != WCE_MMSE_COV) return "";
+    const int k0 = cov_lr_k0(c);
+    if (k0 < 0) return "";
+    DeviceGuard g(c->device);   // cu_count() reads the current device
+    return wce::lr_kernel_name(k0, c->cov_rank, units);
 }
 
 static int check_frames(const wce_frames *in, bool need_blocks)

@@ -14,10 +14,12 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
+constexpr int32_t STATE_LAYOUT = 4;   // State layout version: bump with every change to struct State
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
-// others (one RCCL broadcast, 68 KB).  Complex values are {re, im} fp64.
+// others (one RCCL broadcast of sizeof(State) = wce_state_size() bytes, ~430 KB).
+// Complex values are {re, im} fp64.
 constexpr int LRL_RMAX = 8;                          // ranks on the lane-per-frame low-rank kernel
 constexpr int LRL_NP = LRL_RMAX * (LRL_RMAX + 1) / 2;  // packed lower-triangle entries of its Gram matrix
 struct State {
@@ -54,12 +56,29 @@ struct State {
     double cov_lmax, cov_lmin; // largest / smallest kept eigenvalue of C
     int32_t cov_rank;          // r = number of kept eigen-directions (0..53)
     int32_t cov_k0;            // -1 dense; else first block row of the embedded Gram system
+    int32_t layout;            // STATE_LAYOUT of the build that wrote it
+    int32_t bytes;             // sizeof(State) of the build that wrote it
+    int32_t reserved[2];       // zero (keeps Pk 16-B aligned)
     // Ranks 1..LRL_RMAX (mmse_lr_lane_kernel): the Gram matrix is sum_k |x_k|^2 P_k
     // with P_k[i][j] = conj(U[k][i]) U[k][j], i >= j, packed at i (i + 1) / 2 + j
     // (80-bit products rounded once; zero for other ranks)
     double Pk[NSC * LRL_NP * 2];
 };
 static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
+
+// A state blob this build can use: magic, layout version and size of this
+// build, a known mode, and (WCE_MMSE_COV) a rank and solve form in range.
+// Blobs arrive from other ranks or callers (wce_ctx_load_state,
+// wce_state_validate, wce_ctx_mark_ready after a broadcast).
+inline bool state_ok(const State *st)
+{
+    if (st->magic != STATE_MAGIC || st->layout != STATE_LAYOUT || st->bytes != (int32_t)sizeof(State)) return false;
+    if (st->mode != WCE_MMSE_REF && st->mode != WCE_MMSE_TEXTBOOK && st->mode != WCE_MMSE_COV) return false;
+    if (st->mode == WCE_MMSE_COV)
+        return st->cov_rank >= 0 && st->cov_rank <= NSC && st->cov_k0 >= -1 && st->cov_k0 <= COV_K0_MAX &&
+               (st->cov_k0 >= 0 || st->cov_rank == NSC);
+    return st->cov_k0 == -1;
+}
 
 // Host-side builders (wce_state.cpp, compiled by g++ for x87 long double).
 // `ldc` = long double _Complex as {re, im} pairs of long double.
@@ -149,6 +168,8 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream);
 // the Gram system embedded at block row k0 (State::cov_k0)
 // (rank = State::cov_rank: ranks 1..LRL_RMAX run one frame per lane instead)
 int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream);
+// the kernel launch_mmse_lr runs for `units` (frame, block) units (wce_debug_lr_kernel)
+const char *lr_kernel_name(int k0, int rank, int64_t units);
 // H[f] = mean of X rows 4f .. 4f+3 (MATLAB block average, left to right)
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
@@ -163,8 +184,9 @@ constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1
                                       // (mmse_lr_lane_kernel, direct or LDS-staged by batch size), ranks 9..16
                                       // 16 lanes per frame (mmse_lr_quad_kernel); default
                                       // 1 = every rank on mmse_lr_kernel (one frame per wave), 2 = lane kernel
-                                      // direct, 3 = lane kernel staged; the lane and wave kernels agree to
-                                      // rounding (~1e-15), not bitwise; the lane kernel's two forms bitwise
+                                      // direct, 3 / 4 = lane kernel staged, ranks 7-8 in the one- / two-
+                                      // workgroups-per-CU build at any size; the lane and wave kernels agree
+                                      // to rounding (~1e-15), not bitwise; the staged builds bitwise
 constexpr int WCE_VARIANT_COUNT = 4;
 int set_variant(int which, int value);
 int launch_ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, void *stream);

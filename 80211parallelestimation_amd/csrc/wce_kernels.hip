@@ -2940,6 +2940,55 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     return hip_status(hipGetLastError());
 }
 
+// Which low-rank kernel a (rank, units) launch runs: one decision shared by
+// launch_mmse_lr and lr_kernel_name (wce_debug_lr_kernel: bench labels, tests)
+enum class LrForm { Direct, Staged64, Staged, StagedMW, Quad, Wave };
+static LrForm lr_form(int rank, int64_t units)
+{
+    const int lv = variant(WCE_VARIANT_LR);
+    if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
+        // the LDS-staged form at every size by default (WCE_LR_STAGE_FROM = 0);
+        // the direct form runs only as variant 2, the gate's independent check
+        // of the staging (tests/test_cov_lowrank_gpu.py)
+        const bool staged = lv >= 3 || (lv == 0 && units > (int64_t)WCE_LR_STAGE_FROM);
+        if (!staged) return LrForm::Direct;
+        if (lr_staged_threads(rank) != 256) return LrForm::Staged64;
+        // ranks 7, 8: the two-workgroups-per-CU build (MW = WCE_LR_STAGED_MINWG)
+        // past one 64-unit wave per SIMD; variant 3 forces the MW = 1 build and
+        // variant 4 the MW = 2 build at any size, so the gate checks both
+        const bool many = lv == 4 || (lv == 0 && units > 64 * 4 * (int64_t)cu_count());
+        return rank >= 7 && WCE_LR_STAGED_MINWG > 1 && many ? LrForm::StagedMW : LrForm::Staged;
+    }
+    if (WCE_LR_QUAD && rank > LRL_RMAX && rank <= 16 && lv == 0) return LrForm::Quad;
+    return LrForm::Wave;
+}
+
+const char *lr_kernel_name(int k0, int rank, int64_t units)
+{
+    static const char *lane[2][LRL_RMAX + 1] = {
+        {"", "mmse_lr_lane_kernel<1>", "mmse_lr_lane_kernel<2>", "mmse_lr_lane_kernel<3>", "mmse_lr_lane_kernel<4>",
+         "mmse_lr_lane_kernel<5>", "mmse_lr_lane_kernel<6>", "mmse_lr_lane_kernel<7>", "mmse_lr_lane_kernel<8>"},
+        {"", "mmse_lr_lane_staged_kernel<1>", "mmse_lr_lane_staged_kernel<2>", "mmse_lr_lane_staged_kernel<3>",
+         "mmse_lr_lane_staged_kernel<4>", "mmse_lr_lane_staged_kernel<5>", "mmse_lr_lane_staged_kernel<6>",
+         "mmse_lr_lane_staged_kernel<7>", "mmse_lr_lane_staged_kernel<8>"}};
+    static const char *quad[] = {"mmse_lr_quad_kernel<9>", "mmse_lr_quad_kernel<10>", "mmse_lr_quad_kernel<11>",
+                                 "mmse_lr_quad_kernel<12>", "mmse_lr_quad_kernel<13>", "mmse_lr_quad_kernel<14>",
+                                 "mmse_lr_quad_kernel<15>", "mmse_lr_quad_kernel<16>"};
+    static const char *wave[] = {"mmse_lr_kernel<0>", "mmse_lr_kernel<1>", "mmse_lr_kernel<2>", "mmse_lr_kernel<3>",
+                                 "mmse_lr_kernel<4>", "mmse_lr_kernel<5>", "mmse_lr_kernel<6>"};
+    static const char *mw[] = {"mmse_lr_lane_staged_kernel<7, 2>", "mmse_lr_lane_staged_kernel<8, 2>"};
+    static_assert(WCE_LR_STAGED_MINWG == 2 || WCE_LR_STAGED_MINWG <= 1, "lr_kernel_name spells MW = 2");
+    const int r = rank < 1 ? 1 : (rank > LRL_RMAX ? LRL_RMAX : rank);
+    switch (lr_form(rank, units)) {
+    case LrForm::Direct: return lane[0][r];
+    case LrForm::Staged64:
+    case LrForm::Staged: return lane[1][r];
+    case LrForm::StagedMW: return mw[r >= 8 ? 1 : 0];
+    case LrForm::Quad: return quad[(rank > 16 ? 16 : rank) - 9];
+    default: return k0 >= 0 && k0 <= 6 ? wave[k0] : "";
+    }
+}
+
 int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
@@ -2947,25 +2996,23 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
     if (waves > 0x7fffffffll) return WCE_EINVAL;
     if (a.nblk > 1 && !a.split) return WCE_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    const int lv = variant(WCE_VARIANT_LR);
-    if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
-        // direct form up to 98,304 units, the LDS-staged form past it: the direct
-        // form's scattered sectors start to thrash the caches at 131,072
-        // (profiles/r03_ab_lowrank_lane.txt)
-        const bool staged = lv == 3 || (lv == 0 && waves > (int64_t)WCE_LR_STAGE_FROM);
+    const LrForm form = lr_form(rank, waves);
+    if (form == LrForm::Direct || form == LrForm::Staged64 || form == LrForm::Staged || form == LrForm::StagedMW) {
         // direct form: fewer units per wave on a small batch (latency-bound at one wave per SIMD)
         const int fpw = waves <= (int64_t)WCE_LR_FPW_BELOW ? WCE_LR_FPW : 64;
         const int64_t dw = (waves + fpw - 1) / fpw;
         const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((dw + 3) / 4)), bd(256);
         const dim3 gs4((unsigned)((waves + 255) / 256)), bs4(256);   // staged, 4-wave workgroups (WCE_LR_STAGED_LDS_P)
-        const bool many = waves > 64 * 4 * (int64_t)cu_count();       // more than one 64-unit wave per SIMD
 #define WCE_LRL(RR)                                                                                         \
     case RR:                                                                                                \
-        if (staged && lr_staged_threads(RR) == 256 && RR >= 7 && WCE_LR_STAGED_MINWG > 1 && many)          \
-            hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
-        else if (staged && lr_staged_threads(RR) == 256)                                                    \
-            hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs4, bs4, 0, s, st, a);                      \
-        else if (staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a);          \
+        if constexpr (RR >= 7 && lr_staged_threads(RR) == 256 && WCE_LR_STAGED_MINWG > 1) {                \
+            if (form == LrForm::StagedMW) {                                                                 \
+                hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
+                break;                                                                                      \
+            }                                                                                               \
+        }                                                                                                   \
+        if (form == LrForm::Staged) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs4, bs4, 0, s, st, a); \
+        else if (form == LrForm::Staged64) hipLaunchKernelGGL(mmse_lr_lane_staged_kernel<RR>, gs, bs, 0, s, st, a); \
         else hipLaunchKernelGGL(mmse_lr_lane_kernel<RR>, gd, bd, 0, s, st, a, fpw);                         \
         break;
         switch (rank) {
@@ -2975,7 +3022,7 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
 #undef WCE_LRL
         return hip_status(hipGetLastError());
     }
-    if (WCE_LR_QUAD && rank > LRL_RMAX && rank <= 16 && lv == 0) {
+    if (form == LrForm::Quad) {
         const dim3 gq((unsigned)((waves + 15) / 16)), bq(256);
         switch (rank) {
         case 9: hipLaunchKernelGGL(mmse_lr_quad_kernel<9>, gq, bq, 0, s, st, a); break;

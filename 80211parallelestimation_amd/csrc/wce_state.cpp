@@ -260,6 +260,8 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
     st->ow2 = ow2;
     st->mode = mode;
     st->magic = STATE_MAGIC;
+    st->layout = STATE_LAYOUT;
+    st->bytes = (int32_t)sizeof(State);
     return WCE_OK;
 }
 
@@ -501,7 +503,7 @@ extern "C" int wce_debug_cov_factor(const void *blob, size_t bytes, double *U, i
     using namespace wce;
     if (!blob || bytes < sizeof(State)) return WCE_EINVAL;
     const State *st = static_cast<const State *>(blob);
-    if (st->magic != STATE_MAGIC || st->mode != WCE_MMSE_COV) return WCE_EINVAL;
+    if (!state_ok(st) || st->mode != WCE_MMSE_COV) return WCE_EINVAL;
     if (U) std::memcpy(U, st->U, sizeof(double) * 2 * NSC * CLD);
     if (rank) *rank = st->cov_rank;
     if (k0) *k0 = st->cov_k0;
@@ -517,7 +519,7 @@ extern "C" int wce_state_validate(const void *blob, size_t bytes, int *mode)
     using namespace wce;
     if (!blob || bytes < sizeof(State)) return WCE_EINVAL;
     const State *st = static_cast<const State *>(blob);
-    if (st->magic != STATE_MAGIC) return WCE_ESTATE;
+    if (!state_ok(st)) return WCE_ESTATE;
     if (mode) *mode = st->mode;
     return WCE_OK;
 }

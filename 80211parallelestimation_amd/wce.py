@@ -101,6 +101,7 @@ ABI = {
     "wce_debug_set_flat_chunk": [ctypes.c_int64],
     "wce_debug_set_variant": [c_int, c_int],
     "wce_debug_set_cov_path": [c_void_p, c_int],
+    "wce_debug_lr_kernel": [c_void_p, c_int64],
     "wce_debug_cov_factor": [c_void_p, c_size_t, c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_double),
                              POINTER(c_double)],
     "wce_ctx_cov_info": [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_double), POINTER(c_double)],
@@ -163,7 +164,7 @@ ABI = {
 }
 _VOID = {"WiFi_channel_estimation_LT_LS", "WiFi_channel_estimation_PS_Linear", "WiFi_channel_estimation_PS_Cubic",
          "WiFi_channel_estimation_PS_Sinc", "WiFi_channel_estimation_PS_MMSE"}
-_STR = {"wce_last_error", "wce_version"}
+_STR = {"wce_last_error", "wce_version", "wce_debug_lr_kernel"}
 
 
 def load(path: str = LIB_PATH):
@@ -336,6 +337,10 @@ class Context:
     def set_cov_path(self, path: int):
         """A/B: 0 = the state's choice, 1 = dense Ryy solve, 2 = low-rank Gram path."""
         _check(load().wce_debug_set_cov_path(self.handle, path), "set_cov_path")
+
+    def lr_kernel(self, units: int) -> str:
+        """The low-rank kernel an estimate over `units` (frame, block) units runs ("" on the dense path)."""
+        return load().wce_debug_lr_kernel(self.handle, int(units)).decode()
 
     def set_border_dot(self, on: bool):
         """A/B switch: rank-1 covariance via a second bordered row (default on)."""

@@ -950,7 +950,23 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
     return res
 
 
-def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
+def tile_block0(wce, tx, rx, B, n):
+    """n frames holding block 0 only (frame_stride = 53), block 0 of the B
+    frames in tx / rx tiled n / B times: a 1,048,576-frame low-rank batch in
+    1.8 GB instead of 27 GB (the per-frame MMSE reads block 0 only)."""
+    lib = wce.load()
+    out = []
+    for src in (tx, rx):
+        h = np.ascontiguousarray(src.numpy()[:, 0])
+        d = wce.DeviceArray((n, N))
+        for off in range(0, n, B):
+            m = min(B, n - off)
+            assert lib.wce_memcpy_htod(d.addr + off * N * 16, h.ctypes.data, m * N * 16) == 0
+        out.append(d)
+    return out[0], out[1], wce.Context.frames(out[0], out[1], n, frame_stride=N, block_stride=N)
+
+
+def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
     """WCE_MMSE_COV with a power-delay profile of L taps (rank L, the channel
     model of SURVEY 8(d)): the low-rank Gram path, which meets 1e-10 where
     the dense Ryy solve cannot.  Ranks 1..8 run one frame per
@@ -958,9 +974,11 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
     shared per workgroup in LDS; 2,544 B per frame move: tx + rx block in, H
     out), ranks 9..16 16 lanes per frame (mmse_lr_quad_kernel), higher ranks
     one frame per wave (mmse_lr_kernel).  Per-frame rate on the headline's
-    frames, beside the wave kernel (ranks <= 16) and
-    the dense path forced on the same ctx (wce_debug_set_variant /
-    wce_debug_set_cov_path) for comparison."""
+    frames, beside the wave kernel (ranks <= 16) and the dense path forced on
+    the same ctx (wce_debug_set_variant / wce_debug_set_cov_path).  Rank 8
+    also at 1,048,576 frames (configs[3]'s batch), where ranks 7 and 8 run
+    the two-workgroups-per-CU build.  Kernel names come from the library's
+    own selection (wce_debug_lr_kernel); every leg's H is scanned."""
     s = stream.handle
     lib = wce.load()
     H = wce.DeviceArray((B, N))
@@ -979,11 +997,10 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
         t = time_events(wce, stream, f, reps)
         lane = lr and 1 <= r <= 8
         quad = lr and 9 <= r <= 16
-        k0 = min((N - r) // 8, 6)
         leg = {"rank": r, "path": "low-rank" if lr else "dense",
-               "kernel": f"mmse_lr_lane_staged_kernel<{r}>" if lane else f"mmse_lr_quad_kernel<{r}>" if quad else
-               (f"mmse_lr_kernel<{k0}>" if lr else "mmse_solve_kernel<false> + H = C W"),
-               "ms_per_step": t, "frames_per_s": B / (t * 1e-3)}
+               "kernel": c.lr_kernel(B) if lr else "mmse_solve_kernel<false> + H = C W",
+               "ms_per_step": t, "frames_per_s": B / (t * 1e-3),
+               "nonfinite_frames": ctx_scan(c, H, B, s)}
         if lane or quad:
             leg["achieved_GBs"] = 3 * N * 16 * B / (t * 1e-3) / 1e9
             leg["hbm_frac"] = leg["achieved_GBs"] / PEAK_HBM_GBS
@@ -992,9 +1009,26 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
                 for _ in range(2):
                     f()
                 tw = time_events(wce, stream, f, reps)
+                leg.update({"wave_kernel": c.lr_kernel(B), "wave_kernel_ms_per_step": tw})
             finally:
                 assert lib.wce_debug_set_variant(3, 0) == 0
-            leg.update({"wave_kernel": f"mmse_lr_kernel<{k0}>", "wave_kernel_ms_per_step": tw})
+        if L == 8:
+            txb, rxb, frb = tile_block0(wce, tx, rx, B, big)
+            Hb = wce.DeviceArray((big, N))
+            ob = wce.Outputs(None, None, None, None, Hb.addr, None, N, 0, 0, 0, 0)
+            fb = lambda: c.estimate(frb, ob, wce.PS_MMSE, s)
+            for _ in range(2):
+                fb()
+            tb = time_events(wce, stream, fb, max(3, reps // 4))
+            gbs = 3 * N * 16 * big / (tb * 1e-3) / 1e9
+            kb, src = pmc_leg("lowrank8_1m", big, N * 16.0 * big, tol=0.05)
+            leg[f"frames_{big}"] = {
+                "kernel": c.lr_kernel(big), "frames": big, "ms_per_step": tb, "frames_per_s": big / (tb * 1e-3),
+                "roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": 3 * N * 16 * big,
+                             "traffic": hbm_bytes(kb) if kb else None, "pmc_source": src},
+                "nonfinite_frames": ctx_scan(c, Hb, big, s)}
+            del txb, rxb, Hb
         c.set_cov_path(1)
         for _ in range(2):
             f()
@@ -1003,6 +1037,11 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps):
         out[f"L{L}"] = leg
         del c
     return out
+
+
+def ctx_scan(c, H, n, s):
+    """non-finite frames of an fp64 output (wce_nonfinite_scan, untimed)"""
+    return int(c.nonfinite_scan(H, n, stream=s)[1])
 
 
 def bench_frame_cov(wce, make_ctx, stream, n, reps):
@@ -1094,6 +1133,22 @@ def cpu_reference(budget_s):
     out["mmse_ref_mode"] = {"value": m / t, "unit": "frames/s", "sample": f"{m} frames, {t:.2f} s",
                             "note": "the reference's literal PS_MMSE also spends ~4 s per frame inverting F "
                                     "and returns NaN; both are removed here"}
+    if hasattr(lib, "refh_bench_mmse_formula"):
+        # the headline (TEXTBOOK) mode through the reference's own arithmetic:
+        # WiFi_channel_estimation_PS_MMSE.m:26-33 composed from multiply()
+        # (utils.c:16-31) and the cofactor inverse() (utils.c:141-170) of each
+        # frame's 52 x 52 Ryy, ~4 s per frame; the inputs.h frame and channel
+        # variations of it, 1 frame on 1 core, then `cores` frames on `cores`
+        lib.refh_bench_mmse_formula.restype = ctypes.c_double
+        lib.refh_bench_mmse_formula.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_double, P, P]
+        t1 = lib.refh_bench_mmse_formula(1, 1, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(H))
+        tc = lib.refh_bench_mmse_formula(cores, cores, p(tx), p(rx), p(F), float(inp["ow2"]), p(hls), p(H))
+        out["mmse_textbook"] = {
+            "value": 1.0 / t1, "unit": "frames/s", "cores": 1, "sample": f"1 frame, {t1:.2f} s",
+            "frames_parallel": {"value": cores / tc, "unit": "frames/s", "cores": cores,
+                                "sample": f"{cores} frames, {tc:.2f} s, frames-parallel OpenMP loop"},
+            "routine": "refh_mmse_formula: the .m formula from the reference's multiply() and cofactor inverse()",
+            "note": "the headline mode; the GPU runs the same formula as a bordered Cholesky (DESIGN.md s2)"}
     return out
 
 

@@ -36,11 +36,14 @@ int wce_debug_set_flat_chunk(long long frames);
  * blocks; 1 = the same uncapped; 2 = one element per thread, default).
  * which 2: REF PS_MMSE with LS outputs in one call (0 = one element per
  * thread, ref_ls_elem_kernel, default; 1 = the wave-per-frame fused solve).
- * which 3: WCE_MMSE_COV low-rank path (0 = ranks 1..8 one frame per lane,
- * mmse_lr_lane_kernel, its direct or LDS-staged form by batch size, and
+ * which 3: WCE_MMSE_COV low-rank path (0 = ranks 1..8 one frame per lane in
+ * the LDS-staged form, mmse_lr_lane_staged_kernel, ranks 7 and 8 in its
+ * two-workgroups-per-CU build past 65,536 units on a 256-CU device, and
  * ranks 9..16 16 lanes per frame, mmse_lr_quad_kernel, default; 1 = every
- * rank one frame per wave; 2 / 3 = the lane kernel's direct / staged form at
- * any size, ranks past 8 one frame per wave).
+ * rank one frame per wave; 2 = the lane kernel's direct form,
+ * mmse_lr_lane_kernel; 3 / 4 = the staged form with ranks 7 and 8 in the
+ * one- / two-workgroups-per-CU build at any size; 2..4: ranks past 8 one
+ * frame per wave).
  * Process-wide; variants 0..2 give bit-identical results, variant 3's two
  * kernels sum in different orders and agree to rounding (tests check both). */
 int wce_debug_set_variant(int which, int value);
@@ -48,6 +51,10 @@ int wce_debug_set_variant(int which, int value);
  * chose (default), 1 = always the dense Ryy solve, 2 = always the low-rank
  * Gram path (at the state's rank).  ctx is a wce_ctx*. */
 int wce_debug_set_cov_path(struct wce_ctx *ctx, int path);
+/* The kernel a WCE_MMSE_COV low-rank estimate over `units` (frame, block)
+ * units runs under the current variant (e.g. "mmse_lr_lane_staged_kernel<8, 2>");
+ * "" for a ctx on the dense path.  For bench labels and the gate's checks. */
+const char *wce_debug_lr_kernel(struct wce_ctx *ctx, long long units);
 #ifdef __cplusplus
 }
 #endif

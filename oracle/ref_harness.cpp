@@ -238,4 +238,20 @@ double refh_bench_mmse_omp(int n, int threads, ldc *tx, ldc *rx, ldc *F, double 
     return omp_get_wtime() - t0;
 }
 
+// TEXTBOOK PS_MMSE (WiFi_channel_estimation_PS_MMSE.m:26-33, the bench's
+// headline mode) through the reference's own multiply() and cofactor
+// inverse() (refh_mmse_formula above), frames split over `threads` OpenMP
+// threads (1 = sequential).  Each frame inverts its own 52 x 52 Ryy with the
+// reference's O(n^5) cofactor routine (~4 s per frame on one core).
+double refh_bench_mmse_formula(int n, int threads, ldc *tx, ldc *rx, ldc *F, double ow2, ldc *H_ls, ldc *H)
+{
+    const double t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+    for (int f = 0; f < n; f++) {
+        const size_t o = (size_t)f * SAMPUTIL;
+        refh_mmse_formula(tx + o, rx + o, F, ow2, H_ls, NULL, H + o);
+    }
+    return omp_get_wtime() - t0;
+}
+
 }  // extern "C"

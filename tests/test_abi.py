@@ -134,14 +134,45 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
     ref = (F @ R.astype(np.clongdouble) @ F.conj().T).astype(np.complex128)
     assert np.max(np.abs(C - ref)) / np.max(np.abs(ref)) < 1e-14
     # State tail: a, b, ow2, xmask, mode, magic, then the low-rank factor
-    # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0 and
-    # the lane kernel's P_k (53 x 36 complex)
-    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 53 * 36 * 16)]
+    # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0,
+    # the layout version and size (+ 8 B reserved), and the lane kernel's P_k
+    # (53 x 36 complex)
+    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 16 + 53 * 36 * 16)]
     a, b, ow2 = t[-40:-16].view(np.float64)
     mode, magic = t[-8:].view(np.int32)
     assert (a, b, ow2, mode, magic) == (1.0, inp["ow2"], inp["ow2"], wce.MMSE_COV, 0x80211)
     assert t[-16:-8].view(np.uint64)[0] == (1 << 53) - 1    # X = diag(tx) over all 53
     assert wce.state_mode(blob) == wce.MMSE_COV
+
+
+def _state_field_offset(blob):
+    """byte offset of (cov_rank, cov_k0, layout, bytes) in a state blob"""
+    return len(blob) - (53 * 36 * 16 + 24)
+
+
+def test_state_validation_rejects_foreign_blobs(wce, golden):
+    """wce_state_validate / wce_ctx_load_state accept only a state of this
+    build: magic, layout version, size, mode, and a COV rank / solve form in
+    range (a larger blob from another build used to pass)."""
+    inp = golden["inputs"]
+    R = np.zeros((N, N), np.complex128)
+    R[:8, :8] = _pdp_cov(8, 0.5)                                  # 8 taps: rank 8, Gram path
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    o = _state_field_offset(blob)
+    rank, k0, layout, nbytes = blob[o:o + 16].view(np.int32)
+    assert (rank, nbytes) == (8, len(blob)) and k0 == (53 - 8) // 8 and layout >= 4
+    assert wce.state_mode(blob) == wce.MMSE_COV
+    for field, bad in ((0, 54), (0, -1), (1, 7), (1, -2), (2, layout + 1), (3, len(blob) + 16)):
+        b2 = blob.copy()
+        b2[o + 4 * field:o + 4 * field + 4] = np.array([bad], np.int32).view(np.uint8)
+        with pytest.raises(wce.WceError):
+            wce.state_mode(b2)
+    b2 = blob.copy()
+    b2[o + 4:o + 8] = np.array([-1], np.int32).view(np.uint8)   # dense form needs full rank
+    with pytest.raises(wce.WceError):
+        wce.state_mode(b2)
+    with pytest.raises(wce.WceError):
+        wce.state_mode(blob[:-16].copy())                          # short blob
 
 
 @pytest.mark.gpu

@@ -48,8 +48,11 @@ def _run(wce, ctx, fr, mask, f32=False):
     ("TEXTBOOK", "LT_LS|PS_LINEAR", False, "C"),     # ls_elem_kernel
     ("TEXTBOOK", "ALL", True, "C"),                  # fused solve + LS family + equalization, fp32 outputs
     ("COV", "PS_MMSE", False, "C"),                  # dense solve + MFMA apply
-    ("COV8", "PS_MMSE", False, "C"),                 # low-rank Gram path (8-tap PDP, mmse_lr_kernel<5>)
-    ("COV8", "PS_MMSE", False, "MATLAB"),            # low-rank, split per-block solves + block mean
+    ("COV8", "PS_MMSE", False, "C"),                 # 8-tap PDP: one frame per lane, mmse_lr_lane_staged_kernel<8>
+    ("COV8", "PS_MMSE", False, "MATLAB"),            # the same, split per-block solves + block mean
+    ("COV12", "PS_MMSE", False, "C"),                # 12 taps: 16 lanes per frame, mmse_lr_quad_kernel<12>
+    ("COV24", "PS_MMSE", False, "C"),                # 24 taps: one frame per wave, mmse_lr_kernel<3>
+    ("COV24", "PS_MMSE", False, "MATLAB"),           # the same, split per-block solves
     ("REF", "ALL", True, "C"),                       # ref_ls_elem_kernel, fp32 LS / eq
     ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "C"),   # per-frame covariance: factor matvecs + solve
     ("TEXTBOOK", "LS_ALL", False, "MATLAB"),         # ls_kernel, MATLAB semantics (4-block averages)
@@ -60,11 +63,15 @@ def test_64bit_frame_indexing(layouts, mode, mask, f32, sem):
     if mode == "COV":
         p = np.exp(-0.12 * np.arange(N))
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4)
-    elif mode == "COV8":
+    elif mode.startswith("COV"):
+        L = int(mode[3:])
         p = np.zeros(N)
-        p[:8] = np.exp(-0.5 * np.arange(8))
+        p[:L] = np.exp(-0.5 * np.arange(L))
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4)
-        assert ctx.cov_info()[:2] == (8, True)
+        assert ctx.cov_info()[:2] == (L, True)
+        units = B * (4 if sem == "MATLAB" else 1)
+        assert ctx.lr_kernel(units) == {8: "mmse_lr_lane_staged_kernel<8>", 12: "mmse_lr_quad_kernel<12>",
+                                        24: "mmse_lr_kernel<3>"}[L]
     else:
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], getattr(wce, "MMSE_" + mode))
     m = 0

@@ -221,34 +221,44 @@ def test_profiling_entry_rejects_lowrank(gpu_wce, golden):
 
 @pytest.mark.parametrize("L", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
-    """Ranks 1..8 run one frame per lane (mmse_lr_lane_kernel): BPSK and QPSK
-    frames against the long double solve, and against the wave-per-frame Gram
-    kernel (variant WCE_VARIANT_LR = 1) on the same frames, C and MATLAB
-    semantics, 515 frames (a partial last wave of lanes).  The lane kernel's
-    direct and LDS-staged forms (variants 2, 3; the batch size picks one)
-    agree to rounding."""
+    """Ranks 1..8 run one frame per lane (mmse_lr_lane_staged_kernel): BPSK and
+    QPSK frames against the long double solve, and against the wave-per-frame
+    Gram kernel (variant WCE_VARIANT_LR = 1) on the same frames, C and MATLAB
+    semantics, 515 frames (a partial last wave of lanes).  The product at this
+    size is the staged one-workgroup-per-CU build (variant 3 forces it: bit
+    for bit); the two-workgroups build (variant 4; ranks 7, 8) computes the
+    same sums (bit for bit); the direct form (variant 2: per-lane loads, no
+    LDS staging) is the independent check of the staging (to rounding)."""
     inp = golden["inputs"]
     lib = gpu_wce.load()
     R = pdp_rhh(L, 0.4)
     ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
     assert ctx.cov_info()[:2] == (L, True)
     B = 515
+    assert ctx.lr_kernel(B) == f"mmse_lr_lane_staged_kernel<{L}>"
     tx, rx = synth(ctx, gpu_wce, B, seed=0x1A0 + L)
     rng = np.random.default_rng(L)
     txq = constellation(rng, "qpsk", tx.shape)
     txq[:, :, 26] = 0
     rxq = channel_frames(rng, txq, inp["ow2"])
     C = c_ld(oracle, R)
+    names = {2: f"mmse_lr_lane_kernel<{L}>", 3: f"mmse_lr_lane_staged_kernel<{L}>",
+             4: f"mmse_lr_lane_staged_kernel<{L}, 2>" if L >= 7 else f"mmse_lr_lane_staged_kernel<{L}>"}
     try:
         for t, r in ((tx, rx), (txq, rxq)):
             got = {}
-            for v in (0, 1, 3):
+            for v in (0, 1, 2, 3, 4):
                 assert lib.wce_debug_set_variant(3, v) == 0
+                if v in names:
+                    assert ctx.lr_kernel(B) == names[v]
                 got[v] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE)["ps_mmse"]
                 got[v, "m"] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE, semantics=gpu_wce.SEM_MATLAB)["ps_mmse"]
+            for v in (3, 4):
+                assert np.array_equal(got[v], got[0]) and np.array_equal(got[v, "m"], got[0, "m"]), v
             # direct vs LDS-staged form: same sums in the same order (the compiler may
             # contract a product into an FMA differently in the two instantiations)
-            assert max(normrel(got[0], got[3]).max(), normrel(got[0, "m"], got[3, "m"]).max()) < 1e-12
+            dd = max(normrel(got[0], got[2]).max(), normrel(got[0, "m"], got[2, "m"]).max())
+            assert dd < 1e-12, dd
             sel = np.r_[0:30, B - 10:B]
             err = normrel(got[0][sel], solve_ld(oracle, C, t[sel, 0], r[sel, 0], inp["ow2"]))
             assert err.max() < TOL, err.max()
@@ -258,10 +268,68 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
             # the two kernels: the same algebra summed in another order (rank 1
             # carries the most rounding, ~1e-11 from the long double solve, r03 probe)
             d = max(normrel(got[0], got[1]).max(), normrel(got[0, "m"], got[1, "m"]).max())
-            print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, lane vs wave kernel {d:.2e}")
+            print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, lane vs wave kernel {d:.2e}, "
+                  f"direct vs staged {dd:.2e}")
             assert d < TOL
     finally:
         assert lib.wce_debug_set_variant(3, 0) == 0
+
+
+@pytest.mark.parametrize("L", [7, 8])
+@pytest.mark.parametrize("matlab", [False, True])
+def test_lane_two_workgroup_build_at_size(gpu_wce, golden, oracle, L, matlab):
+    """Ranks 7 and 8 past one 64-unit wave per SIMD (> 65,536 (frame, block)
+    units on 256 CUs) run the two-workgroups-per-CU build
+    mmse_lr_lane_staged_kernel<R, 2> (launch_mmse_lr; rank 8 spills there):
+    70,001 frames in C semantics, 17,001 frames = 68,004 units in MATLAB split
+    mode.  The first half of the batch is BPSK, the second QPSK (the
+    correction pass).  Non-finite scan clean; the first, the last and 30
+    random frames against the long double solve with C formed in 80 bits
+    (WiFi_channel_estimation_PS_MMSE.m:26-33); the whole batch bit-equal to
+    the one-workgroup build forced through variant 3."""
+    wce = gpu_wce
+    inp = golden["inputs"]
+    lib = wce.load()
+    R = pdp_rhh(L, 0.5)
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    B = 17001 if matlab else 70001
+    units = 4 * B if matlab else B
+    NB = 4                                             # blocks 0..3 held per frame
+    rng = np.random.default_rng(0x7E0 + L + 16 * matlab)
+    tx = np.where(rng.random((B, NB, N)) < 0.5, -A, A).astype(np.complex128)
+    tx[B // 2:] = constellation(rng, "qpsk", (B - B // 2, NB, N))
+    tx[:, :, 26] = 0
+    rx = channel_frames(rng, tx, inp["ow2"])
+    dtx, drx = wce.DeviceArray.from_numpy(tx), wce.DeviceArray.from_numpy(rx)
+    fr = ctx.frames(dtx, drx, B, frame_stride=NB * N, semantics=wce.SEM_MATLAB if matlab else wce.SEM_C)
+
+    def run(v):
+        assert lib.wce_debug_set_variant(3, v) == 0
+        H = wce.DeviceArray((B, N), zero=True)
+        ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0), wce.PS_MMSE)
+        wce.synchronize()
+        return H
+
+    try:
+        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}, 2>"
+        H = run(0)
+        assert ctx.nonfinite_scan(H, B)[1] == 0
+        got = H.numpy()
+        assert lib.wce_debug_set_variant(3, 3) == 0
+        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}>"
+        assert np.array_equal(run(3).numpy(), got)
+    finally:
+        assert lib.wce_debug_set_variant(3, 0) == 0
+    C = c_ld(oracle, R)
+    sel = np.concatenate([[0, B - 1], rng.choice(B, 30, replace=False)])
+    if matlab:
+        per = [solve_ld(oracle, C, tx[sel, b], rx[sel, b], inp["ow2"]) for b in range(4)]
+        exp = (((per[0] + per[1]) + per[2]) + per[3]) / 4
+    else:
+        exp = solve_ld(oracle, C, tx[sel, 0], rx[sel, 0], inp["ow2"])
+    err = normrel(got[sel], exp)
+    print(f"\nrank {L} {'MATLAB' if matlab else 'C'} {B} frames ({units} units): max {err.max():.2e}")
+    assert err.max() < TOL, (int(sel[err.argmax()]), err.max())
 
 
 @pytest.mark.parametrize("L", [9, 10, 12, 13, 16])

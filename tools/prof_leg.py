@@ -13,7 +13,8 @@ legs (bench.py field -> kernel, frames per launch):
   front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
   config5    config5_sharded     mmse_solve_ls_kernel<true,true,true>  1,048,576 (all 5 + eq, fp32 LS)
   config5_ref(_f32) config5_ref   ref_ls_elem_kernel<true>      1,048,576 (REF + LS family + eq, fp64 / fp32 LS)
-  lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_staged_kernel<L> (L <= 8) / mmse_lr_kernel<K0>  65,536 (COV, L-tap PDP: rank L)
+  lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_staged_kernel<L> (L <= 8) / mmse_lr_quad_kernel<L>  65,536 (COV, L-tap PDP: rank L)
+  lowrank8_1m cov_lowrank.L8.frames_1048576  mmse_lr_lane_staged_kernel<8, 2>  1,048,576 (block 0 only)
 """
 import argparse
 import importlib
@@ -42,6 +43,7 @@ LEGS = {
     "lowrank4": ("mmse_lr_lane_staged_kernel<4>", 65536),
     "lowrank8": ("mmse_lr_lane_staged_kernel<8>", 65536),
     "lowrank16": ("mmse_lr_quad_kernel<16>", 65536),
+    "lowrank8_1m": ("mmse_lr_lane_staged_kernel<8, 2>", 1 << 20),   # block 0 only, frame_stride 53
 }
 
 
@@ -86,12 +88,24 @@ def main():
             W = wce.DeviceArray((n, N), zero=True)
             ctx.mmse_solve(fr, W, N)
             run = lambda: ctx.mmse_apply(W, H, n, N)
+    elif leg == "lowrank8_1m":
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rank(8))
+        B = 65536
+        tx0, rx0 = wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, NBLK, N))
+        ctx.synth(tx0, rx0, None, B, seed=0x80211)
+        tx, rx, fr = bench.tile_block0(wce, tx0, rx0, B, n)
+        del tx0, rx0
+        assert ctx.lr_kernel(n) == LEGS[leg][0]
+        H = wce.DeviceArray((n, N), zero=True)
+        run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
+                                   wce.PS_MMSE)
     elif leg.startswith("lowrank"):
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rank(int(leg[7:])))
         tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
         ctx.synth(tx, rx, None, n, seed=0x80211)
         H = wce.DeviceArray((n, N), zero=True)
         fr = ctx.frames(tx, rx, n)
+        assert ctx.lr_kernel(n) == LEGS[leg][0]
         run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
                                    wce.PS_MMSE)
     elif leg.startswith("config5_ref"):
