@@ -474,13 +474,30 @@ int wce_ctx_reserve(wce_ctx *c, int64_t n)
 
 // WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvecs), into
 // the solve arguments.  lt_ready: the caller's LT_LS output already holds H_LT.
-static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready,
-                          wce::SolveArgs &sa, double *ws, void *stream)
+// REF in C semantics takes one launch (ref_fc_kernel): with `hout` it also
+// writes H = u s and sets *done; otherwise u and w (pilot rows) go to the
+// workspace for ref_ls_elem_kernel.
+static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready, bool hout,
+                          wce::SolveArgs &sa, double *ws, bool *done, void *stream)
 {
     const int64_t n = in->n_frames;
     if (!in->rx_pre) return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
     int rc = WCE_OK;
     double *hw = ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
+    const State *st = c->d_state;
+    *done = false;
+    if (c->mode == WCE_MMSE_REF && sa.ref_pilots && in->semantics == WCE_SEM_C &&
+        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0) {
+        rc = wce::launch_ref_fc(st, sa, reinterpret_cast<const double *>(in->rx_pre), in->pre_stride,
+                                reinterpret_cast<const double *>(in->tx_pre), uw, ww, WS_LD, hout, stream);
+        if (rc) return fail(rc, "ref_fc launch (frame covariance)");
+        *done = hout;
+        sa.cu = uw;
+        sa.cw = ww;
+        sa.cs = WS_LD;
+        sa.hout = 1;
+        return WCE_OK;
+    }
     const double *h = hw;
     int64_t hs = WS_LD;
     if (lt_ready) {
@@ -500,7 +517,6 @@ static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
         rc = wce::launch_ls(c->d_state, a, stream);
         if (rc) return fail(rc, "ls launch (H_LT for frame covariance)");
     }
-    const State *st = c->d_state;
     if (c->mode == WCE_MMSE_REF) {
         rc = wce::launch_matvec(st->Mg, st->Mu, h, hs, gw, uw, WS_LD, n, false, stream);     // g, u
         if (!rc) rc = wce::launch_matvec(st->Mw, nullptr, gw, WS_LD, ww, nullptr, WS_LD, n, true, stream);
@@ -586,8 +602,10 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     }
     if (fc) {
         const bool lt_ready = !fuse && (mask & WCE_EST_LT_LS) && !(out->flags & WCE_OUT_LS_F32);
-        rc = prep_frame_cov(c, in, out, lt_ready, sa, ws, stream);
+        bool done = false;   // REF, C semantics: H written by the factor launch itself
+        rc = prep_frame_cov(c, in, out, lt_ready, !fuse, sa, ws, &done, stream);
         if (rc) return rc;
+        if (done) return WCE_OK;
     }
     double *aux = ws ? ws + (WS_ARRAYS - 1) * n * WS_LD * 2 : nullptr;
     if (split) {
@@ -842,7 +860,7 @@ int wce_event_elapsed_ms(float *ms, void *a, void *b)
 extern "C" int wce_debug_set_variant(int which, int value)
 {
     const int rc = wce::set_variant(which, value);
-    return rc ? fail(rc, "variant: which in [0, 4), value in [0, 16)") : WCE_OK;
+    return rc ? fail(rc, "variant: which in [0, 5), value in [0, 16)") : WCE_OK;
 }
 
 extern "C" int wce_debug_set_flat_chunk(long long frames)

@@ -170,6 +170,10 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream);
 int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream);
 // the kernel launch_mmse_lr runs for `units` (frame, block) units (wce_debug_lr_kernel)
 const char *lr_kernel_name(int k0, int rank, int64_t units);
+// REF + WCE_MMSE_FRAME_COV (C semantics) in one launch: LT_LS of rx_pre, u = Mu h,
+// w = Mw q(Mg h) at the pilot rows; hout: H = u s to a.w, else u / w rows to uw / ww
+int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
+                  double *uw, double *ww, int64_t wld, bool hout, void *stream);
 // H[f] = mean of X rows 4f .. 4f+3 (MATLAB block average, left to right)
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
@@ -187,7 +191,11 @@ constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1
                                       // direct, 3 / 4 = lane kernel staged, ranks 7-8 in the one- / two-
                                       // workgroups-per-CU build at any size; the lane and wave kernels agree
                                       // to rounding (~1e-15), not bitwise; the staged builds bitwise
-constexpr int WCE_VARIANT_COUNT = 4;
+constexpr int WCE_VARIANT_REF_FC = 4;  // REF + WCE_MMSE_FRAME_COV, C semantics: 0 = ref_fc_kernel (LT_LS, the
+                                      // g / u / w products and the read-out in one launch, default), 1 = the
+                                      // LT_LS pass + two matvec launches + the REF read-out; bit-identical
+constexpr int WCE_VARIANT_COUNT = 5;
+int variant_value(int which);
 int set_variant(int which, int value);
 int launch_ldc_convert(const void *src, void *dst, int64_t n, bool to_complex, void *stream);
 int launch_nonfinite_scan(const double *H, int64_t stride, int64_t n, bool f32, uint32_t *bits,

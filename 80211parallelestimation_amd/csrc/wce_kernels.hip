@@ -125,6 +125,9 @@ __device__ __forceinline__ void st_out(double *p, int64_t idx, double2 v, bool f
 
 // store the requested LS-family outputs of frame f, subcarrier k, and run
 // WiFi_Equalization.m:1-9 over the frame's 15 blocks rv (already loaded)
+#ifndef WCE_EQ_F32_MATH   // fp32 outputs: the equalizer's divisions in fp32 (0: fp64, rounded on the store)
+#define WCE_EQ_F32_MATH 1
+#endif
 template <bool EQ>
 __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
                                             double2 hcub, double2 hsnc, const double2 (&rv)[NBLK])
@@ -138,6 +141,36 @@ __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, u
     if constexpr (EQ) {
         const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
         const int64_t eb = f * a.eqfs + k;
+        if (f32 && WCE_EQ_F32_MATH) {
+            // WCE_OUT_LS_F32 (BASELINE configs[4]'s fp32 interpolation stage): the
+            // 15 divisions in fp32.  H_UTIL_b = hlt + ((b+1)/15)(hps - hlt) stays
+            // fp64 (one fma per component: the blend cancels where the channel
+            // fades -- fp32 there is 7e-6 off), scaled by 2^-e, e the exponent of
+            // the larger of |hlt|, |hps| (exact, and |H_UTIL|^2 stays inside fp32's
+            // range), then rounded to fp32; rx_b is rounded to fp32 and scaled
+            // alike; rx / H_UTIL by v_rcp_f32 (1 ulp).  A numpy model of these
+            // roundings: <= 4.0e-7 norm-relative from the fp64 quotient over 40,000
+            // frames (G4 allows 1e-6; tests/test_config5_gpu.py checks it).
+            // WiFi_Equalization.m:3-8.
+            const double2 dps = csub(hps, hlt);
+            int e = 0;
+            (void)frexp(fmax(fmax(fabs(hlt.x), fabs(hlt.y)), fmax(fabs(hps.x), fabs(hps.y))), &e);
+            e = e < -120 ? -120 : (e > 120 ? 120 : e);
+            const double sc = ldexp(1.0, -e);
+            const float sf = (float)sc;
+            const double2 h0s = cscale(hlt, sc), d0s = cscale(dps, sc);
+#pragma unroll
+            for (int b = 0; b < NBLK; b++) {
+                const double t = (double)(b + 1) / NBLK;
+                const float ur = (float)fma(d0s.x, t, h0s.x), ui = (float)fma(d0s.y, t, h0s.y);
+                const float xr = (float)rv[b].x * sf, xi = (float)rv[b].y * sf;
+                const float inv = __builtin_amdgcn_rcpf(fmaf(ur, ur, ui * ui));
+                v2f q = {fmaf(xr, ur, xi * ui) * inv, fmaf(xi, ur, -(xr * ui)) * inv};
+                if (k == WCE_DC) q = v2f{0.0f, 0.0f};
+                __builtin_nontemporal_store(q, reinterpret_cast<v2f *>(a.eq) + eb + b * a.eqbs);
+            }
+            return;
+        }
 #pragma unroll
         for (int b = 0; b < NBLK; b++) {
             const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
@@ -2706,6 +2739,142 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
 }
 
 // =====================================================================
+// REF per-frame covariance in one launch (WCE_MMSE_FRAME_COV with
+// WCE_MMSE_REF, C semantics; round 4).  main.c's PS_MMSE consumes the
+// frame's own H_EST_LT_LS (main.c:37-53, 148): g = invF h, Rhh = g q(g)^T,
+// C = F Rhh FH = u w^T with u = F invF h = Mu h and w = Mw q(g), and with
+// Ryy = 2 ow2 I and X the 4 pilots, H = u s, s = sum_p w_p x_p rx_p / b
+// (main.c:186-205).  Only w at the pilot rows P = {5, 19, 33, 47} is ever
+// read.  Per 16-frame tile (one wave):
+//   h = LT_LS(tx_pre, rx_pre_f)            ls_elem_kernel's formula, in the
+//                                          MFMA A layout (frame l&15, j = 4s + (l>>4))
+//   g = Mg h, u = Mu h                     matvec_kernel's 3M chains, same order
+//   q(g) = re g - im g                     through LDS into the A layout
+//   w_P = Mw[P, :] q(g)                    matvec_kernel<QIN>'s chain, output
+//                                          blocks 0..2 only (rows 5, 19, 33, 47)
+//   HOUT: s and H = u s                    ref_term / ref_sum4 / ref_out (the REF kernels' order)
+//   else: u and w_P to the workspace       for ref_ls_elem_kernel (the LS outputs)
+// Every value is rounded exactly as the four launches it replaces (LT_LS pass,
+// the g/u matvec, the w matvec, the REF read-out) round it, so H is
+// bit-identical to them; g never goes to HBM and w is formed for 4 rows of 53.
+// =====================================================================
+struct RefFcLds {
+    double q[16][64 + 1];   // q(g) of the tile's 16 frames (row stride 65: the transposing reads spread over banks)
+    double2 w[16][4];       // w at the 4 pilots, per frame
+    double2 s[16];          // s per frame
+};
+template <bool HOUT>
+__global__ __launch_bounds__(256) void ref_fc_kernel(const State *__restrict__ st, SolveArgs a,
+                                                     const double *__restrict__ rx_pre, int64_t ps,
+                                                     const double *__restrict__ tx_pre, double *uw, double *ww,
+                                                     int64_t wld)
+{
+    __shared__ RefFcLds lds[APPLY_WAVES];
+    const int lane = threadIdx.x & 63;
+    RefFcLds &L = lds[threadIdx.x >> 6];
+    const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
+    if (f0 >= a.n) return;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t fa = f0 + ml;
+    const double *txp = tx_pre ? tx_pre : st->tx_pre;
+    // ---- h = LT_LS of the frame's own preamble (main.c:66-75), A layout
+    double ar[KSTEPS], ai[KSTEPS];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        double2 h = make_double2(0, 0);
+        if (fa < a.n && j < NSC) {
+            const double2 rp = ld2_nt(rx_pre, fa * ps + j);
+            const double2 t = ld2(txp, j);
+            const double cq = t.x - t.y;
+            h = cdiv(make_double2(cq * rp.x, cq * rp.y), make_double2(cq * t.x, cq * t.y));
+            if (j == WCE_DC) h = make_double2(0, 0);
+        }
+        ar[s] = h.x;
+        ai[s] = h.y;
+    }
+    // one 16-row output block of M h for the tile: matvec_kernel's 3M chains and order
+    auto mh = [&](const double *M, int nt, v4d &accr, v4d &acci) {
+        const int i = 16 * nt + ml;
+        v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const double2 c = ld2(M, i * CLD + 4 * s + kl);   // zero-padded 64 x 64
+            p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, p1, 0, 0, 0);
+            p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, p2, 0, 0, 0);
+            p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s] + ai[s], c.x + c.y, p3, 0, 0, 0);
+        }
+        accr = p1 - p2;
+        acci = (p3 - p1) - p2;
+    };
+    // ---- g = Mg h, straight to q(g) = re - im in LDS (transposed)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int i = 16 * nt + ml;
+        v4d gr, gi;
+        mh(st->Mg, nt, gr, gi);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L.q[kl + 4 * r][i] = i < NSC ? gr[r] - gi[r] : 0.0;   // matvec reads rows < 53 only
+        __builtin_amdgcn_sched_barrier(0);   // one block's C loads in flight at a time (no 4-block hoist)
+    }
+    wave_lds_sync();
+    // ---- w = Mw q(g) at the pilot rows: matvec_kernel<QIN>'s accr chain, blocks 0..2
+    {
+        double qa[KSTEPS];
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) qa[s] = L.q[ml][4 * s + kl];
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) {
+            const int i = 16 * nt + ml;
+            v4d accr = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s)
+                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(qa[s], st->Mw[2 * (i * CLD + 4 * s + kl)], accr, 0, 0, 0);
+            const int p = i == WCE_P0 ? 0 : i == WCE_P1 ? 1 : i == WCE_P2 ? 2 : i == WCE_P3 ? 3 : -1;
+            if (p >= 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) L.w[kl + 4 * r][p] = make_double2(accr[r], 0.0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    wave_lds_sync();
+    const int pil = kl == 0 ? WCE_P0 : kl == 1 ? WCE_P1 : kl == 2 ? WCE_P2 : WCE_P3;
+    if constexpr (HOUT) {
+        // ---- s = w^T X rx / b over the 4 pilots of the frame's block (lane: frame ml, pilot kl)
+        double2 t = make_double2(0, 0);
+        if (fa < a.n) {
+            const int64_t o = fa * a.fs + (int64_t)a.blk * a.bs + pil;
+            t = ref_term(L.w[ml][kl], ld2(a.tx, o), ld2(a.rx, o));
+        }
+        L.w[ml][kl] = t;   // (each lane rewrites only its own slot)
+        wave_lds_sync();
+        if (kl == 0) L.s[ml] = ref_sum4(L.w[ml][0], L.w[ml][1], L.w[ml][2], L.w[ml][3], 1.0 / st->bcoef);
+        wave_lds_sync();
+    } else if (fa < a.n) {
+        st2(ww, fa * wld + pil, L.w[ml][kl]);   // w at the pilot rows, for ref_ls_elem_kernel
+    }
+    // ---- u = Mu h, block by block: H = u s (HOUT), or u to the workspace
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const int i = 16 * nt + ml;
+        v4d ur, ui;
+        mh(st->Mu, nt, ur, ui);
+        if (i < NSC) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t fr = f0 + kl + 4 * r;
+                if (fr >= a.n) continue;
+                const double2 uv = make_double2(ur[r], ui[r]);
+                if constexpr (HOUT) st2(a.w, fr * a.ws + i, ref_out(uv, L.s[kl + 4 * r]));
+                else st2(uw, fr * wld + i, uv);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// =====================================================================
 // Synthetic frames: splitmix64 counter RNG keyed by (seed, frame, stream).
 // =====================================================================
 __device__ __forceinline__ uint64_t mix64(uint64_t x)
@@ -2833,7 +3002,7 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 #ifndef WCE_LR_WAVE_ONLY   // build-time default of WCE_VARIANT_LR (A/B builds: 1 = every rank on mmse_lr_kernel)
 #define WCE_LR_WAVE_ONLY 0
 #endif
-static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, WCE_LR_WAVE_ONLY};
+static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, WCE_LR_WAVE_ONLY, 0};
 int set_variant(int which, int value)
 {
     if (which < 0 || which >= WCE_VARIANT_COUNT || value < 0 || value > 15) return WCE_EINVAL;
@@ -2841,6 +3010,7 @@ int set_variant(int which, int value)
     return WCE_OK;
 }
 static inline int variant(int which) { return __atomic_load_n(&g_variant[which], __ATOMIC_RELAXED); }
+int variant_value(int which) { return which >= 0 && which < WCE_VARIANT_COUNT ? variant(which) : 0; }
 
 // blocks of 4 waves for a tile kernel: one wave per tile up to the device's
 // resident-wave budget (CUs x waves per CU), grid-stride past it
@@ -3509,6 +3679,19 @@ int launch_matvec(const double *M1, const double *M2, const double *X, int64_t x
     if (qin) hipLaunchKernelGGL((matvec_kernel<true, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
     else if (M2) hipLaunchKernelGGL((matvec_kernel<false, true>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
     else hipLaunchKernelGGL((matvec_kernel<false, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
+    return hip_status(hipGetLastError());
+}
+
+int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
+                  double *uw, double *ww, int64_t wld, bool hout, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    if (a.split || !rx_pre) return WCE_EINVAL;
+    const int64_t blocks = (a.n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
+    const dim3 g((unsigned)blocks), b(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (hout) hipLaunchKernelGGL(ref_fc_kernel<true>, g, b, 0, s, st, a, rx_pre, ps, tx_pre, uw, ww, wld);
+    else hipLaunchKernelGGL(ref_fc_kernel<false>, g, b, 0, s, st, a, rx_pre, ps, tx_pre, uw, ww, wld);
     return hip_status(hipGetLastError());
 }
 

@@ -55,6 +55,8 @@ def _run(wce, ctx, fr, mask, f32=False):
     ("COV24", "PS_MMSE", False, "MATLAB"),           # the same, split per-block solves
     ("REF", "ALL", True, "C"),                       # ref_ls_elem_kernel, fp32 LS / eq
     ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "C"),   # per-frame covariance: factor matvecs + solve
+    ("REF", "PS_MMSE|FRAME_COV", False, "C"),        # ref_fc_kernel: LT_LS, factors and H = u s in one launch
+    ("REF", "ALL|FRAME_COV", True, "C"),             # ref_fc_kernel factors, then ref_ls_elem_kernel
     ("TEXTBOOK", "LS_ALL", False, "MATLAB"),         # ls_kernel, MATLAB semantics (4-block averages)
     ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "MATLAB"),   # split per-block solves + fc_finish
 ])
@@ -75,6 +77,7 @@ def test_64bit_frame_indexing(layouts, mode, mask, f32, sem):
     else:
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], getattr(wce, "MMSE_" + mode))
     m = 0
+    ctx.reserve(B)
     for name in mask.split("|"):
         m |= getattr(wce, name)
     se = getattr(wce, "SEM_" + sem)

@@ -128,3 +128,46 @@ def test_frame_cov_errors(gpu_wce, golden):
         ctx.estimate(ctx.frames(tx, rx, 2), o, gpu_wce.PS_MMSE | gpu_wce.FRAME_COV)
     with pytest.raises(gpu_wce.WceError):
         ctx.reserve(-1)
+
+
+@pytest.mark.parametrize("mask_name", ["MMSE", "ALL", "MMSE_LIN"])
+@pytest.mark.parametrize("f32", [False, True])
+def test_ref_fused_factor_kernel_equals_four_launches(gpu_wce, golden, oracle, mask_name, f32):
+    """REF + FRAME_COV in C semantics runs ref_fc_kernel (round 4): LT_LS of
+    the frame's preamble, g = invF h and u = F invF h on MFMA, w = Mw q(g)
+    at the 4 pilot rows only, and (PS_MMSE alone) s and H = u s, in one
+    launch.  It rounds every value as the four launches it replaces (LT_LS
+    pass, two matvec launches, REF read-out: variant WCE_VARIANT_REF_FC = 1),
+    so H and every LS output are bit-identical, on a ragged batch (not a
+    multiple of 16 frames), block 2 of the frame, a caller tx_pre, and a
+    non-dense output stride; frames vs the bit-exact oracle of main.c's
+    PS_MMSE with the frame's own LT_LS (main.c:37-53, 148-205)."""
+    wce = gpu_wce
+    lib = wce.load()
+    r = golden["ref"]
+    inp = golden["inputs"]
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+    B = 1037
+    tx, rx, pre = wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, N))
+    ctx.synth(tx, rx, pre, B, seed=0xFC)
+    wce.synchronize()
+    t, x, p = tx.numpy(), rx.numpy(), pre.numpy()
+    p[1] = r["pre_rx"][1]                                   # a golden preamble of its own
+    tpre = inp["tx_pre"] * (1.0 + 0.0j)
+    mask = {"MMSE": wce.PS_MMSE, "ALL": wce.ALL, "MMSE_LIN": wce.PS_MMSE | wce.PS_LINEAR}[mask_name] | wce.FRAME_COV
+    got = {}
+    try:
+        for v in (0, 1):
+            assert lib.wce_debug_set_variant(4, v) == 0
+            got[v] = ctx.estimate_host(t, x, rx_pre=p, mask=mask, block=2, tx_pre=tpre, ls_f32=f32)
+    finally:
+        assert lib.wce_debug_set_variant(4, 0) == 0
+    for k in got[0]:
+        assert np.array_equal(got[0][k], got[1][k]), k
+    H = got[0]["ps_mmse"]
+    assert np.isfinite(H).all()
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    for f in (0, 1, 2, 511, B - 1):
+        hls = oracle.lt_ls(tpre, p[f])
+        exp = oracle.mmse_ref_repaired(t[f, 2], x[f, 2], F, inp["ow2"], hls, invF)
+        assert normrel(H[f], exp) < TOL, f
