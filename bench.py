@@ -49,6 +49,7 @@ BYTES_REF_ALG = 8 * 16 + N * 16          # REF PS_MMSE: 4 tx + 4 rx pilots in, H
 BYTES_PILOT_SECTORS = 8 * 64             # the 8 pilot reads of a frame each fetch a whole 64-B sector
 PEAK_FP64_TFLOPS = 78.6                  # MI355X FP64 vector = FP64 matrix (spec)
 PEAK_HBM_GBS = 8000.0                    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KSTEPS_MFMA = 14                         # 4-deep f64 MFMA k-steps over 56 >= 53 subcarriers
 METRIC = "MMSE-estimated 802.11 frames/sec (53 subcarriers) at 1/2/4/8 MI355X; % roofline"
 
 
@@ -907,7 +908,11 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
     """BASELINE configs[4] in main.c semantics (round 3): REF PS_MMSE + LT_LS /
     PS_Linear / PS_Cubic / PS_Sinc + equalization over n frames with per-frame
     preambles, one HBM pass (ref_ls_elem_kernel: one (frame, subcarrier)
-    element per thread).  Bytes per frame, SURVEY 8(d): rx 15x53 + tx block 0 +
+    element per thread).  frame_cov_*: the same with WCE_MMSE_FRAME_COV, i.e.
+    each frame's PS_MMSE from its own LT_LS as main.c:37-53 / 148 chain them
+    (round 4: ref_fc_kernel forms the factors, then the same one-pass kernel;
+    the factor rows' HBM round trip, 2 x 848 + 4 x 64 B per frame, is not
+    algorithmic and shows in `traffic`).  Bytes per frame, SURVEY 8(d): rx 15x53 + tx block 0 +
     rx_pre in, 5 H + eq out = 31,376 (fp64) / 23,320 (LS + eq stored fp32); the
     kernel reads only tx's 4 pilots of block 0, so it moves 784 B less
     (30,592 / 22,536: its minimum I/O, the rate quoted as `achieved`)."""
@@ -918,12 +923,17 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
     res = {"workload": f"BASELINE configs[4], main.c semantics: REF PS_MMSE + LT_LS + PS_Linear/Cubic/Sinc + "
                        f"equalization, per-frame preambles, {n} frames, one HBM pass (ref_ls_elem_kernel)",
            "frames": n}
-    for label, f32, leg in (("fp64", False, "config5_ref"), ("mixed_fp64_solve_fp32_ls", True, "config5_ref_f32")):
+    ctx_ref.reserve(n)   # FRAME_COV: the per-frame factor rows (u, w) live in the ctx's workspace
+    for label, f32, leg, fc in (("fp64", False, "config5_ref", False),
+                                ("mixed_fp64_solve_fp32_ls", True, "config5_ref_f32", False),
+                                ("frame_cov_fp64", False, "config5_ref_fc", True),
+                                ("frame_cov_mixed_fp32_ls", True, "config5_ref_fc_f32", True)):
         dt = np.complex64 if f32 else np.complex128
         outs = [wce.DeviceArray((n, N), dt) for _ in range(4)] + [wce.DeviceArray((n, N))]
         eq = wce.DeviceArray((n, NBLK, N), dt)
         o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32 if f32 else 0)
-        f = lambda: ctx_ref.estimate(fr, o, wce.ALL, s)
+        mask = wce.ALL | (wce.FRAME_COV if fc else 0)
+        f = lambda: ctx_ref.estimate(fr, o, mask, s)
         for _ in range(3):
             f()
         t = time_events(wce, stream, f, reps)
@@ -935,11 +945,16 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
         # WRITE_SIZE runs 5% (fp64) / 11% (fp32) over the output bytes: 53-element
         # rows end in partial 64-B sectors; FETCH_SIZE = streamed rx / rx_pre (x2,
         # the gfx950 correction) + the 8 pilot sectors per frame (counted in full)
-        k, src = pmc_leg(leg, n, out_b * n, tol=0.12)
+        k, src = pmc_leg(leg, n, out_b * n, tol=0.12) if leg != "config5_ref_fc_f32" else (None, "fp32 FRAME_COV leg not profiled")
         traffic = hbm_bytes(k, narrow_fetch_kib=BYTES_PILOT_SECTORS * n / 1024.0) if k else None
+        if fc and traffic is not None:   # + the factor kernel's rx_pre in, u and w rows out (16-frame tiles)
+            kf, _ = pmc_leg("config5_ref_fc_factors", n, 0.0, waves=(n + 15) // 16)
+            traffic = traffic + hbm_bytes(kf) if kf else None
         bad = sum(ctx_ref.nonfinite_scan(h, n, f32=(f32 and i < 4), stream=s)[1] for i, h in enumerate(outs))
         bad += ctx_ref.nonfinite_scan(eq, n * NBLK, f32=f32, stream=s)[1]
         res[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3),
+                      "kernels": "ref_fc_kernel<false> (per-frame u, w) + ref_ls_elem_kernel<true>" if fc else
+                                 "ref_ls_elem_kernel<true>",
                       "roofline": {"bound": "hbm", "kernel": "ref_ls_elem_kernel", "achieved": ach,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
                                    "traffic": traffic, "pmc_source": src,
@@ -1062,7 +1077,21 @@ def bench_frame_cov(wce, make_ctx, stream, n, reps):
         for _ in range(3):
             f()
         t = time_events(wce, stream, f, reps)
-        out[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3)}
+        out[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3), "nonfinite_frames": ctx_scan(c, H, n, s)}
+        if m == wce.MMSE_REF:
+            # one launch (ref_fc_kernel<true>): rx_pre 848 + 8 pilots 128 in, H 848 out
+            alg = (N * 16 + 8 * 16 + N * 16) * n
+            k, src = pmc_leg("frame_cov_ref", n, N * 16.0 * n, waves=(n + 15) // 16)
+            gbs = alg / (t * 1e-3) / 1e9
+            out[label].update({"kernel": "ref_fc_kernel<true> (LT_LS, g / u on f64 MFMA, w at the pilot rows, H = u s)",
+                               "roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                            "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": alg,
+                                            "traffic": hbm_bytes(k, narrow_fetch_kib=BYTES_PILOT_SECTORS * n / 1024.0)
+                                            if k else None, "pmc_source": src,
+                                            # executed: per 16-frame tile 2 x 4 x 14 x 3 (g, u: 3M) + 3 x 14
+                                            # (w) v_mfma_f64_16x16x4 of 2,048 flop
+                                            "mfma_executed_tflops": (2 * 4 * KSTEPS_MFMA * 3 + 3 * KSTEPS_MFMA) * 2048
+                                            * ((n + 15) // 16) / (t * 1e-3) / 1e12}})
         del c
     return out
 

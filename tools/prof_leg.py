@@ -13,6 +13,8 @@ legs (bench.py field -> kernel, frames per launch):
   front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
   config5    config5_sharded     mmse_solve_ls_kernel<true,true,true>  1,048,576 (all 5 + eq, fp32 LS)
   config5_ref(_f32) config5_ref   ref_ls_elem_kernel<true>      1,048,576 (REF + LS family + eq, fp64 / fp32 LS)
+  config5_ref_fc(_factors)       ref_ls_elem_kernel<true> / ref_fc_kernel<false>  1,048,576 (the same | FRAME_COV)
+  frame_cov_ref frame_cov.ref    ref_fc_kernel<true>              65,536 (REF PS_MMSE | FRAME_COV: one launch)
   lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_staged_kernel<L> (L <= 8) / mmse_lr_quad_kernel<L>  65,536 (COV, L-tap PDP: rank L)
   lowrank8_1m cov_lowrank.L8.frames_1048576  mmse_lr_lane_staged_kernel<8, 2>  1,048,576 (block 0 only)
 """
@@ -40,6 +42,9 @@ LEGS = {
     "config5": ("mmse_solve_ls_kernel<true, true, true>", 1 << 20),
     "config5_ref": ("ref_ls_elem_kernel<true>", 1 << 20),
     "config5_ref_f32": ("ref_ls_elem_kernel<true>", 1 << 20),
+    "config5_ref_fc": ("ref_ls_elem_kernel<true>", 1 << 20),          # REF + FRAME_COV, all 5 + eq (round 4) ...
+    "config5_ref_fc_factors": ("ref_fc_kernel<false>", 1 << 20),     # ... and its factor kernel (same workload)
+    "frame_cov_ref": ("ref_fc_kernel<true>", 65536),        # REF + FRAME_COV, PS_MMSE only: the whole step
     "lowrank4": ("mmse_lr_lane_staged_kernel<4>", 65536),
     "lowrank8": ("mmse_lr_lane_staged_kernel<8>", 65536),
     "lowrank16": ("mmse_lr_quad_kernel<16>", 65536),
@@ -108,8 +113,18 @@ def main():
         assert ctx.lr_kernel(n) == LEGS[leg][0]
         run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
                                    wce.PS_MMSE)
+    elif leg == "frame_cov_ref":
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
+        ctx.synth(tx, rx, pre, n, seed=0x80211)
+        ctx.reserve(n)
+        H = wce.DeviceArray((n, N), zero=True)
+        fr = ctx.frames(tx, rx, n, rx_pre=pre)
+        run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
+                                   wce.PS_MMSE | wce.FRAME_COV)
     elif leg.startswith("config5_ref"):
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+        ctx.reserve(n)
         f32 = leg.endswith("f32")
         dt = np.complex64 if f32 else np.complex128
         tx, rx, pre = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, N))
@@ -118,7 +133,8 @@ def main():
         eq = wce.DeviceArray((n, NBLK, N), dt)
         o = wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, wce.OUT_LS_F32 if f32 else 0)
         fr = ctx.frames(tx, rx, n, rx_pre=pre)
-        run = lambda: ctx.estimate(fr, o, wce.ALL)
+        mask = wce.ALL | (wce.FRAME_COV if leg.startswith("config5_ref_fc") else 0)
+        run = lambda: ctx.estimate(fr, o, mask)
     elif leg == "ref":
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
         tx, rx, fr = bench.ref_frames(wce, ctx, n)
