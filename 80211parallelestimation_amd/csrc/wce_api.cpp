@@ -26,6 +26,9 @@ struct wce_ctx {
     int32_t cov_k0 = -1;        // State::cov_k0 (WCE_MMSE_COV: >= 0 low-rank Gram path, -1 dense)
     int32_t cov_rank = 0;       // State::cov_rank
     int cov_path = 0;           // wce_debug_set_cov_path: 0 auto, 1 dense, 2 low-rank
+    bool cm_on = false;         // State::cm_on: a constant-modulus operator is loaded (wce_ctx_set_modulus)
+    bool cm_use = true;         // wce_debug_set_cm: A/B switch of that path
+    std::vector<wce_complex> rhh;   // WCE_MMSE_COV ctx built here: the caller's Rhh (for wce_ctx_set_modulus)
     // Workspaces (FRAME_COV factors, MATLAB per-block rows), one per stream:
     // calls on different streams never share scratch, so they may run
     // concurrently (SURVEY 8(b) threading).  A call holds its stream's entry
@@ -151,7 +154,11 @@ int wce_ctx_create_cov(wce_ctx **out, int device, const wce_complex *tx_pre, con
     rc = wce_ctx_create_empty(&c, device);
     if (rc) { delete h; return rc; }
     rc = wce_ctx_load_state(c, h, sizeof(State));
-    if (!rc) { c->host = *h; c->has_host = true; }
+    if (!rc) {
+        c->host = *h;
+        c->has_host = true;
+        c->rhh.assign(Rhh, Rhh + wce::NSC * wce::NSC);
+    }
     delete h;
     if (rc) { wce_ctx_destroy(c); return rc; }
     *out = c;
@@ -192,6 +199,7 @@ int wce_ctx_mark_ready(wce_ctx *c)
     c->mode = h->mode;
     c->cov_rank = h->cov_rank;
     c->cov_k0 = h->cov_k0;
+    c->cm_on = h->cm_on != 0;
     c->ready = true;
     return WCE_OK;
 }
@@ -207,6 +215,7 @@ int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
     c->mode = st->mode;
     c->cov_k0 = st->cov_k0;
     c->cov_rank = st->cov_rank;
+    c->cm_on = st->cm_on != 0;
     c->ready = true;
     return WCE_OK;
 }
@@ -256,6 +265,30 @@ int wce_ctx_cov_info(wce_ctx *c, int *rank, int *low_rank, double *lambda_max, d
     if (low_rank) *low_rank = cov_lr_k0(c) >= 0;
     if (lambda_max) *lambda_max = lm[0];
     if (lambda_min) *lambda_min = lm[1];
+    return WCE_OK;
+}
+
+int wce_ctx_set_modulus(wce_ctx *c, const wce_complex *x_ref)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    if (!c->ready) return fail(WCE_ESTATE, "ctx not ready");
+    if (c->mode != WCE_MMSE_COV) return fail(WCE_EINVAL, "wce_ctx_set_modulus: not a WCE_MMSE_COV context");
+    if (!c->has_host || c->rhh.empty())
+        return fail(WCE_ESTATE, "wce_ctx_set_modulus needs the ctx that built the state (wce_ctx_create_cov); "
+                                "set it before the broadcast, or use wce_state_set_modulus on the blob");
+    int rc = wce::host_build_cm(&c->host, wce::host_reference_F(), c->rhh.data(), x_ref);
+    if (rc) return fail(rc, "constant-modulus operator: x_ref not finite, or Rhh / state mismatch");
+    DeviceGuard g(c->device);
+    HIPCHECK(hipDeviceSynchronize(), "sync before state update");   // no estimate may read the old state mid-copy
+    HIPCHECK(hipMemcpy(c->d_state, &c->host, sizeof(State), hipMemcpyHostToDevice), "upload state");
+    c->cm_on = c->host.cm_on != 0;
+    return WCE_OK;
+}
+
+extern "C" int wce_debug_set_cm(wce_ctx *c, int on)
+{
+    if (!c) return fail(WCE_EINVAL, "null ctx");
+    c->cm_use = on != 0;
     return WCE_OK;
 }
 
@@ -570,7 +603,12 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     // Config-5 fusion: the LS family and equalization ride in the MMSE solve's
     // epilogue (C semantics); otherwise one HBM-streaming LS pass.
     const int lr_k0 = (mask & WCE_MMSE_FRAME_COV) ? -1 : cov_lr_k0(c);   // WCE_MMSE_COV low-rank path
-    const bool fuse = c->fuse && ls && mmse && in->semantics == WCE_SEM_C && lr_k0 < 0;
+    // constant-modulus frames on the shared operator K (wce_ctx_set_modulus), the
+    // rest on the per-frame kernels, which skip the flagged frames.  Not for ranks
+    // 1..8 (the lane kernels are already bound by the frames' HBM traffic).
+    const bool cm = mmse && c->mode == WCE_MMSE_COV && c->cm_on && c->cm_use && in->semantics == WCE_SEM_C &&
+                    !(mask & WCE_MMSE_FRAME_COV) && (lr_k0 < 0 || c->cov_rank > wce::LRL_RMAX);
+    const bool fuse = c->fuse && ls && mmse && in->semantics == WCE_SEM_C && lr_k0 < 0 && !cm;
     const wce::LsArgs la = ls_args(in, out, mask, eq_src);
     if (ls && !fuse) {
         rc = wce::launch_ls(c->d_state, la, stream);
@@ -583,7 +621,7 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     if (split && n * sa.nblk > INT32_MAX) return fail(WCE_EINVAL, "n_frames * 4 > 2^31 - 1 (MATLAB semantics)");
     std::unique_lock<std::mutex> lk;
     double *ws = nullptr;
-    if (fc || split) {
+    if (fc || split || cm) {
         wce::Workspace *w = fixed;
         if (!w) {
             w = stream_ws(c, stream, lk);
@@ -618,6 +656,12 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
         }
     }
     double *H = reinterpret_cast<double *>(out->ps_mmse);
+    if (cm) {   // flags (one byte per frame) in the aux array, unused in C semantics
+        uint8_t *flags = reinterpret_cast<uint8_t *>(aux);
+        rc = wce::launch_cm(c->d_state, sa, flags, stream);
+        if (rc) return fail(rc, "constant-modulus launch");
+        sa.skip = flags;
+    }
     if (lr_k0 >= 0) {   // H = U s straight from the solve (split: H_b rows, then the block mean)
         rc = wce::launch_mmse_lr(c->d_state, lr_k0, c->cov_rank, sa, stream);
         if (rc) return fail(rc, "mmse_lr launch");
@@ -628,7 +672,7 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     if (rc) return fail(rc, "mmse_solve launch");
     if (sa.hout && split) rc = wce::launch_fc_finish(sa, aux, H, out->out_stride, stream);
     else if (split) rc = wce::launch_matvec_avg(c->d_state->C, ws, WS_LD, sa.nblk, H, out->out_stride, n, stream);
-    else if (!sa.hout) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream);   // H = C W in place
+    else if (!sa.hout) rc = wce::launch_mmse_apply(c->d_state, H, H, out->out_stride, n, stream, sa.skip);   // H = C W in place
     if (rc) return fail(rc, "mmse apply launch");
     return WCE_OK;
 }
@@ -657,7 +701,8 @@ int wce_plan_create(wce_plan **out_plan, wce_ctx *c, const wce_frames *in, const
     if (!p) return fail(WCE_ENOMEM, "alloc");
     p->device = c->device;
     // size the plan's workspace now: nothing may allocate while the stream is captured
-    if ((mask & WCE_MMSE_FRAME_COV) || (in->semantics == WCE_SEM_MATLAB && (mask & WCE_EST_PS_MMSE))) {
+    if ((mask & WCE_MMSE_FRAME_COV) || (in->semantics == WCE_SEM_MATLAB && (mask & WCE_EST_PS_MMSE)) ||
+        (c->mode == WCE_MMSE_COV && c->cm_on && (mask & WCE_EST_PS_MMSE))) {
         int rc = grow_ws(c, p->ws, in->n_frames > 0 ? in->n_frames : 1, nullptr);
         if (rc) { delete p; return rc; }
     }

@@ -63,6 +63,14 @@ struct State {
     // with P_k[i][j] = conj(U[k][i]) U[k][j], i >= j, packed at i (i + 1) / 2 + j
     // (80-bit products rounded once; zero for other ranks)
     double Pk[NSC * LRL_NP * 2];
+    // WCE_MMSE_COV, constant-modulus frames (wce_ctx_set_modulus, round 4): for
+    // frames whose |x_k|^2 equals pcm[k] on every subcarrier, P = diag(pcm) is
+    // frame-independent and so is K = (a C P + b I)^-1 C (80-bit, host), and
+    // H = K (conj(x) o rx) [+ C ((x - conj x) o (rx - a x o H1)) / b].
+    double Kcm[CLD * CLD * 2];
+    double pcm[NPAD];
+    int32_t cm_on;
+    int32_t cm_reserved[3];
 };
 static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
 
@@ -96,6 +104,9 @@ const ldc *host_reference_F();
 void host_lt_ls(const ldc *tx_pre, const ldc *rx_pre, ldc *H);
 // Fill a host State from F / invF / H_LS (long double) for `mode`.
 int host_apply_cov(State *st, const ldc *F, const wce_complex *Rhh);
+// WCE_MMSE_COV constant-modulus operator K = (a C P + b I)^-1 C, P = diag(|x_ref|^2)
+// (x_ref null: off), from the same Rhh the state was built with
+int host_build_cm(State *st, const ldc *F, const wce_complex *Rhh, const wce_complex *x_ref);
 int host_build_state(State *st, const ldc *F, const ldc *invF, const ldc *H_LS,
                      const ldc *tx_pre, double ow2, int mode);
 
@@ -129,6 +140,7 @@ struct SolveArgs {
     double *dots;
     int32_t ref_pilots;       // REF (main.c): a = 0 and X = the 4 pilots -> mmse_ref_flat_kernel
     int32_t pad;
+    const uint8_t *skip;      // per unit: nonzero = H already written (constant-modulus path); null = none
 };
 struct SynthArgs {
     double *tx, *rx, *rx_pre;
@@ -153,7 +165,12 @@ int launch_front(const FrontArgs &a, bool preamble, void *stream);
 int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream);
 // solve + LS family + equalization of each frame in one launch (C semantics, one block)
 int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, void *stream);
-int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream);
+int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream,
+                      const uint8_t *skip = nullptr);
+// constant-modulus frames of a WCE_MMSE_COV batch (C semantics): H = K (conj x o rx)
+// (+ the correction for non-real x) for every frame whose |x|^2 matches State::pcm;
+// flags[f] = 1 for those frames, 0 for the others (left to the per-frame path)
+int launch_cm(const State *st, const SolveArgs &a, uint8_t *flags, void *stream);
 // Y1[f] = M1 X[f] (and Y2[f] = M2 X[f] if M2), M = padded 64 x 64 complex;
 // qin: X replaced by (re X - im X, 0) first.
 int launch_matvec(const double *M1, const double *M2, const double *X, int64_t xs, double *Y1, double *Y2,

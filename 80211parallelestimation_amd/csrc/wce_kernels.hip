@@ -1677,7 +1677,7 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
     const int64_t g = blockIdx.x;
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
-    if (f >= a.n) return;
+    if (f >= a.n || (a.skip && a.skip[g])) return;   // skip: H already written (constant-modulus path)
     const double2 w = solve_block<R1>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs, f);
     if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, w);
 }
@@ -1928,7 +1928,7 @@ __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *
     const int64_t g = blockIdx.x;
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
-    if (f >= a.n) return;
+    if (f >= a.n || (a.skip && a.skip[g])) return;   // skip: H already written (constant-modulus path)
     const double2 h = lr_solve<K0>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs);
     if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, h);
 }
@@ -2393,7 +2393,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);
     constexpr int uld = CLD;
 #endif
-    if (g >= units) return;   // whole 16-lane rows
+    if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows (skip: the constant-modulus path wrote H)
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
     const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
@@ -2671,7 +2671,7 @@ __device__ __forceinline__ void tail_rows(CLoad cload, const double (&ar)[KSTEPS
 template <bool QIN, bool TWO, int NB = 1>
 __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ M1, const double *__restrict__ M2,
                                                      const double *X, int64_t xs, double *Y1, double *Y2,
-                                                     int64_t ys, int64_t n)
+                                                     int64_t ys, int64_t n, const uint8_t *__restrict__ skip)
 {
     const int lane = threadIdx.x & 63;
     const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
@@ -2729,7 +2729,7 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int64_t fr = f0 + kl + 4 * r;
-                    if (fr < n) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
+                    if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
                 }
             }
         }
@@ -2872,6 +2872,143 @@ __global__ __launch_bounds__(256) void ref_fc_kernel(const State *__restrict__ s
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+// =====================================================================
+// WCE_MMSE_COV, constant-modulus frames (round 4; wce_ctx_set_modulus).
+// Ryy = a X C X^H + b I depends on the frame's symbols only through
+// P = X^H X = diag |x_k|^2 once the phases are split off, and for PSK frames
+// (the reference's BPSK, inputs.h; QPSK) P is the same for every frame.  By
+// the push-through identity C X^H (a X C X^H + b I)^-1 = (a C P + b I)^-1 C X^H:
+//   H1 = K (conj(x) o rx),   K = (a C P + b I)^-1 C   (State::Kcm, 80-bit host)
+// and for non-real x (the .m file applies X, not X^H; b Ryy^-1 rx = rx - a x o H1)
+//   H  = H1 + C [(x - conj x) o (rx - a x o H1)] / b,
+// the Gram path's correction term (mmse_lr_kernel), formed the same way.
+// Per 16-frame tile (one wave), everything in ONE register layout: lane l
+// holds frame l & 15 at subcarriers j = 4 s + (l >> 4).  That is the
+// v_mfma_f64_16x16x4 B operand (k = j, n = frame) and, with the matrix as the A
+// operand (m = output row), also the D layout of the product (row 16 nt + 4 r
+// + (l >> 4) = 4 s' + (l >> 4) with s' = 4 nt + r): H1 lands where the
+// correction's inputs are, with no transpose.
+//  - x, rx loads; the pattern check |x_j|^2 == pcm[j] (the host's fma, bit for
+//    bit) on every subcarrier, per frame over its 4 lanes (ballot);
+//  - H1 = K (conj x o rx) on MFMA (3M: three real products per complex one);
+//  - a non-real frame in the tile (wave-uniform): y2 = (x - conj x) o (rx - a x
+//    o H1), H = H1 + (C y2) (1 / b);
+//  - H of the matching frames stored; flags[f] = 1 for them, 0 for the others
+//    (left to the per-frame kernels, which skip the flagged units).
+// =====================================================================
+__device__ __forceinline__ void cm_rows3(const double *__restrict__ M, int nt, const double (&yr)[KSTEPS],
+                                         const double (&yi)[KSTEPS], int ml, int kl, v4d &hr, v4d &hi)
+{
+    v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
+    const int i = 16 * nt + ml;   // A operand: M[i][4 s + kl]
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const double2 c = ld2(M, i * CLD + 4 * s + kl);   // zero-padded 64 x 64
+        p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(c.x, yr[s], p1, 0, 0, 0);
+        p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(c.y, yi[s], p2, 0, 0, 0);
+        p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(c.x + c.y, yr[s] + yi[s], p3, 0, 0, 0);
+    }
+    hr = p1 - p2;
+    hi = (p3 - p1) - p2;
+}
+// Two launches: CPLX = false checks every frame, finishes the tiles whose
+// matching frames are all real (flags 1) and marks matching non-real frames
+// 2; CPLX = true (its own register allocation: the correction holds all of
+// H1) finishes the tiles holding a 2, and exits at once elsewhere.
+template <bool CPLX>
+__global__ __launch_bounds__(256) void cm_kernel(const State *__restrict__ st, SolveArgs a, uint8_t *__restrict__ flags)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
+    if (f0 >= a.n) return;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t fa = f0 + ml;
+    const bool live = fa < a.n;
+    if (CPLX && __ballot(live && flags[fa] == 2) == 0) return;   // (wave-uniform) nothing left here
+    const int64_t base = live ? fa * a.fs + (int64_t)a.blk * a.bs : 0;
+    const uint64_t xm = st->xmask;
+    const double ac = st->acoef;
+    double yr[KSTEPS], yi[KSTEPS];
+    bool bad = !live, cplx = false;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        double2 x = make_double2(0, 0), r = x;
+        if (live && j < NSC) {
+            x = ld2(a.tx, base + j);
+            r = ld2(a.rx, base + j);
+            if (!((xm >> j) & 1ull)) x = make_double2(0, 0);
+            bad |= fma(x.x, x.x, x.y * x.y) != st->pcm[j];
+            cplx |= x.y != 0.0;
+        }
+        yr[s] = fma(x.x, r.x, x.y * r.y);    // conj(x) rx
+        yi[s] = fma(x.x, r.y, -x.y * r.x);
+    }
+    const uint64_t bb = __ballot(bad), cb = __ballot(cplx);
+    const uint32_t ok = ~(uint32_t)((bb | (bb >> 16) | (bb >> 32) | (bb >> 48)) & 0xffffu) & 0xffffu;
+    const uint32_t cx = (uint32_t)((cb | (cb >> 16) | (cb >> 32) | (cb >> 48)) & 0xffffu) & ok;
+    if (!CPLX && kl == 0 && live) flags[fa] = !((ok >> ml) & 1u) ? 0 : (cx != 0 ? 2 : 1);
+    if (ok == 0) return;                        // (wave-uniform) no frame of this tile matches
+    const bool mine = (ok >> ml) & 1u;
+    if (!CPLX && cx != 0) return;               // (wave-uniform) the CPLX launch finishes this tile
+    if (!CPLX) {                                // real symbols: H = K (conj x o rx), block by block
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            v4d hr, hi;
+            cm_rows3(st->Kcm, nt, yr, yi, ml, kl, hr, hi);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * nt + 4 * r + kl;
+                if (mine && i < NSC) st2(a.w, fa * a.ws + i, make_double2(hr[r], hi[r]));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
+    // non-real symbols in the tile: all of H1 first (it is the correction's input)
+    double h1r[16], h1i[16];   // row 4 s + kl at index s (s = 14, 15: padding rows 56..63)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        v4d hr, hi;
+        cm_rows3(st->Kcm, nt, yr, yi, ml, kl, hr, hi);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            h1r[4 * nt + r] = hr[r];
+            h1i[4 * nt + r] = hi[r];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // y2 = (x - conj x) o (rx - a x o H1): the frame's loads again (L2-resident)
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        double2 x = make_double2(0, 0), r = x;
+        if (mine && j < NSC) {
+            x = ld2(a.tx, base + j);
+            r = ld2(a.rx, base + j);
+            if (!((xm >> j) & 1ull)) x = make_double2(0, 0);
+        }
+        const double2 rho = csub(r, cscale(cmul(x, make_double2(h1r[s], h1i[s])), ac));
+        yr[s] = -2.0 * x.y * rho.y;
+        yi[s] = 2.0 * x.y * rho.x;
+        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // 4 subcarriers' loads in flight at a time
+    }
+    const double rb = 1.0 / st->bcoef;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        v4d cr, ci;
+        cm_rows3(st->C, nt, yr, yi, ml, kl, cr, ci);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int s = 4 * nt + r, i = 4 * s + kl;
+            if (mine && i < NSC && s < KSTEPS)
+                st2(a.w, fa * a.ws + i, make_double2(h1r[s] + cr[r] * rb, h1i[s] + ci[r] * rb));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (kl == 0 && mine) flags[fa] = 1;
 }
 
 // =====================================================================
@@ -3427,7 +3564,8 @@ __device__ __forceinline__ void apply_tile_acc(const double2 *sc, const double (
 template <int PF, bool NOW>
 __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double *scs, const double (&ar)[KSTEPS],
                                                 const double (&ai)[KSTEPS], int ml, int kl, ApplyAcc &o,
-                                                double *Y = nullptr, int64_t ys = 0, int64_t f0 = 0, int64_t n = 0)
+                                                double *Y = nullptr, int64_t ys = 0, int64_t f0 = 0, int64_t n = 0,
+                                                const uint8_t *__restrict__ skip = nullptr)
 {
     constexpr int NS = APPLY_NT * KSTEPS;
     double2 cb[PF];
@@ -3450,11 +3588,11 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t fr = f0 + kl + 4 * r;
-                if (fr < n) st2(Y, fr * ys + i, make_double2(sr + r, si + nt));
+                if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(sr + r, si + nt));
             }
         }
         const int64_t fr = f0 + ml;
-        if (fr < n) {
+        if (fr < n && !(skip && skip[fr])) {
             st2(Y, fr * ys + 48 + kl, make_double2(sr, si));
             if (kl == 0) st2(Y, fr * ys + 52, make_double2(si, sr));
         }
@@ -3487,7 +3625,7 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int64_t fr = f0 + kl + 4 * r;
-                        if (fr < n) st2(Y, fr * ys + i, make_double2(hr[r], hi[r]));
+                        if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(hr[r], hi[r]));
                     }
                 }
             } else {
@@ -3525,7 +3663,7 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
     o.tr1 = a1 - b1; o.ti1 = (g1 - a1) - b1;
     if (NOW) {
         const int64_t fr = f0 + ml;
-        if (fr < n) {
+        if (fr < n && !(skip && skip[fr])) {
             st2(Y, fr * ys + 48 + kl, make_double2(o.tr0, o.ti0));
             if (kl == 0) st2(Y, fr * ys + 52, make_double2(o.tr1, o.ti1));
         }
@@ -3533,7 +3671,7 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
 }
 
 __device__ __forceinline__ void apply_tile_store(const ApplyAcc &o, double *Y, int64_t ys, int64_t f0, int64_t n,
-                                                 int ml, int kl)
+                                                 int ml, int kl, const uint8_t *__restrict__ skip)
 {
 #pragma unroll
     for (int nt = 0; nt < APPLY_NT; ++nt) {
@@ -3542,19 +3680,20 @@ __device__ __forceinline__ void apply_tile_store(const ApplyAcc &o, double *Y, i
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t fr = f0 + kl + 4 * r;
-                if (fr < n) st2(Y, fr * ys + i, make_double2(o.r[nt][r], o.i[nt][r]));
+                if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(o.r[nt][r], o.i[nt][r]));
             }
         }
     }
     const int64_t fr = f0 + ml;
-    if (fr < n) {
+    if (fr < n && !(skip && skip[fr])) {
         st2(Y, fr * ys + 48 + kl, make_double2(o.tr0, o.ti0));
         if (kl == 0) st2(Y, fr * ys + 52, make_double2(o.tr1, o.ti1));   // rows 53..55: padding, never stored
     }
 }
 
 __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const double *__restrict__ M, const double *X,
-                                                                        int64_t xs, double *Y, int64_t ys, int64_t n)
+                                                                        int64_t xs, double *Y, int64_t ys, int64_t n,
+                                                                        const uint8_t *__restrict__ skip)
 {
     __shared__ double2 sc[APPLY_ROWS * ACS];
     __shared__ double scs[WCE_APPLY_3M ? APPLY_ROWS * ACS : 1];   // Re c + Im c (3M form)
@@ -3586,7 +3725,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
             asm volatile("" ::"v"(ar[s]), "v"(ai[s]));   // W_g complete HERE, before the stores below are issued
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (fprev >= 0) apply_tile_store(acc, Y, ys, fprev, n, ml, kl);   // W_g has landed; W aliasing Y: tile fprev's W was read a tile ago
+        if (fprev >= 0) apply_tile_store(acc, Y, ys, fprev, n, ml, kl, skip);   // W_g has landed; W aliasing Y: tile fprev's W was read a tile ago
         __builtin_amdgcn_sched_barrier(0);
         if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);
         __builtin_amdgcn_sched_barrier(0);
@@ -3594,7 +3733,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
         else apply_tile_acc<WCE_APPLY_PF ? WCE_APPLY_PF : 5>(sc, ar, ai, ml, kl, acc);
         fprev = 16 * g;
     }
-    apply_tile_store(acc, Y, ys, fprev, n, ml, kl);
+    apply_tile_store(acc, Y, ys, fprev, n, ml, kl, skip);
     return;
 #endif
     for (; g < ng; g += stride) {
@@ -3609,7 +3748,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
 #if WCE_APPLY_3M
         {
             ApplyAcc unused;
-            apply_tile_acc3<WCE_APPLY_PF ? WCE_APPLY_PF : 2, true>(sc, scs, ar, ai, ml, kl, unused, Y, ys, f0, n);
+            apply_tile_acc3<WCE_APPLY_PF ? WCE_APPLY_PF : 2, true>(sc, scs, ar, ai, ml, kl, unused, Y, ys, f0, n, skip);
         }
         continue;
 #endif
@@ -3642,18 +3781,23 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
     }
 }
 
-int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream)
+int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream,
+                      const uint8_t *skip)
 {
     // the streaming kernel once every wave gets >= 4 tiles (131,072 frames on
     // 256 CUs); below that one wave round of matvec_kernel is as fast or faster
     // (profiles/r02_ab_apply.txt)
     const int64_t tiles = (n + 15) / 16;
-    if (!WCE_APPLY_V2 || tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * WCE_APPLY_WG_PER_CU)
-        return launch_matvec(st->C, nullptr, W, stride, H, nullptr, stride, n, false, stream);
+    if (!WCE_APPLY_V2 || tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * WCE_APPLY_WG_PER_CU) {
+        const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
+        hipLaunchKernelGGL((matvec_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                           st->C, nullptr, W, stride, H, nullptr, stride, n, skip);
+        return hip_status(hipGetLastError());
+    }
     static_assert(APPLY_WAVES == LS_WAVES, "tile_blocks counts LS_WAVES waves per workgroup");
     const int64_t blocks = tile_blocks(tiles, APPLY_WAVES * WCE_APPLY_WG_PER_CU);
     hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st->C, W, stride, H,
-                       stride, n);
+                       stride, n, skip);
     return hip_status(hipGetLastError());
 }
 
@@ -3664,7 +3808,7 @@ int launch_matvec_avg(const double *M, const double *X, int64_t xs, int nb, doub
     if (nb != 4) return WCE_EINVAL;   // MATLAB semantics averages blocks 1..4
     const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
     hipLaunchKernelGGL((matvec_kernel<false, false, 4>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                       M, nullptr, X, xs, Y, nullptr, ys, n);
+                       M, nullptr, X, xs, Y, nullptr, ys, n, (const uint8_t *)nullptr);
     return hip_status(hipGetLastError());
 }
 
@@ -3676,9 +3820,10 @@ int launch_matvec(const double *M1, const double *M2, const double *X, int64_t x
     const dim3 g((unsigned)blocks), b(256);
     hipStream_t s = (hipStream_t)stream;
     if (qin && M2) return WCE_EINVAL;
-    if (qin) hipLaunchKernelGGL((matvec_kernel<true, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
-    else if (M2) hipLaunchKernelGGL((matvec_kernel<false, true>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
-    else hipLaunchKernelGGL((matvec_kernel<false, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n);
+    const uint8_t *none = nullptr;
+    if (qin) hipLaunchKernelGGL((matvec_kernel<true, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n, none);
+    else if (M2) hipLaunchKernelGGL((matvec_kernel<false, true>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n, none);
+    else hipLaunchKernelGGL((matvec_kernel<false, false>), g, b, 0, s, M1, M2, X, xs, Y1, Y2, ys, n, none);
     return hip_status(hipGetLastError());
 }
 
@@ -3692,6 +3837,16 @@ int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int
     hipStream_t s = (hipStream_t)stream;
     if (hout) hipLaunchKernelGGL(ref_fc_kernel<true>, g, b, 0, s, st, a, rx_pre, ps, tx_pre, uw, ww, wld);
     else hipLaunchKernelGGL(ref_fc_kernel<false>, g, b, 0, s, st, a, rx_pre, ps, tx_pre, uw, ww, wld);
+    return hip_status(hipGetLastError());
+}
+
+int launch_cm(const State *st, const SolveArgs &a, uint8_t *flags, void *stream)
+{
+    if (a.n <= 0) return WCE_OK;
+    if (a.split || !flags) return WCE_EINVAL;
+    const int64_t blocks = (a.n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
+    hipLaunchKernelGGL(cm_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, flags);
+    hipLaunchKernelGGL(cm_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, flags);
     return hip_status(hipGetLastError());
 }
 

@@ -467,7 +467,111 @@ int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
     st->mode = WCE_MMSE_COV;
     return WCE_OK;
 }
+// WCE_MMSE_COV, constant-modulus frames (round 4): for frames whose symbols
+// have |x_k|^2 = p_k on every subcarrier (p from x_ref; 0 off the X mask),
+// C X^H (a X C X^H + b I)^-1 = (a C P + b I)^-1 C X^H (push-through), so
+//     K = (a C P + b I)^-1 C = U (a U^H P U + b I_r)^-1 U^H      (C = U U^H)
+// is frame-independent.  It is formed in 80 bits through the eigen-
+// decomposition of the r x r Hermitian G = a U^H P U + b I = Q D Q^H (cyclic
+// Jacobi): K = (U Q) D^-1 (U Q)^H.  G has cond up to 1 + a lambda_max p / b
+// (~2e6 at the bench's SNR); an explicitly inverted Cholesky factor would
+// carry eps cond(G)^2 into K y, the eigen form eps cond(G) = ~1e-13 at 80 bits,
+// and rounding K to fp64 adds ~sqrt(53) eps.
+int host_build_cm(State *st, const ldc *Fl, const wce_complex *Rhh, const wce_complex *x_ref)
+{
+    if (st->mode != WCE_MMSE_COV) return WCE_EINVAL;
+    std::memset(st->Kcm, 0, sizeof(st->Kcm));
+    std::memset(st->pcm, 0, sizeof(st->pcm));
+    st->cm_on = 0;
+    if (!x_ref) return WCE_OK;
+    if (!Rhh) return WCE_EINVAL;
+    const int n = NSC;
+    double p[NSC];
+    for (int k = 0; k < n; k++) {
+        if (!std::isfinite(x_ref[k].re) || !std::isfinite(x_ref[k].im)) return WCE_EINVAL;
+        // the kernel's |x|^2, bit for bit: fma(re, re, im * im)
+        p[k] = ((st->xmask >> k) & 1ull) ? std::fma(x_ref[k].re, x_ref[k].re, x_ref[k].im * x_ref[k].im) : 0.0;
+    }
+    // U (80 bits) from the Hermitian part of Rhh, exactly as host_apply_cov keeps it
+    std::vector<ldc> Rh(n * n), V(n * n);
+    std::vector<long double> lam(n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            Rh[i * n + j].re = 0.5L * ((long double)Rhh[i * n + j].re + Rhh[j * n + i].re);
+            Rh[i * n + j].im = 0.5L * ((long double)Rhh[i * n + j].im - Rhh[j * n + i].im);
+        }
+    host_hermitian_eig(Rh.data(), n, lam.data(), V.data());
+    long double lmax = 0.0L;
+    for (int j = 0; j < n; j++) lmax = std::max(lmax, lam[j]);
+    std::vector<int> ord(n);
+    for (int j = 0; j < n; j++) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](int x, int y) { return lam[x] > lam[y]; });
+    int r = 0;
+    while (r < n && lam[ord[r]] > kCovRankTol * lmax && lmax > 0.0L) r++;
+    if (r != st->cov_rank) return WCE_EINVAL;   // not the Rhh this state was built from
+    if (r == 0) { st->cm_on = 1; std::memcpy(st->pcm, p, sizeof(p)); return WCE_OK; }   // C = 0: K = 0
+    std::vector<cld> F(n * n), U((size_t)n * r);
+    for (int i = 0; i < n * n; i++) F[i] = from(Fl[i]);
+    for (int j = 0; j < r; j++) {
+        const long double sl = sqrtl(lam[ord[j]]);
+        for (int k = 0; k < n; k++) {
+            cld u = mk(0, 0);
+            for (int t = 0; t < n; t++) u = u + F[k * n + t] * from(V[t * n + ord[j]]);
+            U[(size_t)k * r + j] = u * mk(sl, 0.0L);
+        }
+    }
+    // G = a U^H P U + b I
+    std::vector<ldc> G((size_t)r * r), Q((size_t)r * r);
+    std::vector<long double> d(r);
+    const long double a = st->acoef, b = st->bcoef;
+    for (int i = 0; i < r; i++)
+        for (int j = 0; j < r; j++) {
+            cld acc = mk(0, 0);
+            for (int k = 0; k < n; k++) {
+                cld ui = U[(size_t)k * r + i];
+                __imag__ ui = -__imag__ ui;
+                acc = acc + ui * U[(size_t)k * r + j] * mk((long double)p[k], 0.0L);
+            }
+            acc = acc * mk(a, 0.0L);
+            if (i == j) acc = acc + mk(b, 0.0L);
+            G[(size_t)i * r + j] = to(acc);
+        }
+    host_hermitian_eig(G.data(), r, d.data(), Q.data());
+    // W = U Q (n x r); K = W D^-1 W^H
+    std::vector<cld> W((size_t)n * r);
+    for (int k = 0; k < n; k++)
+        for (int l = 0; l < r; l++) {
+            cld acc = mk(0, 0);
+            for (int m = 0; m < r; m++) acc = acc + U[(size_t)k * r + m] * from(Q[(size_t)m * r + l]);
+            W[(size_t)k * r + l] = acc;
+        }
+    for (int l = 0; l < r; l++)
+        if (!(d[l] > 0.0L)) return WCE_EINVAL;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            cld acc = mk(0, 0);
+            for (int l = 0; l < r; l++) {
+                cld wj = W[(size_t)j * r + l];
+                __imag__ wj = -__imag__ wj;
+                acc = acc + W[(size_t)i * r + l] * wj * mk(1.0L / d[l], 0.0L);
+            }
+            st->Kcm[2 * (i * CLD + j)] = (double)__real__ acc;
+            st->Kcm[2 * (i * CLD + j) + 1] = (double)__imag__ acc;
+        }
+    std::memcpy(st->pcm, p, sizeof(p));
+    st->cm_on = 1;
+    return WCE_OK;
+}
 }  // namespace wce
+
+extern "C" int wce_state_set_modulus(void *blob, size_t bytes, const wce_complex *Rhh, const wce_complex *x_ref)
+{
+    using namespace wce;
+    if (!blob || bytes < sizeof(State)) return WCE_EINVAL;
+    State *st = static_cast<State *>(blob);
+    if (!state_ok(st) || st->mode != WCE_MMSE_COV) return WCE_EINVAL;
+    return host_build_cm(st, host_reference_F(), Rhh, x_ref);
+}
 
 extern "C" int wce_state_build_cov(void *out, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
                                    const wce_complex *Rhh, double ow2)

@@ -105,6 +105,9 @@ ABI = {
     "wce_debug_cov_factor": [c_void_p, c_size_t, c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_double),
                              POINTER(c_double)],
     "wce_ctx_cov_info": [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_double), POINTER(c_double)],
+    "wce_ctx_set_modulus": [c_void_p, c_void_p],
+    "wce_state_set_modulus": [c_void_p, c_size_t, c_void_p, c_void_p],
+    "wce_debug_set_cm": [c_void_p, c_int],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
@@ -333,6 +336,20 @@ class Context:
         _check(load().wce_ctx_cov_info(self.handle, ctypes.byref(r), ctypes.byref(lr), ctypes.byref(lmax),
                                        ctypes.byref(lmin)), "cov_info")
         return r.value, bool(lr.value), lmax.value, lmin.value
+
+    def set_modulus(self, x_ref):
+        """WCE_MMSE_COV: the constant-modulus operator for frames with |x|^2 = |x_ref|^2 (None: off)."""
+        if x_ref is None:
+            _check(load().wce_ctx_set_modulus(self.handle, None), "wce_ctx_set_modulus")
+            return
+        x = _as_c128(x_ref)
+        if x.shape != (NSC,):
+            raise ValueError("x_ref must hold 53 subcarriers")
+        _check(load().wce_ctx_set_modulus(self.handle, x.ctypes.data_as(c_void_p)), "wce_ctx_set_modulus")
+
+    def set_cm(self, on: bool):
+        """A/B switch of the constant-modulus path (default on once a pattern is set)."""
+        _check(load().wce_debug_set_cm(self.handle, int(bool(on))), "wce_debug_set_cm")
 
     def set_cov_path(self, path: int):
         """A/B: 0 = the state's choice, 1 = dense Ryy solve, 2 = low-rank Gram path."""

@@ -109,6 +109,22 @@ int wce_ctx_create_cov(wce_ctx **ctx, int device, const wce_complex *tx_pre, con
 /* WCE_MMSE_COV context: the rank r, whether the low-rank path runs (1) or the
  * dense one (0), and the largest / smallest kept eigenvalue of C (outputs may be NULL). */
 int wce_ctx_cov_info(wce_ctx *ctx, int *rank, int *low_rank, double *lambda_max, double *lambda_min);
+/* WCE_MMSE_COV, constant-modulus frames (round 4; WiFi_channel_estimation_PS_MMSE.m:29-32).
+ * Ryy depends on a frame's symbols only through P = diag |x_k|^2 (and their
+ * phases), and for PSK frames -- the reference's BPSK data (inputs.h), QPSK --
+ * P is the same for every frame.  x_ref: one frame's 53 symbols; p_k = |x_ref,k|^2
+ * (0 off the X mask) is the pattern.  The ctx forms once, in 80-bit on the
+ * host, K = (a C P + b I)^-1 C (the push-through of C X^H Ryy^-1) and uploads
+ * it.  Estimates in C semantics then check every frame on the device: a frame
+ * whose |x_k|^2 equals p_k bit for bit on all subcarriers takes
+ *     H = K (conj(x) o rx)   [+ C ((x - conj x) o (rx - a x o H1)) / b for non-real x]
+ * -- two batched f64-MFMA products, no per-frame factorisation -- and every
+ * other frame the per-frame solve, as without the pattern.  Ranks <= 8 keep
+ * the one-frame-per-lane kernels (already bound by the frames' HBM traffic).
+ * x_ref NULL: off.  Needs the ctx that built the state (wce_ctx_create_cov);
+ * it updates the shared state, so a multi-GPU run sets it before the
+ * broadcast.  Not safe against estimates in flight on this ctx. */
+int wce_ctx_set_modulus(wce_ctx *ctx, const wce_complex *x_ref);
 
 /* Device pointer and size of the packed shared state (C, H_LT, tx_pre, sinc
  * table, MMSE coefficients): the single buffer a multi-GPU run broadcasts
@@ -125,6 +141,8 @@ int wce_state_build(void *host_state, size_t bytes, const wce_complex *tx_pre, c
 int wce_state_build_cov(void *host_state, size_t bytes, const wce_complex *tx_pre, const wce_complex *rx_pre,
                         const wce_complex *Rhh, double ow2);
 int wce_ctx_load_state(wce_ctx *ctx, const void *host_state, size_t bytes);
+/* wce_ctx_set_modulus on a host blob built by wce_state_build_cov from the same Rhh. */
+int wce_state_set_modulus(void *host_state, size_t bytes, const wce_complex *Rhh, const wce_complex *x_ref);
 /* Host-only check of a state blob (e.g. bytes received from another rank):
  * WCE_OK and its MMSE mode (may be NULL) if it holds a valid state, else
  * WCE_EINVAL (too short) / WCE_ESTATE (no valid magic). */

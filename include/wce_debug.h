@@ -55,6 +55,8 @@ int wce_debug_set_cov_path(struct wce_ctx *ctx, int path);
  * units runs under the current variant (e.g. "mmse_lr_lane_staged_kernel<8, 2>");
  * "" for a ctx on the dense path.  For bench labels and the gate's checks. */
 const char *wce_debug_lr_kernel(struct wce_ctx *ctx, long long units);
+/* A/B switch of the constant-modulus path (wce_ctx_set_modulus); on by default. */
+int wce_debug_set_cm(struct wce_ctx *ctx, int on);
 #ifdef __cplusplus
 }
 #endif

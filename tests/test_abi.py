@@ -115,6 +115,9 @@ def test_no_device_fails_loudly(wce):
         wce.WiFi_channel_estimation_PS_Linear(np.ones(N), np.ones(N))
 
 
+CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16     # State's constant-modulus operator Kcm, pattern pcm, cm_on (+ 12 B)
+
+
 def _pdp_cov(L=53, decay=0.12):
     """Exponential power-delay-profile channel covariance (time domain, full rank)."""
     p = np.exp(-decay * np.arange(L))
@@ -135,9 +138,9 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
     assert np.max(np.abs(C - ref)) / np.max(np.abs(ref)) < 1e-14
     # State tail: a, b, ow2, xmask, mode, magic, then the low-rank factor
     # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0,
-    # the layout version and size (+ 8 B reserved), and the lane kernel's P_k
-    # (53 x 36 complex)
-    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 16 + 53 * 36 * 16)]
+    # the layout version and size (+ 8 B reserved), the lane kernel's P_k
+    # (53 x 36 complex) and the constant-modulus operator (CM_TAIL)
+    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 16 + 53 * 36 * 16 + CM_TAIL)]
     a, b, ow2 = t[-40:-16].view(np.float64)
     mode, magic = t[-8:].view(np.int32)
     assert (a, b, ow2, mode, magic) == (1.0, inp["ow2"], inp["ow2"], wce.MMSE_COV, 0x80211)
@@ -147,7 +150,7 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
 
 def _state_field_offset(blob):
     """byte offset of (cov_rank, cov_k0, layout, bytes) in a state blob"""
-    return len(blob) - (53 * 36 * 16 + 24)
+    return len(blob) - (53 * 36 * 16 + 24 + CM_TAIL)
 
 
 def test_state_validation_rejects_foreign_blobs(wce, golden):

@@ -127,7 +127,9 @@ def test_lane_gram_factors(wce, oracle, inp, L, rot):
     blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
     U, r, _, _, _ = wce.cov_factor(blob)
     assert r == L
-    P = blob[len(blob) - N * 36 * 16:].view(np.complex128).reshape(N, 36)   # the State's last member
+    CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16   # the constant-modulus members after P_k (round 4)
+    end = len(blob) - CM_TAIL
+    P = blob[end - N * 36 * 16:end].view(np.complex128).reshape(N, 36)
     if L > 8:
         assert not np.any(P)
         return
@@ -139,3 +141,77 @@ def test_lane_gram_factors(wce, oracle, inp, L, rot):
     assert np.max(np.abs(P - ref)) < 4e-16 * scale * 4
     assert not np.any(P[:, [i * (i + 1) // 2 + i for i in range(8)]].imag)
     assert not np.any(P[:, L * (L + 1) // 2:])
+
+
+def _cm_operator(wce, blob, R, x_ref):
+    """wce_state_set_modulus on a host blob -> (K 53 x 53, pattern p, on)."""
+    import ctypes
+    lib = wce.load()
+    x = np.ascontiguousarray(x_ref, np.complex128)
+    Rc = np.ascontiguousarray(R, np.complex128)
+    rc = lib.wce_state_set_modulus(blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes, Rc.ctypes.data_as(ctypes.c_void_p),
+                                   x.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0, rc
+    tail = blob[len(blob) - (64 * 64 * 16 + 64 * 8 + 16):]
+    K = tail[:64 * 64 * 16].view(np.complex128).reshape(64, 64)[:N, :N]
+    p = tail[64 * 64 * 16:64 * 64 * 16 + 64 * 8].view(np.float64)[:N]
+    on = int(tail[-16:-12].view(np.int32)[0])
+    return K, p, on
+
+
+@pytest.mark.parametrize("L,decay", [(16, 0.5), (24, 0.3), (53, 0.5), (53, 0.12)])
+@pytest.mark.parametrize("kind", ["bpsk", "qpsk"])
+def test_constant_modulus_operator(wce, oracle, inp, L, decay, kind):
+    """K = (a C P + b I)^-1 C, formed in 80 bits through the eigen-decomposition
+    of a U^H P U + b I (wce_state.cpp host_build_cm), applied as the GPU's
+    constant-modulus path does -- H1 = K (conj x o rx), plus for non-real x
+    the correction C ((x - conj x) o (rx - a x o H1)) / b -- in fp64 numpy,
+    against the long double unified solve with C formed in 80 bits
+    (WiFi_channel_estimation_PS_MMSE.m:26-33) on frames whose symbols share
+    x_ref's moduli (DC null)."""
+    R = pdp_rhh(L, decay)
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    rng = np.random.default_rng(L + 100 * (kind == "qpsk"))
+    A = 8.8753
+
+    def symbols(m):
+        if kind == "bpsk":
+            x = rng.choice([-A, A], (m, N)).astype(np.complex128)
+        else:
+            x = A * (rng.choice([-1.0, 1.0], (m, N)) + 1j * rng.choice([-1.0, 1.0], (m, N))) / np.sqrt(2)
+        x[:, 26] = 0
+        return x
+    x = symbols(33)
+    K, p, on = _cm_operator(wce, blob, R, x[0])
+    assert on == 1 and p[26] == 0.0 and np.all(p[np.arange(N) != 26] == np.abs(x[0, 0]) ** 2 * 0 + p[0])
+    F = oracle.fmatrix()
+    C_ld = F @ oracle._ld(R) @ F.conj().T
+    C = np.asarray(C_ld, np.complex128)
+    h = (rng.standard_normal((33, N)) + 1j * rng.standard_normal((33, N))) * 0.01
+    rx = h * x + np.sqrt(inp["ow2"] / 2) * (rng.standard_normal((33, N)) + 1j * rng.standard_normal((33, N)))
+    ow2 = float(inp["ow2"])
+    worst = 0.0
+    for f in range(33):
+        H = K @ (np.conj(x[f]) * rx[f])
+        if kind == "qpsk":
+            H = H + (C @ ((x[f] - np.conj(x[f])) * (rx[f] - x[f] * H))) / ow2
+        exp = oracle.mmse_unified(C_ld, np.ones(N, np.uint8), 1.0, ow2, x[f], rx[f])
+        worst = max(worst, float(normrel(H, exp)))
+    print(f"\nL={L} decay={decay} {kind}: max {worst:.2e}")
+    assert worst < 1e-11
+
+
+def test_constant_modulus_rejects_mismatch(wce, inp):
+    import ctypes
+    lib = wce.load()
+    R = pdp_rhh(16, 0.5)
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    x = np.full(N, 8.8753 + 0j)
+    R2 = pdp_rhh(12, 0.5)                       # not the Rhh of this state (rank differs)
+    rc = lib.wce_state_set_modulus(blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes,
+                                   R2.ctypes.data_as(ctypes.c_void_p), x.ctypes.data_as(ctypes.c_void_p))
+    assert rc != 0
+    x[3] = np.nan
+    rc = lib.wce_state_set_modulus(blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes,
+                                   R.ctypes.data_as(ctypes.c_void_p), x.ctypes.data_as(ctypes.c_void_p))
+    assert rc != 0

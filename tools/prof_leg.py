@@ -49,6 +49,8 @@ LEGS = {
     "lowrank8": ("mmse_lr_lane_staged_kernel<8>", 65536),
     "lowrank16": ("mmse_lr_quad_kernel<16>", 65536),
     "lowrank8_1m": ("mmse_lr_lane_staged_kernel<8, 2>", 1 << 20),   # block 0 only, frame_stride 53
+    "cm16": ("cm_kernel<false>", 65536),         # constant-modulus operator path, 16-tap PDP (round 4)
+    "cm53": ("cm_kernel<false>", 65536),         # the same, 53-tap exp(-0.5 k) (wide spectrum)
 }
 
 
@@ -102,6 +104,16 @@ def main():
         del tx0, rx0
         assert ctx.lr_kernel(n) == LEGS[leg][0]
         H = wce.DeviceArray((n, N), zero=True)
+        run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
+                                   wce.PS_MMSE)
+    elif leg.startswith("cm"):
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rank(int(leg[2:])))
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211)
+        wce.synchronize()
+        ctx.set_modulus(tx.rows(0)[0, 0])
+        H = wce.DeviceArray((n, N), zero=True)
+        fr = ctx.frames(tx, rx, n)
         run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
                                    wce.PS_MMSE)
     elif leg.startswith("lowrank"):
