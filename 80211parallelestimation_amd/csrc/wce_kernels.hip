@@ -2603,6 +2603,15 @@ __global__ __launch_bounds__(256) void fc_finish_kernel(SolveArgs a, const doubl
 // =====================================================================
 constexpr int APPLY_WAVES = 4;
 
+// A 16-frame tile whose every live frame is flagged done (the constant-modulus
+// path wrote their H) needs no W loads, MFMAs or stores (wave-uniform).
+__device__ __forceinline__ bool tile_done(const uint8_t *__restrict__ skip, int64_t f0, int64_t n, int lane)
+{
+    if (!skip) return false;
+    const int64_t f = f0 + (lane & 15);
+    return __ballot(f < n && skip[f] == 0) == 0;
+}
+
 #ifndef WCE_APPLY_3M   // H = C W with three real MFMA products per complex product (apply_tile_acc3, matvec_kernel)
 #define WCE_APPLY_3M 1
 #endif
@@ -2675,7 +2684,7 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
 {
     const int lane = threadIdx.x & 63;
     const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
-    if (f0 >= n) return;
+    if (f0 >= n || tile_done(skip, f0, n, lane)) return;
     const int ml = lane & 15, kl = lane >> 4;
     const int64_t fa = f0 + ml;
     double ar[KSTEPS], ai[KSTEPS], nai[KSTEPS];
@@ -3431,13 +3440,13 @@ constexpr int ACS = 58;
 // staged rows of C: 56 once rows 48..55 are the last ones read (tail_rows)
 constexpr int APPLY_ROWS = WCE_APPLY_TAIL4 ? 56 : 64;
 __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t n, int64_t g, int ml, int kl,
-                                           double2 (&w)[KSTEPS])
+                                           double2 (&w)[KSTEPS], bool done = false)
 {
     const int64_t fa = 16 * g + ml;
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
         const int j = 4 * s + kl;
-        w[s] = (fa < n && j < NSC) ? ld2(X, fa * xs + j) : make_double2(0, 0);
+        w[s] = (!done && fa < n && j < NSC) ? ld2(X, fa * xs + j) : make_double2(0, 0);
     }
 }
 
@@ -3711,7 +3720,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
     int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6);
     if (g >= ng) return;
     double2 wn[KSTEPS];
-    apply_load(X, xs, n, g, ml, kl, wn);
+    apply_load(X, xs, n, g, ml, kl, wn, tile_done(skip, 16 * g, n, lane));
 #if WCE_APPLY_DEFER
     static_assert(WCE_APPLY_TAIL4, "the deferred form holds the 4x4x4 tail rows");
     ApplyAcc acc;
@@ -3743,8 +3752,10 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
             ar[s] = wn[s].x;
             ai[s] = wn[s].y;
         }
-        if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);   // next tile, under this one's MFMAs
+        if (g + stride < ng)   // next tile, under this one's MFMAs
+            apply_load(X, xs, n, g + stride, ml, kl, wn, tile_done(skip, 16 * (g + stride), n, lane));
         const int64_t f0 = 16 * g;
+        if (tile_done(skip, f0, n, lane)) continue;
 #if WCE_APPLY_3M
         {
             ApplyAcc unused;

@@ -381,7 +381,10 @@ def test_ls_outputs_f32(gpu_wce, golden, fuse):
     assert got["ps_mmse"].dtype == np.complex128
     assert normrel(got["ps_mmse"], ref["ps_mmse"]).max() < 1e-14
     e32 = got["eq"].reshape(B, -1).astype(np.complex128)
-    assert normrel(e32, ref["eq"].reshape(B, -1)).max() < 1e-7
+    # the equalizer divides in fp32 when its outputs are fp32 (WCE_EQ_F32_MATH,
+    # round 4: fp64 blend, fp32 quotient, <= 4e-7 in a numpy model): SURVEY
+    # 8(c) G4's 1e-6, no longer the store's rounding alone
+    assert normrel(e32, ref["eq"].reshape(B, -1)).max() < 1e-6
 
 
 def test_model_covariance_dense_solve(gpu_wce, golden, oracle):
