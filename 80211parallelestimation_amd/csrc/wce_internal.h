@@ -195,10 +195,9 @@ int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
 // kernel variants for A/B timing (wce_debug_set_variant)
-constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks (default), 1 = 64-frame tiles,
-                                      // 2 = chunks with an uncapped grid
-constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 0 = 512-element chunks (grid capped at 2,048 blocks),
-                                      // 1 = the same uncapped, 2 = one element per thread (ls_elem_kernel, default)
+constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks (grid capped, default), 2 = uncapped grid
+constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 2 = one element per thread (ls_elem_kernel, default),
+                                      // 3 = the per-frame LIGHT ls_kernel
 constexpr int WCE_VARIANT_REF_LS = 2;  // REF PS_MMSE + LS family (+ eq), C semantics: 0 = ref_ls_elem_kernel
                                       // (one element per thread, default), 1 = mmse_solve_ls_kernel (wave per frame)
 constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1..LRL_RMAX one frame per lane

@@ -4,8 +4,8 @@
 //   ls_kernel             LT_LS + PS_Linear/Cubic/Sinc + equalization, one
 //                         wave per frame, HBM streaming (main.c:66-146,
 //                         WiFi_Equalization.m); C or MATLAB semantics.
-//   ls_flat_kernel        LT_LS + PS_Linear only (BASELINE configs[1]), C
-//                         semantics, over flat (frame, subcarrier) elements.
+//   ls_elem_kernel        LT_LS + PS_Linear only (BASELINE configs[1]), C
+//                         semantics, one (frame, subcarrier) element per thread.
 //   mmse_ref_flat_kernel  PS_MMSE in main.c semantics (diagonal Ryy: 4 pilot
 //                         terms per frame, H = u s), flat elements, HBM-bound.
 //   solve_block           the per-frame MMSE core: Ryy = a X C X' + b I built
@@ -33,9 +33,6 @@
 #include "wce_device.h"
 
 // A/B and timing-only switches (tools/variants.sh); defaults are the product.
-#ifndef WCE_BS_SHFL      // A/B: back-substitution butterfly through ds_bpermute
-#define WCE_BS_SHFL 0
-#endif
 
 namespace wce {
 
@@ -186,9 +183,6 @@ __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, u
     }
 }
 template <bool EQ>
-#ifndef WCE_EQ_NT_LOAD   // A/B: the equalizer's rx blocks (read once) by nontemporal loads
-#define WCE_EQ_NT_LOAD 1
-#endif
 __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
                                          double2 hcub, double2 hsnc)
 {
@@ -196,7 +190,7 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
     if constexpr (EQ) {
 #pragma unroll
         for (int b = 0; b < NBLK; b++)
-            rv[b] = WCE_EQ_NT_LOAD ? ld2_nt(a.rx, f * a.fs + k + b * a.bs) : ld2(a.rx, f * a.fs + k + b * a.bs);
+            rv[b] = ld2_nt(a.rx, f * a.fs + k + b * a.bs);
     }
     ls_store_rv<EQ>(a, f, k, mask, hlt, hlin, hcub, hsnc, rv);
 }
@@ -205,9 +199,6 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
 // blocks 0..3 -- Linear/Cubic/Sinc are linear in the pilot values, so the
 // 4-block average of the per-block estimates is the per-block formula applied
 // to the averaged pilots -- proper conj in LT_LS, cubic divisors 14/28/42.
-#ifndef WCE_LS_NO_LIGHT   // A/B: route config 2 through the generic LS kernel
-#define WCE_LS_NO_LIGHT 0
-#endif
 // LIGHT: the request is a subset of LT_LS | PS_Linear (BASELINE configs[1]);
 // the Cubic/Sinc constants and paths compile out, which keeps the kernel under
 // 128 VGPRs (4 waves/SIMD: twice the loads in flight of the generic kernel).
@@ -287,20 +278,12 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 }
 
 // =====================================================================
-// LT_LS + PS_Linear, C semantics (BASELINE configs[1]) over the flat element
-// index e = f * 53 + k of a frame range.  Every lane of every load and store
-// instruction carries one (frame, subcarrier) element, so that 64-lane
-// instructions stream 1 KiB with no idle lanes 53..63.  The kernel is
-// latency-bound (its two input streams do not overlap, r01_ab_ls.txt):
-// what it needs is bytes in flight, and ~60 VGPRs give 8 waves/SIMD where
-// the per-frame kernel holds 2.  A wave-chunk is 512 elements (<= 11 frames).
-// Its pilot LS values (4 per frame, one division each on lanes 4j+p) go
-// through a per-wave LDS table.  The arithmetic is ls_kernel's: outputs are
-// bit-identical.
+// LT_LS + PS_Linear, C semantics (BASELINE configs[1]): ls_elem_kernel below,
+// one (frame, subcarrier) element per thread.  The flat-index machinery here
+// (frames per launch, 512-element wave-chunks) also serves the REF read-out
+// (mmse_ref_flat_kernel) and the non-finite scan.  (Round 1's ls_flat_kernel,
+// 512-element chunks per wave, was retired in round 4: profiles/r02_ab_ls.txt.)
 // =====================================================================
-#ifndef WCE_LS_FLAT   // A/B: 0 = configs[1] requests run the per-frame LIGHT kernel
-#define WCE_LS_FLAT 1
-#endif
 #ifndef WCE_FLAT_U
 #define WCE_FLAT_U 8
 #endif
@@ -322,88 +305,12 @@ int set_flat_chunk(int64_t frames)
     return WCE_OK;
 }
 
-__global__ __launch_bounds__(256) void ls_flat_kernel(const State *__restrict__ st, LsArgs a, int64_t f_begin,
-                                                      uint32_t nfr)
-{
-    __shared__ double2 s_txp[64], s_hlt[64];
-    __shared__ double2 s_hp[LS_WAVES][4 * FLAT_FR];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool do_lt = (a.mask & WCE_EST_LT_LS) && a.lt, do_lin = (a.mask & WCE_EST_PS_LINEAR) && a.lin;
-    const bool f32 = a.f32 != 0;
-    if (threadIdx.x < NSC) {
-        s_txp[threadIdx.x] = ld2(a.tx_pre ? a.tx_pre : st->tx_pre, threadIdx.x);
-        s_hlt[threadIdx.x] = ld2(st->h_lt, threadIdx.x);
-    }
-    __syncthreads();
-    const uint32_t E = nfr * (uint32_t)NSC;
-    const uint32_t nchunks = (E + FLAT_CHUNK - 1) / FLAT_CHUNK;
-    const int pj = lane & 3;
-    const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
-    double2 *hp_tab = s_hp[w];
-    for (uint32_t c = blockIdx.x * LS_WAVES + w; c < nchunks; c += gridDim.x * LS_WAVES) {
-        const uint32_t e0 = c * FLAT_CHUNK;
-        const uint32_t ff = e0 / NSC;                       // first frame of the chunk
-        // ---- every load of the chunk issued before any use
-        double2 ptx = make_double2(1, 0), prx = make_double2(0, 0);
-        if (do_lin && lane < 4 * FLAT_FR) {
-            const uint32_t fr = min(ff + (uint32_t)(lane >> 2), nfr - 1);
-            const int64_t o = (f_begin + fr) * a.fs + (int64_t)a.blk * a.bs + pil;
-            ptx = ld2(a.tx, o);
-            prx = ld2(a.rx, o);
-        }
-        double2 rp[FLAT_U];
-#pragma unroll
-        for (int i = 0; i < FLAT_U; ++i) {
-            const uint32_t e = min(e0 + 64u * i + lane, E - 1);
-            const uint32_t f = e / NSC, k = e - f * NSC;
-            rp[i] = (do_lt && a.rx_pre) ? ld2(a.rx_pre, (f_begin + f) * a.ps + k) : make_double2(0, 0);
-        }
-        if (do_lin) {
-            const double2 hp = cdiv(prx, ptx);              // main.c:82-84
-            if (lane < 4 * FLAT_FR) hp_tab[lane] = hp;
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int i = 0; i < FLAT_U; ++i) {
-            const uint32_t e = e0 + 64u * i + lane;
-            const uint32_t f = e / NSC, k = e - f * NSC;
-            const int64_t o = (f_begin + f) * a.os + k;
-            if (do_lt) {                                    // main.c:66-75
-                double2 h = s_hlt[k];
-                if (a.rx_pre) {
-                    const double2 t = s_txp[k];
-                    const double cq = t.x - t.y;
-                    h = cdiv(make_double2(cq * rp[i].x, cq * rp[i].y), make_double2(cq * t.x, cq * t.y));
-                }
-                if (k == WCE_DC) h = make_double2(0, 0);
-                if (e < E) st_out(a.lt, o, h, f32);
-            }
-            if (do_lin) {                                   // main.c:86-99
-                const int seg = k < WCE_P1 ? 0 : (k < WCE_P2 ? 1 : 2);
-                const double alpha = (double)((int)k - (seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2))) *
-                                     (1.0 / 14.0);
-                const int fl = (int)(f - ff) * 4 + seg;
-                const double2 lo = hp_tab[fl < 4 * FLAT_FR - 1 ? fl : 4 * FLAT_FR - 2];
-                const double2 hi = hp_tab[fl < 4 * FLAT_FR - 1 ? fl + 1 : 4 * FLAT_FR - 1];
-                if (e < E) st_out(a.lin, o, clerp(lo, hi, alpha), f32);
-            }
-        }
-        wave_lds_sync();                                    // hp_tab is rewritten by the next chunk
-    }
-}
-
 // One (frame, subcarrier) element per thread, no grid stride (round 2): the
 // store pattern that streams fastest on MI355X (7.0 TB/s one-shot against
 // 4.7 TB/s grid-strided, profiles/r02_ubench_hbm.txt).  Each lane loads the
 // two pilot pairs its linear segment needs (the lanes of a wave cover ~1.2
 // frames, so one pilot load instruction touches ~2 sectors) and divides them
 // itself; the arithmetic is ls_kernel's, so outputs are bit-identical.
-#ifndef WCE_LS_NT_LOAD   // A/B: nontemporal loads of rx_pre in ls_elem_kernel
-#define WCE_LS_NT_LOAD 1
-#endif
-#ifndef WCE_LS_NT_PILOT  // A/B: nontemporal pilot loads too
-#define WCE_LS_NT_PILOT 0
-#endif
 __global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ st, LsArgs a, int64_t f_begin,
                                                       uint32_t nfr)
 {
@@ -425,24 +332,13 @@ __global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ 
         const int64_t o = fg * a.fs + (int64_t)a.blk * a.bs;
         const int plo = seg == 0 ? WCE_P0 : (seg == 1 ? WCE_P1 : WCE_P2);
         const int phi = seg == 0 ? WCE_P1 : (seg == 1 ? WCE_P2 : WCE_P3);
-        if (WCE_LS_NT_PILOT) {
-            plo_t = ld2_nt(a.tx, o + plo);
-            plo_r = ld2_nt(a.rx, o + plo);
-            phi_t = ld2_nt(a.tx, o + phi);
-            phi_r = ld2_nt(a.rx, o + phi);
-        } else {
-            plo_t = ld2(a.tx, o + plo);
-            plo_r = ld2(a.rx, o + plo);
-            phi_t = ld2(a.tx, o + phi);
-            phi_r = ld2(a.rx, o + phi);
-        }
+        plo_t = ld2(a.tx, o + plo);   // (cached: the next frame's lanes reuse the sectors; nontemporal 588 -> 625 us)
+        plo_r = ld2(a.rx, o + plo);
+        phi_t = ld2(a.tx, o + phi);
+        phi_r = ld2(a.rx, o + phi);
     }
     if (do_lt && a.rx_pre) {
-        if (WCE_LS_NT_LOAD) {   // streamed once: nontemporal
-            rp = ld2_nt(a.rx_pre, fg * a.ps + k);
-        } else {
-            rp = ld2(a.rx_pre, fg * a.ps + k);
-        }
+        rp = ld2_nt(a.rx_pre, fg * a.ps + k);   // streamed once: nontemporal
     }
     const int64_t out = fg * a.os + k;
     if (do_lt) {                                    // main.c:66-75
@@ -467,17 +363,11 @@ __global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ 
 // X keeps the 4 pilots only (main.c:148-212, repaired as in DESIGN.md s2):
 // H_f = u_f s_f with s_f = sum_p w_f[P_p] tx_f[P_p] rx_f[P_p] / b.  Per frame
 // that is 4 pilot pairs in (64-B sectors, as the LS path) and 53 outputs:
-// HBM-bound, so it runs like ls_flat_kernel over e = 53 f + k -- lanes 4j+p
+// HBM-bound, so it runs over the flat element index e = 53 f + k -- lanes 4j+p
 // form frame j's pilot terms, a quad DPP sum gives s_j into a per-wave LDS
 // table, and every element lane writes u[k] s.  cs == 0: one shared (u, w)
 // (the ctx's C_ref); cs != 0: per-frame factors (WCE_MMSE_FRAME_COV).
 // =====================================================================
-#ifndef WCE_REF_FLAT   // A/B: 0 = REF runs inside mmse_solve_fc_kernel (one wave per frame)
-#define WCE_REF_FLAT 1
-#endif
-#ifndef WCE_REF_TILE_WAVES_PER_CU
-#define WCE_REF_TILE_WAVES_PER_CU 28   // 71 VGPRs: 7 waves/SIMD
-#endif
 template <int CTRL>
 __device__ __forceinline__ double dpp_quad(double v)
 {
@@ -627,75 +517,6 @@ __global__ __launch_bounds__(256) void ref_ls_elem_kernel(const State *__restric
 }
 
 // =====================================================================
-// Frame tiles (round 2): a wave owns 64 consecutive frames at a time.  Lane j
-// issues ALL of frame j's pilot loads at once (8 x 16 B: 512 B in flight per
-// lane, against 2 x 16 B on 44 lanes per 512-element chunk above), reduces
-// them lane-locally, and publishes one value per frame through a per-wave LDS
-// table; the wave then streams the tile's 64 x 53 outputs -- one contiguous
-// 54 KB run -- with 53 full-wave nontemporal 16-B stores, element
-// e = 64 i + lane walked incrementally (k += 11, f += 1, wrap at 53: no
-// division).  The grid holds one wave per resident slot (launch_flat_tiles).
-// =====================================================================
-constexpr int TILE_F = 64;                 // frames per wave tile
-
-// element walk of a tile: lane l starts at (f, k) = (l / 53, l % 53)
-struct TileWalk {
-    int f, k;
-    __device__ __forceinline__ explicit TileWalk(int lane) : f(lane >= NSC ? 1 : 0), k(lane >= NSC ? lane - NSC : lane) {}
-    __device__ __forceinline__ void next()
-    {
-        k += 64 - NSC;
-        f += 1;
-        if (k >= NSC) { k -= NSC; f += 1; }
-    }
-};
-
-__global__ __launch_bounds__(256) void mmse_ref_tile_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
-                                                            uint32_t nfr)
-{
-    __shared__ double2 s_u[64];
-    __shared__ double2 s_s[LS_WAVES][TILE_F];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool shared = a.cs == 0;
-    if (shared && threadIdx.x < NSC) s_u[threadIdx.x] = ld2(a.cu, threadIdx.x);
-    __syncthreads();
-    const double rb = 1.0 / st->bcoef;
-    const uint32_t ntiles = (nfr + TILE_F - 1) / TILE_F;
-    double2 *s_tab = s_s[w];
-    for (uint32_t t = blockIdx.x * LS_WAVES + w; t < ntiles; t += gridDim.x * LS_WAVES) {
-        const uint32_t f0 = t * TILE_F;
-        const uint32_t fr = min(f0 + (uint32_t)lane, nfr - 1);
-        const int64_t fo = (f_begin + fr) * a.fs + (int64_t)a.blk * a.bs;
-        double2 xt[4], xr[4], wp[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            xt[p] = ld2(a.tx, fo + PILOT[p]);
-            xr[p] = ld2(a.rx, fo + PILOT[p]);
-            const int64_t wo = shared ? PILOT[p] : (f_begin + fr) * a.cs + PILOT[p];
-            wp[p] = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
-        }
-        // s_j = w^T X rx / b over frame j's pilots, summed in quad_sum_c's
-        // order ((t0 + t1) + (t2 + t3)) so the result matches the chunked kernel
-        double2 tp[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) tp[p] = ref_term(wp[p], xt[p], xr[p]);
-        s_tab[lane] = ref_sum4(tp[0], tp[1], tp[2], tp[3], rb);
-        wave_lds_sync();
-        const uint32_t nf = min((uint32_t)TILE_F, nfr - f0);
-        const uint32_t ne = nf * NSC;
-        TileWalk wk(lane);
-        const int64_t obase = (f_begin + f0) * a.ws;
-#pragma unroll 4
-        for (uint32_t e = lane; e < ne; e += 64) {
-            const double2 u = shared ? s_u[wk.k] : ld2(a.cu, (f_begin + f0 + wk.f) * a.cs + wk.k);
-            st2_nt(a.w, obase + (int64_t)wk.f * a.ws + wk.k, ref_out(u, s_tab[wk.f]));
-            wk.next();
-        }
-        wave_lds_sync();   // s_tab is rewritten by the next tile
-    }
-}
-
-// =====================================================================
 // MMSE solve.  One wave per frame, lane = 8p + q holds A[p+8a][q+8b] for the
 // 28 register blocks a >= b (a, b < 7): the block-cyclic 8x8 grid spreads the
 // shrinking trailing matrix evenly over lanes.  Row 53 holds conj(rx), so the
@@ -736,39 +557,27 @@ struct SolveLds {
 __device__ __forceinline__ int conv_idx(int row, int c) { return row * CVS + c; }
 
 
-#ifndef WCE_RSQ_NEWTON2   // A/B: two Newton steps instead of one third-order step
-#define WCE_RSQ_NEWTON2 0
-#endif
 // 1/sqrt(d) from v_rsq_f64 (relative error ~2^-24).  One third-order
 // (Householder) step y += y e (1/2 + 3e/8), e = 1 - d y^2: error ~2^-72
-// before rounding, 5 VALU on a 4-deep chain (two Newton steps: 7 on 6).
+// before rounding, 5 VALU on a 4-deep chain (two Newton steps: 7 on 6, 2.1%
+// slower, retired in round 4).
 __device__ __forceinline__ double rsq_nr(double d)
 {
-    double y = __builtin_amdgcn_rsq(d);
-    if (WCE_RSQ_NEWTON2) {
-        const double hd = 0.5 * d;
-        double e = fma(-hd * y, y, 0.5);
-        y = fma(y, e, y);
-        e = fma(-hd * y, y, 0.5);
-        return fma(y, e, y);
-    }
+    const double y = __builtin_amdgcn_rsq(d);
     const double e = fma(-d * y, y, 1.0);
     return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
-#ifndef WCE_MASK_DEAD   // A/B: exec-mask the lanes whose updates are never read
-#define WCE_MASK_DEAD 1
-#endif
 // acc -= l conj(c) on the lanes of the (compile-time) lane mask m only.  The
 // other lanes carry elements that are never read (upper halves of diagonal
-// blocks, padding row 55, rows above the pivot in a row panel).  With
-// WCE_MASK_DEAD their FMAs are switched off in EXEC for the four FMAs (and
+// blocks, padding row 55, rows above the pivot in a row panel).  Their FMAs
+// are switched off in EXEC for the four FMAs (and
 // EXEC restored) inside one asm statement: written as a C++ branch the
 // compiler turns it into selects and divergent control flow that spills.
 // The masked lanes keep their old (dead) values: "+v" ties in to out.
 __device__ __forceinline__ void cmsub_live(uint64_t m, double2 &acc, double2 l, double2 c)
 {
-    if (WCE_MASK_DEAD && m != ~0ull) {
+    if (m != ~0ull) {
         // m & EXEC is formed by the compiler: the asm itself writes no SCC
         // (an s_and_b64 in here would clobber an SCC live across it)
         const uint64_t em = m & __builtin_amdgcn_read_exec();
@@ -819,9 +628,6 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
         cmsub_live(cm & kRows55, A[RB - 1][BB], Ur[RB - 1], v);
     }
 }
-#ifndef WCE_CHAIN_1LANE   // A/B: the pivot's 1/sqrt on one lane (EXEC = 1), result to SGPRs
-#define WCE_CHAIN_1LANE 1
-#endif
 // 1/sqrt(d) of a wave-uniform pivot d.  The kernel is power-capped, so the
 // 6-op chain runs on one lane alone (EXEC = that lane inside the asm) and
 // comes back as a scalar (v_readlane): the same arithmetic as rsq_nr (one
@@ -830,7 +636,6 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
 // control flow the asm never writes a lane that is switched off.
 __device__ __forceinline__ double rsq_uniform(double d)
 {
-    if (!WCE_CHAIN_1LANE) return rsq_nr(d);
     double y, t, e;
     uint64_t sv;
     const double c38 = 0.375;
@@ -851,84 +656,10 @@ __device__ __forceinline__ double rsq_uniform(double d)
     return readlane_f64(y, l0);   // the lane that computed it
 }
 
-// A[aa][BB] -= Ur[aa] * conj(v) for aa = BB..6
-template <int BB>
-__device__ __forceinline__ void upd_col(double2 (&A)[RB][RB], const double2 (&Ur)[RB], double2 v)
-{
-#pragma unroll
-    for (int aa = BB; aa < RB; ++aa) cmsub_conj(A[aa][BB], Ur[aa], v);
-}
-
-// Bulk of the rank-1 update, block columns BB..6.  The column operand
-// v = r * u[q + 8 bb] is read from LDS per block column (streamed), so only
-// the 7 row operands stay resident: fewer live registers, more waves.
-template <int BB>
-__device__ __forceinline__ void upd_cols_from(double2 (&A)[RB][RB], const double2 (&Ur)[RB], const double2 *col,
-                                              int q, double r)
-{
-    if constexpr (BB < RB) {
-        upd_col_live<BB>(A, Ur, cscale(col[q + 8 * BB], r));
-        upd_cols_from<BB + 1>(A, Ur, col, q, r);
-    }
-}
-
-// Publish column k (unscaled) from the lanes that own it (q == kq).  Only
-// stores sit under the branch: no register is redefined in it.
-template <int KB>
-__device__ __forceinline__ void publish_col(const double2 (&A)[RB][RB], double2 *buf, int p, int q, int kq)
-{
-    if (q == kq) {
-#pragma unroll
-        for (int aa = KB; aa < RB; ++aa) buf[p + 8 * aa] = A[aa][KB];
-    }
-}
-
-// Step k of the factorisation.  NEXT_IN_BLOCK: column k+1 lies in block KB
-// (runtime kq); otherwise k is the last column of block KB and the next pivot
-// opens block KB + 1 (compile-time), or k = 52 is the last pivot.
-template <int KB, bool NEXT_IN_BLOCK>
-__device__ __forceinline__ void ldl_step(double2 (&A)[RB][RB], SolveLds &s, int p, int q, double &r, double &rsel,
-                                         int kq)
-{
-    const int k = 8 * KB + kq;
-    const double2 *col = s.u[k & 1];
-    const double rk = r;
-    double2 Ur[RB];
-#pragma unroll
-    for (int aa = KB; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
-    rsel = (q == kq) ? rk : rsel;      // lanes of column k keep r_k (select: no LDS store per step)
-    double2 *next = s.u[(k + 1) & 1];
-    if constexpr (NEXT_IN_BLOCK) {
-        // lookahead: columns > k of block KB first; the lane mask is folded into r
-        const double rm = (q > kq) ? rk : 0.0;
-        if (WCE_MASK_DEAD == 2) {   // columns <= kq of block KB are final: masked instead of scaled by 0
-            const uint64_t byte = (0xffull << (kq + 1)) & 0xffull;
-            upd_col_live<KB>(A, Ur, cscale(col[q + 8 * KB], rk), byte * 0x0101010101010101ull);
-        } else {   // (a runtime mask costs more SALU than it saves here: A/B in profiles/r02_ab_mask.txt)
-            upd_col<KB>(A, Ur, cscale(col[q + 8 * KB], rm));
-        }
-        r = rcp_nr(readlane_f64(A[KB][KB].x, 9 * (kq + 1)));
-        publish_col<KB>(A, next, p, q, kq + 1);
-        upd_cols_from<KB + 1>(A, Ur, col, q, rk);
-    } else if constexpr (KB + 1 < RB) {
-        upd_col_live<KB + 1>(A, Ur, cscale(col[q + 8 * (KB + 1)], rk));
-        r = rcp_nr(readlane_f64(A[KB + 1][KB + 1].x, 0));
-        publish_col<KB + 1>(A, next, p, q, 0);
-        upd_cols_from<KB + 2>(A, Ur, col, q, rk);
-    }
-    wave_lds_sync();
-}
-
-template <int KB>
-__device__ __forceinline__ void ldl_panel(double2 (&A)[RB][RB], SolveLds &s, int p, int q, double &r)
-{
-    constexpr int NK = (KB == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
-    double rsel = 0.0;
-#pragma unroll 1
-    for (int kq = 0; kq < NK - 1; ++kq) ldl_step<KB, true>(A, s, p, q, r, rsel, kq);
-    ldl_step<KB, false>(A, s, p, q, r, rsel, NK - 1);
-    if (p == 0 && q < NK) s.rd[8 * KB + q] = rsel;   // one store per panel
-}
+// (Round 1's block-cyclic square-root-free LDL^H -- ldl_step / ldl_panel, a
+// masked 8-lane publish per pivot -- was retired in round 4; every path runs
+// the Cholesky row panels below.  Its measurements: profiles/r01_ab_publish.txt,
+// r02_ab_dense.txt.)
 
 // ---------------------------------------------------------------------
 // Row-per-lane panels (the rank-1 read-out path, DOT).  Publishing pivot
@@ -957,9 +688,6 @@ __device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)
 
 // Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
 // registers hold u = L D; r_j = 1/d_j rescales sums once per column.
-#ifndef WCE_BS_DPP   // A/B: back-substitution's diagonal solve takes z_t by DPP broadcast
-#define WCE_BS_DPP 1
-#endif
 template <int N>
 __device__ __forceinline__ double2 bcast_lane_c(double2 w)
 {
@@ -994,13 +722,7 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     constexpr int NROW = (BLK == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
     // w_j = r_j * (conj(u_53,j) - sum_{i solved} conj(u_ij) z_i),  j = 8*BLK + q
     double2 w = P[BLK];
-#if WCE_BS_SHFL
-    w = cadd(w, shfl_xor_c(w, 8));
-    w = cadd(w, shfl_xor_c(w, 16));
-    w = cadd(w, shfl_xor_c(w, 32));
-#else
     w = sum_over_p(w);   // DPP + permlane swaps: no LDS traffic
-#endif
     w = cscale(w, rq[BLK]);
     // L = u r of the diagonal block, strictly lower part only, scaled and
     // masked once by its owner (r depends on the column q only)
@@ -1016,7 +738,7 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
         // every lane with q = t holds w_t = z_t; DPP row_newbcast:t hands lane t
         // of each 16-lane row to the whole row (two VALU movs instead of four
         // readlanes through SGPRs; s_nop 1: w was written by the previous row)
-        const double2 z = WCE_BS_DPP ? bcast_row_lane<8>(w, t) : readlane_c(w, t);
+        const double2 z = bcast_row_lane<8>(w, t);
         cmsub_conj(w, z, lb[t]);                               // w_q -= conj(L[i][q]) z_i, q < t
     }
     if (p == 0 && q < NROW) s.z[8 * BLK + q] = w;              // one store per block
@@ -1026,9 +748,6 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     for (int bb = 0; bb < BLK; ++bb) cmsub_conj(P[bb], zp, A[BLK][bb]);
 }
 
-#ifndef WCE_PREFETCH_C
-#define WCE_PREFETCH_C 0
-#endif
 #ifndef WCE_ABLATE_KEEP  // timing-only build: dense Cholesky without keeping L (with WCE_ABLATE_BACKSOLVE)
 #define WCE_ABLATE_KEEP 0
 #endif
@@ -1038,20 +757,8 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
 #ifndef WCE_SOLVE_WAVES_PER_SIMD
 #define WCE_SOLVE_WAVES_PER_SIMD 3
 #endif
-#ifndef WCE_SOLVE_NT_LOAD   // A/B: the solve's frame loads (read once) nontemporal
-#define WCE_SOLVE_NT_LOAD 0
-#endif
-#ifndef WCE_STASH_COLS   // dense Cholesky: finished panel columns to LDS as they complete
-#define WCE_STASH_COLS 1
-#endif
-#ifndef WCE_DENSE_CHOL   // A/B: dense-C solve by row-panel Cholesky keeping L (else block-cyclic LDL^H)
-#define WCE_DENSE_CHOL 1
-#endif
 #ifndef WCE_DENSE_WAVES_PER_SIMD
 #define WCE_DENSE_WAVES_PER_SIMD WCE_SOLVE_WAVES_PER_SIMD
-#endif
-#ifndef WCE_DENSE_SCALED   // A/B: dense C solved as M = C + diag(b / (a |x|^2)) (no per-element X scaling)
-#define WCE_DENSE_SCALED 1
 #endif
 // Dense C, scaled form.  Ryy = a X C X^H + b I = a X M X^H with
 // M = C + diag(b / (a |x_i|^2)), so Ryy^-1 rx = X^-H M^-1 y / a, y = X^-1 rx,
@@ -1097,9 +804,6 @@ __device__ __forceinline__ void upd_cols_chol(double2 (&A)[RB][RB], const double
     }
 }
 
-#ifndef WCE_DPP_PANEL   // in-panel operands by DPP row_newbcast from one prefetched LDS read per step
-#define WCE_DPP_PANEL 1
-#endif
 // acc -= l conj(c_k[8KB + N]) for the row-per-lane panel, where R holds
 // c_k[8KB + (lane & 7)]: DPP row_newbcast:N hands lane N of each 16-lane row
 // (= c_k[8KB + N]) to the whole row as the FMA's first operand (gfx950's
@@ -1137,7 +841,7 @@ __device__ __forceinline__ void cmsub_panel(int c, double2 &acc, double2 l, doub
 // Panel KB in row form.  Entering: P = block column KB with P[0] = c_{8KB}
 // (scaled), c_{8KB} published.
 // K0 = 1: pivot 8KB is already eliminated (exact_first_step), c_{8KB+1} published.
-// R (WCE_DPP_PANEL): c_k[8KB + (lane & 7)] for the step about to run, read
+// R: c_k[8KB + (lane & 7)] for the step about to run, read
 // for step k+1 right after c_{k+1} is published, so the next lookahead does
 // not wait for an LDS round trip.
 // rsel = sel ? rs : rsel, materialised now: left to itself the compiler
@@ -1156,19 +860,12 @@ __device__ __forceinline__ void keep_where(bool sel, double2 &a, double2 c)
     a.y = sel ? c.y : a.y;
 }
 
-#ifndef WCE_KEEP_EXEC   // the KEEP path's per-step lane writes as EXEC-masked moves instead of compare + selects
-#define WCE_KEEP_EXEC 1
-#endif
 // rsel[lane L] = rs (wave-uniform, in SGPRs): one v_mov_b64 under EXEC = lane L
 // instead of v_cmp + two v_cndmask per step.  L is a constant after unrolling.
 // The mask is ANDed with the incoming EXEC (formed outside the asm, which
 // writes no SCC), so a lane switched off around the call is never written.
 __device__ __forceinline__ void keep_rsel_lane(double &rsel, int L, double rs)
 {
-    if (!WCE_KEEP_EXEC) {
-        keep_rsel(rsel, (int)threadIdx.x == L, rs);
-        return;
-    }
     uint64_t sv;
     asm volatile("s_mov_b64 %[sv], exec\n\t"
                  "s_mov_b64 exec, %[m]\n\t"
@@ -1180,10 +877,6 @@ __device__ __forceinline__ void keep_rsel_lane(double &rsel, int L, double rs)
 // a = c on the lanes of mask m (a constant) that are active: two v_mov_b64 under EXEC
 __device__ __forceinline__ void keep_where_mask(uint64_t m, bool sel, double2 &a, double2 c)
 {
-    if (!WCE_KEEP_EXEC) {
-        keep_where(sel, a, c);
-        return;
-    }
     uint64_t sv;
     asm volatile("s_mov_b64 %[sv], exec\n\t"
                  "s_mov_b64 exec, %[m]\n\t"
@@ -1209,11 +902,7 @@ template <int KB>
 __device__ __forceinline__ void to_blocks(double2 (&A)[RB][RB], const double2 (&P)[8], SolveLds &s, int p, int q,
                                           int lane)
 {
-    if (!WCE_STASH_COLS && lane < 56) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) s.conv[conv_idx(lane, c)] = P[c];
-    }
-    if (WCE_STASH_COLS) stash_col(s, lane, 7, P[7]);
+    stash_col(s, lane, 7, P[7]);
     wave_lds_sync();
 #pragma unroll
     for (int aa = KB; aa < RB; ++aa) A[aa][KB] = s.conv[conv_idx(p + 8 * aa, q)];
@@ -1224,7 +913,6 @@ template <int KB, int K0 = 0, bool KEEP = false>
 __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s, int p,
                                            int q, int lane, double &rsel)
 {
-    constexpr bool PRE = WCE_DPP_PANEL != 0;
 #pragma unroll
     for (int kq = K0; kq < 8; ++kq) {
         const int k = 8 * KB + kq;
@@ -1235,23 +923,18 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
         for (int aa = KB + 1; aa < RB; ++aa) Ur[aa] = col[p + 8 * aa];
         if (kq < 7) {
             // row lane of column 8KB+c is live for 8KB+c <= lane <= 54
-            if (WCE_DPP_PANEL) cmsub_panel<KB>(kq + 1, P[kq + 1], P[kq], R);   // lookahead
-            else cmsub_live(lanes_from(k + 1, NSC + 1), P[kq + 1], P[kq], col[8 * KB + kq + 1]);
+            cmsub_panel<KB>(kq + 1, P[kq + 1], P[kq], R);   // lookahead
             const double rs = rsq_uniform(readlane_f64(P[kq + 1].x, k + 1));
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
             if (KEEP) keep_rsel_lane(rsel, k + 1, rs);
-            double2 Rn = R;
-            if (PRE) {
-                wave_lds_sync();
-                Rn = next[8 * KB + (lane & 7)];
-            }
+            wave_lds_sync();
+            const double2 Rn = next[8 * KB + (lane & 7)];
 #pragma unroll
             for (int c = kq + 2; c < 8; ++c) {
-                if (WCE_DPP_PANEL) cmsub_panel<KB>(c, P[c], P[kq], R);
-                else cmsub_live(lanes_from(8 * KB + c, NSC + 1), P[c], P[kq], col[8 * KB + c]);
+                cmsub_panel<KB>(c, P[c], P[kq], R);
             }
-            if (KEEP && WCE_STASH_COLS) stash_col(s, lane, kq, P[kq]);   // final: its last use was above
+            if (KEEP) stash_col(s, lane, kq, P[kq]);   // final: its last use was above
             upd_cols_chol<KB + 1>(A, Ur, col, p, q);
             R = Rn;
         } else {
@@ -1263,10 +946,8 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
                 if (KEEP) keep_rsel_lane(rsel, k + 1, rs);
-                if (PRE) {
-                    wave_lds_sync();
-                    R = next[8 * (KB + 1) + (lane & 7)];
-                }
+                wave_lds_sync();
+                R = next[8 * (KB + 1) + (lane & 7)];
             } else {   // block column 6 stays block-cyclic: the 8 owners of column 48 publish
                 const double rs = rsq_uniform(readlane_f64(A[KB + 1][KB + 1].x, 0));
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
@@ -1336,7 +1017,7 @@ __device__ __forceinline__ void chol_panels_keep(double2 (&A)[RB][RB], double2 (
     }
 }
 
-// The dense-C factorisation (WCE_DENSE_CHOL): the headline's row-per-lane
+// The dense-C factorisation: the headline's row-per-lane
 // Cholesky panels on Ryy bordered by conj(rx) (row 53), keeping L in the
 // block-cyclic registers for the back-substitution; s.rd = 1/sqrt(d_k).
 // Entering: A built (block rows/columns K0..6, row 53 = the conj right-hand
@@ -1359,7 +1040,7 @@ __device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], SolveLds &s, in
         wave_lds_sync();   // conv reads done before the publish (s.u is separate; order only)
         s.u[0][lane] = P[0];
         wave_lds_sync();
-        double2 R = WCE_DPP_PANEL ? s.u[0][8 * K0 + (lane & 7)] : make_double2(0.0, 0.0);
+        double2 R = s.u[0][8 * K0 + (lane & 7)];
         chol_panels_keep<K0>(A, P, R, s, p, q, lane, rsel);
     } else {   // the system is block (6, 6) alone: pivot 48 opens the block-cyclic last panel
         const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 0));
@@ -1499,7 +1180,7 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     P[1] = cscale(P[1], rsq_nr(readlane_f64(P[1].x, 1)));
     s.u[1][lane] = P[1];
     wave_lds_sync();
-    double2 R = WCE_DPP_PANEL ? s.u[1][lane & 7] : make_double2(0.0, 0.0);
+    double2 R = s.u[1][lane & 7];
     double rsel = 0.0;   // unused (no back-substitution)
     chol_panel<0, 1>(A, P, R, s, p, q, lane, rsel);
     chol_panel<1>(A, P, R, s, p, q, lane, rsel);
@@ -1519,27 +1200,16 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     const double ac = st->acoef, bc = st->bcoef;
     double2 A[RB][RB];
     const bool cbuild = !FC && ac != 0.0 && !WCE_ABLATE_RYY;
-#if WCE_PREFETCH_C
-    // C's 28 blocks are issued before the frame's own loads: the two memory
-    // round trips (C from L2, tx/rx from HBM) overlap instead of queueing.
-    // Unconditional (no branch around A: a branch-defined A spills).
-    if constexpr (!FC) {
-#pragma unroll
-        for (int aa = 0; aa < RB; ++aa)
-#pragma unroll
-            for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
-    }
-#endif
     {
         const bool act = lane < NSC;
-        const double2 t = !act ? make_double2(0, 0) : WCE_SOLVE_NT_LOAD ? ld2_nt(a.tx, base + lane) : ld2(a.tx, base + lane);
-        const double2 r = !act ? make_double2(0, 0) : WCE_SOLVE_NT_LOAD ? ld2_nt(a.rx, base + lane) : ld2(a.rx, base + lane);
+        const double2 t = !act ? make_double2(0, 0) : ld2(a.tx, base + lane);
+        const double2 r = !act ? make_double2(0, 0) : ld2(a.rx, base + lane);
         const bool inx = act && ((st->xmask >> lane) & 1ull);
         s.x[lane] = inx ? t : make_double2(0, 0);
         s.rx[lane] = r;
         s.z[lane] = make_double2(0, 0);
         s.rd[lane] = 0.0;
-        if (WCE_DENSE_SCALED && !DOT && cbuild) {   // y = rx / x to u[0], M's diagonal to u[1] (read by the build)
+        if (!DOT && cbuild) {   // y = rx / x to u[0], M's diagonal to u[1] (read by the build)
             const double2 xl = inx ? t : make_double2(0, 0);
             const double tt = ac * (xl.x * xl.x + xl.y * xl.y);
             const bool keep = dense_keep(tt, bc);
@@ -1574,31 +1244,12 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
             for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = cmul(s.u[0][p + 8 * aa], s.u[1][q + 8 * bb]);
-            wave_lds_sync();   // publish_col<0> reuses s.u[0]
-        } else if (WCE_DENSE_SCALED && cbuild) {   // M = C + diag(b / (a |x|^2))  (C zero-padded)
-            if (!WCE_PREFETCH_C) {   // (else A holds C already)
-#pragma unroll
-                for (int aa = 0; aa < RB; ++aa)
-#pragma unroll
-                    for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
-            }
-        } else if (!WCE_DENSE_SCALED && (WCE_PREFETCH_C ? !FC : cbuild)) {   // a X C X'  (C zero-padded: no bounds checks)
-            double2 yr[RB], xc[RB];
-#pragma unroll
-            for (int aa = 0; aa < RB; ++aa) {
-                yr[aa] = cscale(s.x[p + 8 * aa], ac);
-                xc[aa] = cconj(s.x[q + 8 * aa]);
-            }
+            wave_lds_sync();   // the factorisation reuses s.u[0]
+        } else if (cbuild) {   // M = C + diag(b / (a |x|^2))  (C zero-padded: no bounds checks)
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
-                for (int bb = 0; bb <= aa; ++bb) {
-#if WCE_PREFETCH_C
-                    A[aa][bb] = cmul(cmul(yr[aa], A[aa][bb]), xc[bb]);
-#else
-                    A[aa][bb] = cmul(cmul(yr[aa], ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb)), xc[bb]);
-#endif
-                }
+                for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
         } else {
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
@@ -1606,7 +1257,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0, 0);
         }
         // scaled dense form: M's diagonal from u[1], bordered row conj(y) from u[0]
-        const bool scaled = WCE_DENSE_SCALED && cbuild;
+        const bool scaled = cbuild;
         const double2 *brow = scaled ? s.u[0] : s.rx;
 #pragma unroll
         for (int aa = 0; aa < RB - 1; ++aa) A[aa][aa].x += (p == q) ? (scaled ? s.u[1][p + 8 * aa].x : bc) : 0.0;
@@ -1618,21 +1269,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
             for (int bb = 0; bb < RB; ++bb) A[RB - 1][bb] = cconj(brow[q + 8 * bb]);
         }
     }
-    if (WCE_DENSE_CHOL) {
-        dense_chol(A, s, p, q, lane);
-    } else {
-        // pivot 0 and its column
-        double r = rcp_nr(readlane_f64(A[0][0].x, 0));
-        publish_col<0>(A, s.u[0], p, q, 0);
-        wave_lds_sync();
-        ldl_panel<0>(A, s, p, q, r);
-        ldl_panel<1>(A, s, p, q, r);
-        ldl_panel<2>(A, s, p, q, r);
-        ldl_panel<3>(A, s, p, q, r);
-        ldl_panel<4>(A, s, p, q, r);
-        ldl_panel<5>(A, s, p, q, r);
-        ldl_panel<6>(A, s, p, q, r);
-    }
+    dense_chol(A, s, p, q, lane);
     wave_lds_sync();
     // row 53 holds conj(u_53,j) = conj(y_j): w_j = r_j conj(u_53,j)
     double rq[RB];
@@ -1659,7 +1296,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #endif
     wave_lds_sync();
     const double2 xl = s.x[lane];
-    if (WCE_DENSE_SCALED && cbuild) {   // W = (x / (a conj x)) o (M^-1 y)
+    if (cbuild) {   // W = (x / (a conj x)) o (M^-1 y)
         const double tt = ac * (xl.x * xl.x + xl.y * xl.y);
         const double2 ph = dense_keep(tt, bc) ? cscale(cmul(xl, xl), 1.0 / tt) : make_double2(0.0, 0.0);
         return cmul(ph, s.z[lane]);
@@ -1702,9 +1339,11 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
 // 8 K0 + r - 1; rows up to 52 past r get Gram entries 0, i.e. pivot b and a
 // zero right-hand side, so t_j = 0 there), bordered by conj(G^H rx) in row 53
 // exactly where the dense solve keeps conj(rx); the panels before K0 and
-// their back-substitution blocks are skipped.  G^H G and the border row come
-// from v_mfma_f64_16x16x4 tiles of G~ = [X U | rx] (the border is the Gram
-// column j = 53 - 8 K0 of G~), staged through LDS into the register blocks.
+// their back-substitution blocks are skipped.  G^H G and the border row are
+// accumulated on the VALU from G~ = [X U | rx] staged through LDS (the border
+// is the Gram column j = 53 - 8 K0 of G~; lr_gram_valu).  (Round 3's MFMA
+// Gram tiles, 1.25-1.33x slower, were retired in round 4:
+// profiles/r03_ab_lowrank_dense.txt.)
 // =====================================================================
 #ifndef WCE_LR_WAVES_PER_SIMD   // K0 >= 2 (<= 122 VGPRs); 12 KB of LDS per wave caps a CU at 13 waves anyway
 #define WCE_LR_WAVES_PER_SIMD 4
@@ -1719,61 +1358,7 @@ __device__ __forceinline__ double2 lr_gcol(const State *__restrict__ st, const S
     const double2 r = j == RMAX ? s.rx[k] : make_double2(0.0, 0.0);
     return j < RMAX ? g : r;
 }
-
-constexpr int LR_TS = 17;   // row stride (complex) of a staged 16 x 16 Gram tile: conflict-free block reads
-
-// Gram tile (I, J) = rows 16 I .. 16 I + 15 x columns 16 J .. of G~^H G~,
-// then into the register blocks it covers: A = a Gamma + b I on rows < 53,
-// the border row 53 (conj(G^H rx)) and rows 54, 55 (0) as they are.
-template <int K0, int I, int J>
-__device__ __forceinline__ void lr_tile(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB], int lane,
-                                        int p, int q, double ac, double bc)
-{
-    const int ml = lane & 15, kl = lane >> 4;
-    v4d gr = {0, 0, 0, 0}, gi = {0, 0, 0, 0};
-#pragma unroll 2   // (fully unrolled, the 14 steps' operand loads are all hoisted: spills at K0 = 0)
-    for (int t = 0; t < KSTEPS; ++t) {
-        const int k = 4 * t + kl;
-        const double2 ga = lr_gcol<K0>(st, s, k, 16 * I + ml);
-        const double2 gb = (I == J) ? ga : lr_gcol<K0>(st, s, k, 16 * J + ml);
-        // conj(ga) gb = (ga.x gb.x + ga.y gb.y) + i (ga.x gb.y - ga.y gb.x)
-        gr = __builtin_amdgcn_mfma_f64_16x16x4f64(ga.x, gb.x, gr, 0, 0, 0);
-        gr = __builtin_amdgcn_mfma_f64_16x16x4f64(ga.y, gb.y, gr, 0, 0, 0);
-        gi = __builtin_amdgcn_mfma_f64_16x16x4f64(ga.x, gb.y, gi, 0, 0, 0);
-        gi = __builtin_amdgcn_mfma_f64_16x16x4f64(-ga.y, gb.x, gi, 0, 0, 0);
-    }
-    double2 *T = s.conv;   // D[m = kl + 4 r][n = ml]
-#pragma unroll
-    for (int r = 0; r < 4; ++r) T[(kl + 4 * r) * LR_TS + ml] = make_double2(gr[r], gi[r]);
-    wave_lds_sync();
-#pragma unroll
-    for (int da = 0; da < 2; ++da)
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-            const int aa = K0 + 2 * I + da, bb = K0 + 2 * J + db;   // constants after unrolling
-            if (aa < RB && bb <= aa) {
-                const int ai = aa < RB ? aa : RB - 1, bi = bb < RB ? bb : RB - 1;
-                const double2 v = T[(p + 8 * da) * LR_TS + q + 8 * db];
-                const bool gram = p + 8 * aa < NSC;
-                double2 e = cscale(v, ac);
-                e.x += (gram && aa == bb && p == q) ? bc : 0.0;
-                A[ai][bi] = make_double2(gram ? e.x : v.x, gram ? e.y : v.y);
-            }
-        }
-    wave_lds_sync();   // the next tile rewrites T
-}
-template <int K0, int I, int J>
-__device__ __forceinline__ void lr_gram(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB], int lane,
-                                        int p, int q, double ac, double bc)
-{
-    constexpr int NT = (8 * (RB - K0) + 15) / 16;   // tiles per side over block rows K0..6
-    if constexpr (I < NT) {
-        lr_tile<K0, I, J>(st, s, A, lane, p, q, ac, bc);
-        if constexpr (J < I) lr_gram<K0, I, J + 1>(st, s, A, lane, p, q, ac, bc);
-        else lr_gram<K0, I + 1, 0>(st, s, A, lane, p, q, ac, bc);
-    }
-}
-// The same Gram blocks on the VALU, straight into the block-cyclic layout:
+// The Gram blocks on the VALU, straight into the block-cyclic layout:
 // G~ is staged through LDS 8 subcarriers at a time (T[kk][j], j < 56 - 8 K0),
 // and lane (p, q) accumulates A[aa][bb] += conj(G~[k][p + 8 (aa - K0)])
 // G~[k][q + 8 (bb - K0)] for its blocks aa >= bb >= K0 only -- no upper
@@ -1832,9 +1417,6 @@ __device__ __forceinline__ void lr_gram_valu(const State *__restrict__ st, Solve
         }
     }
 }
-#ifndef WCE_LR_GRAM_MFMA   // A/B: 1 = the Gram blocks from v_mfma_f64_16x16x4 tiles (lr_gram)
-#define WCE_LR_GRAM_MFMA 0
-#endif
 
 template <int BLK, int K0>
 __device__ __forceinline__ void back_blocks_from(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
@@ -1870,8 +1452,7 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
     for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
         for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
-    if (WCE_LR_GRAM_MFMA) lr_gram<K0, 0, 0>(st, s, A, lane, p, q, ac, bc);
-    else lr_gram_valu<K0>(st, s, A, lane, p, q, ac, bc);
+    lr_gram_valu<K0>(st, s, A, lane, p, q, ac, bc);
     dense_chol<K0>(A, s, p, q, lane);
     double rq[RB];
 #pragma unroll
@@ -1971,12 +1552,6 @@ __global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *
 #ifndef WCE_LR_LDS_P   // direct form: P_k and U staged in LDS per workgroup instead of scalar loads, for the ranks whose bit is set
 #define WCE_LR_LDS_P 0x110   // ranks 4 and 8 (measured per rank, profiles/r03_ab_lowrank_ldsp.txt)
 #endif
-#ifndef WCE_LR_PF_LO   // direct form, pass 1: tx / rx loads this many subcarriers ahead, ranks 1..4 (0: UNROLL form)
-#define WCE_LR_PF_LO 0
-#endif
-#ifndef WCE_LR_PF_HI   // the same for ranks 5..8
-#define WCE_LR_PF_HI 0
-#endif
 constexpr int LRL_KC = 4;                         // subcarriers per chunk
 constexpr int LRL_NCH = (NSC + LRL_KC - 1) / LRL_KC;   // 14 chunks (k = 52..55: only 52 is live)
 constexpr int LRL_LS = 5;                         // LDS row stride (complex) per frame
@@ -2012,7 +1587,7 @@ __device__ __forceinline__ void lrl_stage(LrLaneLds &s, const LrChunk &q, int la
     asm volatile("" ::: "memory");
 }
 // pass-1 / correction-pass sweep over k: f(k, x_k, rx_k) in order k = 0..52
-template <bool STAGED, int UN, int PF = 0, typename Fn>
+template <bool STAGED, int UN, typename Fn>
 __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, const int64_t (&eb)[4], uint32_t live,
                                           int64_t base, bool own, int lane, Fn fn)
 {
@@ -2028,31 +1603,6 @@ __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, con
                 const int k = LRL_KC * c + kk;
                 if (kk > 0 && k >= NSC) break;   // (uniform) the last chunk holds k = 52 only
                 fn(k, sp->x[lane * LRL_LS + kk], sp->r[lane * LRL_LS + kk]);
-            }
-        }
-    } else if constexpr (PF > 0) {
-        // direct form, loads PF subcarriers ahead: at 65,536 frames a launch is
-        // one wave per SIMD (64 frames per wave), so nothing else hides a load's
-        // round trip; issued just in time, pass 1 waits one per subcarrier
-        double2 xb[PF], rb[PF];
-#pragma unroll
-        for (int j = 0; j < PF; ++j) {
-            xb[j] = own ? ld2(a.tx, base + j) : make_double2(0.0, 0.0);
-            rb[j] = own ? ld2(a.rx, base + j) : make_double2(0.0, 0.0);
-        }
-#pragma unroll 1
-        for (int k0 = 0; k0 < NSC; k0 += PF) {
-#pragma unroll
-            for (int j = 0; j < PF; ++j) {
-                const int k = k0 + j;
-                if (k < NSC) {   // (uniform)
-                    const double2 x = xb[j], r = rb[j];
-                    if (k + PF < NSC) {
-                        xb[j] = own ? ld2(a.tx, base + k + PF) : make_double2(0.0, 0.0);
-                        rb[j] = own ? ld2(a.rx, base + k + PF) : make_double2(0.0, 0.0);
-                    }
-                    fn(k, x, r);
-                }
             }
         }
     } else {
@@ -2114,8 +1664,7 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
     for (int e = 0; e < NO; ++e) go[e] = make_double2(0.0, 0.0);
     bool cplx = false;
     constexpr int UN = R <= 4 ? WCE_LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
-    constexpr int PF = R <= 4 ? WCE_LR_PF_LO : WCE_LR_PF_HI;
-    lrl_sweep<STAGED, UN, PF>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
+    lrl_sweep<STAGED, UN>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
         if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
         cplx |= x.y != 0.0;
         const double w = fma(x.x, x.x, x.y * x.y);
@@ -2368,31 +1917,18 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
     }
 }
 
-#ifndef WCE_LR_QUAD   // ranks 9..16 on mmse_lr_quad_kernel (0: mmse_lr_kernel)
-#define WCE_LR_QUAD 1
-#endif
-#ifndef WCE_LR_QUAD_LDS_U   // pass 1's U_k from an LDS copy per workgroup instead of scalar loads: slower here
-#define WCE_LR_QUAD_LDS_U 0   // (rank 16 237 -> 271 us at 65,536 frames, 3.82 -> 4.39 ms at 1M; profiles/r03_ab_lowrank_ldsp.txt):
-#endif                        // U (13.6 KB at rank 16) stays in the scalar cache, and 3 waves/SIMD hide its latency
+// (pass 1's U_k from an LDS copy per workgroup instead of scalar loads: slower,
+// rank 16 237 -> 271 us at 65,536 frames, 3.82 -> 4.39 ms at 1M; retired in
+// round 4, profiles/r03_ab_lowrank_ldsp.txt: U, 13.6 KB at rank 16, stays in
+// the scalar cache, and 3 waves/SIMD hide its latency)
 template <int R>
 __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restrict__ st, SolveArgs a)
 {
     const int i = threadIdx.x & 15;   // the row of the R x R system this lane holds
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // (frame, block) unit of the row
-#if WCE_LR_QUAD_LDS_U
-    __shared__ double2 sU[NSC * R];
-    {
-        const double2 *Ug = reinterpret_cast<const double2 *>(st->U);
-        for (int e = threadIdx.x; e < NSC * R; e += blockDim.x) sU[e] = Ug[(e / R) * CLD + e % R];
-        __syncthreads();
-    }
-    const double2 *__restrict__ U1 = sU;
-    constexpr int uld = R;
-#else
-    const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);
+    const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);   // wave-uniform: scalar loads
     constexpr int uld = CLD;
-#endif
     if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows (skip: the constant-modulus path wrote H)
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
@@ -2546,7 +2082,7 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
     // ---- LS family + equalization of frame f (main.c:66-146, WiFi_Equalization.m)
     const uint32_t mask = l.mask;
     if (!mask) return;
-    const double2 rp = !l.rx_pre ? make_double2(0, 0) : WCE_EQ_NT_LOAD ? ld2_nt(l.rx_pre, f * l.ps + k) : ld2(l.rx_pre, f * l.ps + k);
+    const double2 rp = !l.rx_pre ? make_double2(0, 0) : ld2_nt(l.rx_pre, f * l.ps + k);
     const LsLane c = ls_lane(st, l.tx_pre, k);
     // pilot LS from the frame data the solve staged in LDS (pilots are in X in both modes)
     // lane j < 4 divides pilot j once; the four values are broadcast by readlane
@@ -2612,66 +2148,19 @@ __device__ __forceinline__ bool tile_done(const uint8_t *__restrict__ skip, int6
     return __ballot(f < n && skip[f] == 0) == 0;
 }
 
-#ifndef WCE_APPLY_3M   // H = C W with three real MFMA products per complex product (apply_tile_acc3, matvec_kernel)
-#define WCE_APPLY_3M 1
-#endif
-
-#ifndef WCE_APPLY_TAIL4   // output rows 48..52 on v_mfma_f64_4x4x4_4b (0: a fourth 16x16x4 row block, rows 48..63)
-#define WCE_APPLY_TAIL4 1
-#endif
-#ifndef WCE_MATVEC_TAIL4   // the same for matvec_kernel: off, its C comes from L2 and the 4x4 form reads twice
-#define WCE_MATVEC_TAIL4 0   // as much of it per tile (45.1 vs 41.6 us at 65,536 frames; equal at 131,072)
-#endif
-constexpr int APPLY_NT = WCE_APPLY_TAIL4 ? 3 : 4;   // 16-row output blocks on 16x16x4
-constexpr int MATVEC_NT = WCE_MATVEC_TAIL4 ? 3 : 4;
-
-// Output rows 48..52 of one 16-frame tile.  The last 16-row block holds 5
-// live rows, so 16x16x4 on it spends 11/16 of its cycles (1/6 of the tile's)
-// on padding; v_mfma_f64_4x4x4_4b_f64 has the same flop rate (16 cycles per
-// 512 flop, profiles/r02_ubench_mfma4.txt) at 4-row granularity: rows 48..55
-// cost half as much.  Its lane map, lane l = 16 r + 4 b + c: A holds A_b[c][r],
-// B holds B_b[r][c], D holds D_b[r][c] (blocks b independent).  Block b =
-// frames 4b .. 4b+3, so B_b[k][n] = W_{4b+n}[4s+k] is exactly the W fragment
-// lane l already holds for 16x16x4 (frame l&15, subcarrier 4s + (l>>4));
-// A_b[m][k] = C[i0+m][4s+k]: lane l reads C[i0 + (l&3)][4s + (l>>4)] (the
-// same in every block); D: lane l gets H_{frame l&15}[i0 + (l>>4)].  Two row
-// groups (48..51, 52..55), four independent chains so that no MFMA waits on
-// the previous one's result (~45 cycles dependent latency, 16 issue).
-template <bool QIN, bool PIPE, typename CLoad>
-__device__ __forceinline__ void tail_rows(CLoad cload, const double (&ar)[KSTEPS], const double (&ai)[KSTEPS],
-                                          double *Y, int64_t ys, int64_t f0, int64_t n, int lane)
-{
-    const int kl = lane >> 4, m4 = lane & 3;
-    double r0 = 0.0, i0 = 0.0, r1 = 0.0, i1 = 0.0;
-    double2 n0 = cload(48 + m4, kl), n1 = cload(52 + m4, kl);
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-        const double2 c0 = n0, c1 = n1;
-        // PIPE (C from LDS, apply_kernel): one k-step of C in flight; the
-        // compiler would otherwise hoist all 28 reads (112 VGPRs) and spill.
-        // matvec_kernel (C from L2, one tile per wave) wants them all issued early.
-        if (PIPE) asm volatile("" ::: "memory");
-        if (s + 1 < KSTEPS) {
-            n0 = cload(48 + m4, 4 * (s + 1) + kl);
-            n1 = cload(52 + m4, 4 * (s + 1) + kl);
-        }
-        r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ar[s], r0, 0, 0, 0);
-        r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ar[s], r1, 0, 0, 0);
-        i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, ar[s], i0, 0, 0, 0);
-        i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, ar[s], i1, 0, 0, 0);
-        if constexpr (!QIN) {
-            r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, -ai[s], r0, 0, 0, 0);
-            r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, -ai[s], r1, 0, 0, 0);
-            i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ai[s], i0, 0, 0, 0);
-            i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ai[s], i1, 0, 0, 0);
-        }
-    }
-    const int64_t fr = f0 + (lane & 15);
-    if (fr < n) {
-        st2(Y, fr * ys + 48 + kl, make_double2(r0, i0));
-        if (kl == 0) st2(Y, fr * ys + 52, make_double2(r1, i1));   // rows 53..55: padding, never stored
-    }
-}
+// H = C W (and the per-frame-covariance factors) in the 3M (Gauss) form: three
+// real MFMA chains per complex product, P1 = sum Re w Re c, P2 = sum Im w Im c,
+// P3 = sum (Re w + Im w)(Re c + Im c); Re = P1 - P2, Im = (P3 - P1) - P2
+// (round 3: 473 -> 406 us per 1,048,576 frames, profiles/r03_ab_apply_3m.txt).
+// apply_kernel computes output rows 48..52 on v_mfma_f64_4x4x4_4b (the last
+// 16-row block holds 5 live rows); matvec_kernel keeps a fourth 16x16x4 block
+// (its C comes from L2, and the 4x4 form reads twice as much of it per tile:
+// 45.1 vs 41.6 us at 65,536 frames).  (Round 4 retired the 4-product form,
+// the per-block C reads, the deferred stores and the 16x16x4 tail of
+// apply_kernel: their A/B results are in profiles/r02_ab_apply.txt,
+// r03_ab_apply_tail.txt, r03_ab_apply_3m.txt.)
+constexpr int APPLY_NT = 3;    // apply_kernel: 16-row output blocks on 16x16x4 (rows 48..52 on 4x4x4)
+constexpr int MATVEC_NT = 4;   // matvec_kernel: all 64 rows on 16x16x4
 
 // Y1[f] = M1 X[f] (and Y2[f] = M2 X[f]) for 16-frame tiles; M padded 64 x 64.
 // QIN: the input is replaced by (re X - im X, 0) (main.c:188's real "conj").
@@ -2712,7 +2201,7 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
         for (int nt = 0; nt < MATVEC_NT; ++nt) {
             const int i = 16 * nt + ml;
             v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
-            if (!QIN && WCE_APPLY_3M) {   // apply_tile_acc3's chains and order: bit-identical to apply_kernel
+            if constexpr (!QIN) {   // apply_kernel's chains and order: bit-identical to it
                 v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
 #pragma unroll
                 for (int s = 0; s < KSTEPS; ++s) {
@@ -2742,8 +2231,6 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
                 }
             }
         }
-        if (WCE_MATVEC_TAIL4)
-            tail_rows<QIN, false>([&](int i, int j) { return ld2(M, i * CLD + j); }, ar, ai, Y, ys, f0, n, lane);
     }
 }
 
@@ -3097,7 +2584,7 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthArgs a, const double *_
 // The reference passes NaN through silently -- its literal PS_MMSE returns
 // NaN x 53 (main.c:148-212) and its divisions by a zero pilot give
 // Inf.  One HBM pass over an output array on the flat element index
-// e = 53 f + k (like ls_flat_kernel: every lane of a load carries one entry);
+// e = 53 f + k (every lane of a load carries one entry);
 // only the rare non-finite lanes touch the bitmap, and the lane whose
 // atomicOr sets a frame's bit is the one that counts that frame.
 // =====================================================================
@@ -3145,10 +2632,7 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
                              // 65,536 frames rank 4 52.1 -> 37.2 us, 5 63.1 -> 40.8, 6 65.8 -> 46.8, 7 75.4 -> 53.0, 8 68.1 -> 64.4
                              // (before the LDS sharing: rank 4 direct 51.6 vs staged ~60 at 65,536, so 98,304 then)
 #endif
-#ifndef WCE_LR_WAVE_ONLY   // build-time default of WCE_VARIANT_LR (A/B builds: 1 = every rank on mmse_lr_kernel)
-#define WCE_LR_WAVE_ONLY 0
-#endif
-static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, WCE_LR_WAVE_ONLY, 0};
+static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, 0, 0};
 int set_variant(int which, int value)
 {
     if (which < 0 || which >= WCE_VARIANT_COUNT || value < 0 || value > 15) return WCE_EINVAL;
@@ -3194,25 +2678,18 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
     if (blocks > 256 * 8) blocks = 256 * 8;      // grid-stride the rest
     const bool eq = (a.mask & WCE_EQUALIZE) && a.eq;
     const dim3 g((unsigned)blocks), b(256);
-    if (WCE_LS_FLAT && !a.matlab && !eq &&
-        (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0) {
+    const bool light = !eq && (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0;
+    // configs[1] (LT_LS / PS_Linear, C semantics): one element per thread;
+    // variant 3 routes it through the per-frame LIGHT kernel (the gate's check)
+    if (light && !a.matlab && variant(WCE_VARIANT_LS) != 3) {
         for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
-            if (variant(WCE_VARIANT_LS) == 2) {
-                const int64_t blocks = (nf * NSC + 255) / 256;
-                hipLaunchKernelGGL(ls_elem_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a,
-                                   f0, (uint32_t)nf);
-                continue;
-            }
-            const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
-            int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
-            if (fb > 256 * 8 && variant(WCE_VARIANT_LS) == 0) fb = 256 * 8;   // grid-stride the rest
-            hipLaunchKernelGGL(ls_flat_kernel, dim3((unsigned)fb), dim3(256), 0, (hipStream_t)stream, st, a, f0,
+            const int64_t blocks = (nf * NSC + 255) / 256;
+            hipLaunchKernelGGL(ls_elem_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, f0,
                                (uint32_t)nf);
         }
         return hip_status(hipGetLastError());
     }
-    const bool light = !WCE_LS_NO_LIGHT && !eq && (a.mask & ~(uint32_t)(WCE_EST_LT_LS | WCE_EST_PS_LINEAR | WCE_EQUALIZE)) == 0;
     hipStream_t s = (hipStream_t)stream;
     if (a.matlab) {
         if (eq) hipLaunchKernelGGL((ls_kernel<true, true>), g, b, 0, s, st, a);
@@ -3235,14 +2712,9 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     if (a.nblk > 1 && !a.split) return WCE_EINVAL;   // block averaging runs split
     const dim3 g((unsigned)waves), b(64);
     hipStream_t s = (hipStream_t)stream;
-    if (WCE_REF_FLAT && a.hout && a.ref_pilots && !a.split) {
+    if (a.hout && a.ref_pilots && !a.split) {
         for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
-            if (variant(WCE_VARIANT_REF) == 1) {
-                const int64_t fb = tile_blocks((nf + TILE_F - 1) / TILE_F, WCE_REF_TILE_WAVES_PER_CU);
-                hipLaunchKernelGGL(mmse_ref_tile_kernel, dim3((unsigned)fb), dim3(256), 0, s, st, a, f0, (uint32_t)nf);
-                continue;
-            }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
             if (fb > 256 * 8 && variant(WCE_VARIANT_REF) == 0) fb = 256 * 8;
@@ -3275,7 +2747,7 @@ static LrForm lr_form(int rank, int64_t units)
         const bool many = lv == 4 || (lv == 0 && units > 64 * 4 * (int64_t)cu_count());
         return rank >= 7 && WCE_LR_STAGED_MINWG > 1 && many ? LrForm::StagedMW : LrForm::Staged;
     }
-    if (WCE_LR_QUAD && rank > LRL_RMAX && rank <= 16 && lv == 0) return LrForm::Quad;
+    if (rank > LRL_RMAX && rank <= 16 && lv == 0) return LrForm::Quad;
     return LrForm::Wave;
 }
 
@@ -3382,9 +2854,6 @@ int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t 
     return hip_status(hipGetLastError());
 }
 
-#ifndef WCE_REF_LS_FLAT   // A/B: 0 = REF + LS requests ride in mmse_solve_ls_kernel (one wave per frame)
-#define WCE_REF_LS_FLAT 1
-#endif
 int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
@@ -3392,7 +2861,7 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
     const dim3 g((unsigned)a.n), b(64);
     hipStream_t s = (hipStream_t)stream;
     const bool eq = (l.mask & WCE_EQUALIZE) && l.eq;
-    if (WCE_REF_LS_FLAT && a.ref_pilots && a.hout && !a.split && variant(WCE_VARIANT_REF_LS) == 0) {
+    if (a.ref_pilots && a.hout && !a.split && variant(WCE_VARIANT_REF_LS) == 0) {
         for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {   // 53 * frames < 2^32 per launch
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
             const dim3 gb((unsigned)((nf * NSC + 255) / 256));
@@ -3421,11 +2890,8 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 // walks a strided sequence of 16-frame tiles, loading tile t + 1's W while
 // its MFMAs run on tile t.  Same fragment maps and summation order as
 // matvec_kernel for rows 0..47; rows 48..52 on v_mfma_f64_4x4x4_4b
-// (tail_rows: 508 -> 465 us per 1,048,576 frames), whose results matched
+// (apply_tile3: 508 -> 465 us per 1,048,576 frames), whose results matched
 // the 16x16x4 form bit for bit on every A/B run (tools/ab_libs.py --leg apply).
-#ifndef WCE_APPLY_V2
-#define WCE_APPLY_V2 1
-#endif
 #ifndef WCE_APPLY_WG_PER_CU
 #define WCE_APPLY_WG_PER_CU 2
 #endif
@@ -3437,8 +2903,8 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 // of r02_pmc_legs.json apply1m); 58 maps every group onto 16 distinct slots
 // (tools/lds_banks.py enumerates the strides).
 constexpr int ACS = 58;
-// staged rows of C: 56 once rows 48..55 are the last ones read (tail_rows)
-constexpr int APPLY_ROWS = WCE_APPLY_TAIL4 ? 56 : 64;
+// staged rows of C: 56 (rows 48..55 are the last ones read)
+constexpr int APPLY_ROWS = 56;
 __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t n, int64_t g, int ml, int kl,
                                            double2 (&w)[KSTEPS], bool done = false)
 {
@@ -3450,133 +2916,27 @@ __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t 
     }
 }
 
-#ifndef WCE_APPLY_PF   // C fragment reads issued this many k-steps ahead, across the 16-row blocks (0: per block, 1 ahead)
-#define WCE_APPLY_PF 2
-#endif
-// Rows 0..47 of one tile as one flat sequence of 3 x 14 k-steps, C's LDS
-// fragment for step t + PF read at step t.  Left to itself the compiler
-// issues each k-step's ds_read_b128 right before its 4 MFMAs and waits on it
-// (lgkmcnt(0) every 4 MFMAs), so the MFMA pipe idles for an LDS round trip
-// per k-step unless the SIMD's other wave fills it.  A scheduling barrier
-// per step pins every read at its step (otherwise the scheduler moves each
-// read back next to its first use).  Same products, same summation order: bit-identical.
-template <int PF>
-__device__ __forceinline__ void apply_rows_pf(const double2 *sc, const double (&ar)[KSTEPS], const double (&ai)[KSTEPS],
-                                              double *Y, int64_t ys, int64_t f0, int64_t n, int ml, int kl)
+// One 16-frame tile: rows 0..47 as one flat sequence of 3 x 14 k-steps, C's
+// LDS fragments for step t + PF read at step t (PF = 2).  Left to itself the
+// compiler issues each k-step's ds_read_b128 right before its MFMAs and waits
+// on it (lgkmcnt(0) every few MFMAs), so the MFMA pipe idles for an LDS round
+// trip per k-step; a scheduling barrier per step pins every read at its step.
+// Each 16-row block's results are stored as soon as they are final.  Rows
+// 48..52 on v_mfma_f64_4x4x4_4b: lane l = 16 r + 4 b + c holds A_b[c][r],
+// B_b[r][c], D_b[r][c] (profiles/r02_ubench_mfma4.txt); block b = frames
+// 4b .. 4b+3, so B_b[k][n] = W_{4b+n}[4s+k] is the W fragment lane l already
+// holds for 16x16x4 (frame l&15, subcarrier 4s + (l>>4)); A_b[m][k] =
+// C[i0+m][4s+k]; D: lane l gets H_{frame l&15}[i0 + (l>>4)].  Two row groups
+// (48..51, 52..55), three independent chains each.  The Gauss form's imaginary
+// part carries ~eps (|Re w| + |Im w|)(|Re c| + |Im c|) per term, the same order
+// as the 4-product form's ~eps (|Re w Im c| + |Im w Re c|).
+constexpr int APPLY_PF = 2;
+__device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs, const double (&ar)[KSTEPS],
+                                            const double (&ai)[KSTEPS], int ml, int kl, double *Y, int64_t ys,
+                                            int64_t f0, int64_t n, const uint8_t *__restrict__ skip)
 {
     constexpr int NS = APPLY_NT * KSTEPS;
-    double2 cb[PF];
-#pragma unroll
-    for (int t = 0; t < PF; ++t) cb[t] = sc[(16 * (t / KSTEPS) + ml) * ACS + 4 * (t % KSTEPS) + kl];
-    v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        const int nt = t / KSTEPS, s = t % KSTEPS;
-        const double2 c = cb[t % PF];
-        if (t + PF < NS) cb[t % PF] = sc[(16 * ((t + PF) / KSTEPS) + ml) * ACS + 4 * ((t + PF) % KSTEPS) + kl];
-        __builtin_amdgcn_sched_barrier(0);
-        // the two chains alternate (no MFMA waits on its predecessor's result);
-        // -ai by the f64 MFMA's A-negate bit (blgp = 1: neg:[1,0,0]), not a VALU xor
-        accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, accr, 0, 0, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s == KSTEPS - 1) {
-            const int i = 16 * nt + ml;
-            if (i < NSC) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t fr = f0 + kl + 4 * r;
-                    if (fr < n) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
-                }
-            }
-            accr = v4d{0, 0, 0, 0};
-            acci = v4d{0, 0, 0, 0};
-        }
-    }
-}
-
-#ifndef WCE_APPLY_DEFER   // a tile's H stores issued at the start of the next tile (after its W has landed)
-#define WCE_APPLY_DEFER 0
-#endif
-// gfx950 has one vmcnt for loads and stores, which may complete out of
-// order, so the wait for the next tile's W (loaded a whole tile ahead) is a
-// vmcnt(0): it also waits for every H store of the tile just finished, issued
-// a few hundred cycles earlier.  Deferred, a tile's results stay in registers
-// (52 VGPRs) and are stored right after that wait, one tile before the next
-// wait that covers them.
-struct ApplyAcc {
-    v4d r[APPLY_NT], i[APPLY_NT];   // rows 16 nt + ml, frames kl + 4 r
-    double tr0, ti0, tr1, ti1;       // tail: row 48 + kl and row 52, frame ml
-};
-template <int PF>
-__device__ __forceinline__ void apply_tile_acc(const double2 *sc, const double (&ar)[KSTEPS], const double (&ai)[KSTEPS],
-                                               int ml, int kl, ApplyAcc &o)
-{
-    constexpr int NS = APPLY_NT * KSTEPS;
-    double2 cb[PF];
-#pragma unroll
-    for (int t = 0; t < PF; ++t) cb[t] = sc[(16 * (t / KSTEPS) + ml) * ACS + 4 * (t % KSTEPS) + kl];
-#pragma unroll
-    for (int nt = 0; nt < APPLY_NT; ++nt) o.r[nt] = o.i[nt] = v4d{0, 0, 0, 0};
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {
-        const int nt = t / KSTEPS, s = t % KSTEPS;
-        const double2 c = cb[t % PF];
-        if (t + PF < NS) cb[t % PF] = sc[(16 * ((t + PF) / KSTEPS) + ml) * ACS + 4 * ((t + PF) % KSTEPS) + kl];
-        __builtin_amdgcn_sched_barrier(0);
-        o.r[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, o.r[nt], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        o.i[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, o.i[nt], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        o.r[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, o.r[nt], 0, 0, 1);   // -ai c.y
-        __builtin_amdgcn_sched_barrier(0);
-        o.i[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, o.i[nt], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // rows 48..55 on v_mfma_f64_4x4x4_4b (tail_rows' maps and order)
-    const int m4 = ml & 3;
-    double r0 = 0.0, i0 = 0.0, r1 = 0.0, i1 = 0.0;
-    double2 n0 = sc[(48 + m4) * ACS + kl], n1 = sc[(52 + m4) * ACS + kl];
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-        const double2 c0 = n0, c1 = n1;
-        asm volatile("" ::: "memory");
-        if (s + 1 < KSTEPS) {
-            n0 = sc[(48 + m4) * ACS + 4 * (s + 1) + kl];
-            n1 = sc[(52 + m4) * ACS + 4 * (s + 1) + kl];
-        }
-        r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ar[s], r0, 0, 0, 0);
-        r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ar[s], r1, 0, 0, 0);
-        i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, ar[s], i0, 0, 0, 0);
-        i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, ar[s], i1, 0, 0, 0);
-        r0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.y, -ai[s], r0, 0, 0, 0);
-        r1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.y, -ai[s], r1, 0, 0, 0);
-        i0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ai[s], i0, 0, 0, 0);
-        i1 = __builtin_amdgcn_mfma_f64_4x4x4f64(c1.x, ai[s], i1, 0, 0, 0);
-    }
-    o.tr0 = r0; o.ti0 = i0; o.tr1 = r1; o.ti1 = i1;
-}
-// The same tile with three real products per complex one instead of four
-// (Gauss): P1 = Σ Re w Re c, P2 = Σ Im w Im c, P3 = Σ (Re w + Im w)(Re c + Im c),
-// Re h = P1 - P2, Im h = P3 - P1 - P2.  25% fewer MFMA cycles; Re c + Im c is
-// a third LDS plane (scs, staged once), Re w + Im w one VALU add per k-step.
-// Exact on integers (tests/test_parity_gpu.py); on real data Im h carries
-// ~eps (|Re w| + |Im w|)(|Re c| + |Im c|) per term instead of
-// ~eps (|Re w Im c| + |Im w Re c|): the same order.
-// NOW: each 16-row block's results are stored as soon as they are final
-// (the deferred form holds 52 more VGPRs, which with three chains spills).
-template <int PF, bool NOW>
-__device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double *scs, const double (&ar)[KSTEPS],
-                                                const double (&ai)[KSTEPS], int ml, int kl, ApplyAcc &o,
-                                                double *Y = nullptr, int64_t ys = 0, int64_t f0 = 0, int64_t n = 0,
-                                                const uint8_t *__restrict__ skip = nullptr)
-{
-    constexpr int NS = APPLY_NT * KSTEPS;
+    constexpr int PF = APPLY_PF;
     double2 cb[PF];
     double cbs[PF];
 #pragma unroll
@@ -3586,28 +2946,6 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
         cbs[t] = scs[e];
     }
     v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
-#ifdef WCE_APPLY_ABLATE_MFMA   // timing-only build: loads and stores alone (H = sums of the tile's W)
-    if (NOW) {
-        double sr = 0.0, si = 0.0;
-#pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) { sr += ar[s]; si += ai[s]; }
-#pragma unroll
-        for (int nt = 0; nt < APPLY_NT; ++nt) {
-            const int i = 16 * nt + ml;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t fr = f0 + kl + 4 * r;
-                if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(sr + r, si + nt));
-            }
-        }
-        const int64_t fr = f0 + ml;
-        if (fr < n && !(skip && skip[fr])) {
-            st2(Y, fr * ys + 48 + kl, make_double2(sr, si));
-            if (kl == 0) st2(Y, fr * ys + 52, make_double2(si, sr));
-        }
-        return;
-    }
-#endif
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
         const int nt = t / KSTEPS, s = t % KSTEPS;
@@ -3627,24 +2965,18 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
         p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(as, cs, p3, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (s == KSTEPS - 1) {
-            if (NOW) {
-                const v4d hr = p1 - p2, hi = (p3 - p1) - p2;
-                const int i = 16 * nt + ml;
-                if (i < NSC) {
+            const v4d hr = p1 - p2, hi = (p3 - p1) - p2;
+            const int i = 16 * nt + ml;
+            if (i < NSC) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int64_t fr = f0 + kl + 4 * r;
-                        if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(hr[r], hi[r]));
-                    }
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t fr = f0 + kl + 4 * r;
+                    if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(hr[r], hi[r]));
                 }
-            } else {
-                o.r[nt] = p1 - p2;
-                o.i[nt] = (p3 - p1) - p2;
             }
             p1 = p2 = p3 = v4d{0, 0, 0, 0};
         }
     }
-    // rows 48..55 on v_mfma_f64_4x4x4_4b (tail_rows' maps), three chains per row group
     const int m4 = ml & 3;
     double a0 = 0.0, b0 = 0.0, g0 = 0.0, a1 = 0.0, b1 = 0.0, g1 = 0.0;
     double2 n0 = sc[(48 + m4) * ACS + kl], n1 = sc[(52 + m4) * ACS + kl];
@@ -3668,35 +3000,10 @@ __device__ __forceinline__ void apply_tile_acc3(const double2 *sc, const double 
         g0 = __builtin_amdgcn_mfma_f64_4x4x4f64(cs0, as, g0, 0, 0, 0);
         g1 = __builtin_amdgcn_mfma_f64_4x4x4f64(cs1, as, g1, 0, 0, 0);
     }
-    o.tr0 = a0 - b0; o.ti0 = (g0 - a0) - b0;
-    o.tr1 = a1 - b1; o.ti1 = (g1 - a1) - b1;
-    if (NOW) {
-        const int64_t fr = f0 + ml;
-        if (fr < n && !(skip && skip[fr])) {
-            st2(Y, fr * ys + 48 + kl, make_double2(o.tr0, o.ti0));
-            if (kl == 0) st2(Y, fr * ys + 52, make_double2(o.tr1, o.ti1));
-        }
-    }
-}
-
-__device__ __forceinline__ void apply_tile_store(const ApplyAcc &o, double *Y, int64_t ys, int64_t f0, int64_t n,
-                                                 int ml, int kl, const uint8_t *__restrict__ skip)
-{
-#pragma unroll
-    for (int nt = 0; nt < APPLY_NT; ++nt) {
-        const int i = 16 * nt + ml;
-        if (i < NSC) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t fr = f0 + kl + 4 * r;
-                if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(o.r[nt][r], o.i[nt][r]));
-            }
-        }
-    }
     const int64_t fr = f0 + ml;
     if (fr < n && !(skip && skip[fr])) {
-        st2(Y, fr * ys + 48 + kl, make_double2(o.tr0, o.ti0));
-        if (kl == 0) st2(Y, fr * ys + 52, make_double2(o.tr1, o.ti1));   // rows 53..55: padding, never stored
+        st2(Y, fr * ys + 48 + kl, make_double2(a0 - b0, (g0 - a0) - b0));
+        if (kl == 0) st2(Y, fr * ys + 52, make_double2(a1 - b1, (g1 - a1) - b1));   // rows 53..55: padding, never stored
     }
 }
 
@@ -3705,12 +3012,12 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
                                                                         const uint8_t *__restrict__ skip)
 {
     __shared__ double2 sc[APPLY_ROWS * ACS];
-    __shared__ double scs[WCE_APPLY_3M ? APPLY_ROWS * ACS : 1];   // Re c + Im c (3M form)
+    __shared__ double scs[APPLY_ROWS * ACS];   // Re c + Im c (3M form)
     for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
         const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
         const double2 c = ld2(M, i * CLD + j);   // M zero-padded 64 x 64
         sc[i * ACS + j] = c;
-        if (WCE_APPLY_3M) scs[i * ACS + j] = c.x + c.y;
+        scs[i * ACS + j] = c.x + c.y;
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -3721,30 +3028,6 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
     if (g >= ng) return;
     double2 wn[KSTEPS];
     apply_load(X, xs, n, g, ml, kl, wn, tile_done(skip, 16 * g, n, lane));
-#if WCE_APPLY_DEFER
-    static_assert(WCE_APPLY_TAIL4, "the deferred form holds the 4x4x4 tail rows");
-    ApplyAcc acc;
-    int64_t fprev = -1;
-    for (; g < ng; g += stride) {
-        double ar[KSTEPS], ai[KSTEPS];
-#pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) {
-            ar[s] = wn[s].x;
-            ai[s] = wn[s].y;
-            asm volatile("" ::"v"(ar[s]), "v"(ai[s]));   // W_g complete HERE, before the stores below are issued
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (fprev >= 0) apply_tile_store(acc, Y, ys, fprev, n, ml, kl, skip);   // W_g has landed; W aliasing Y: tile fprev's W was read a tile ago
-        __builtin_amdgcn_sched_barrier(0);
-        if (g + stride < ng) apply_load(X, xs, n, g + stride, ml, kl, wn);
-        __builtin_amdgcn_sched_barrier(0);
-        if (WCE_APPLY_3M) apply_tile_acc3<WCE_APPLY_PF ? WCE_APPLY_PF : 5, false>(sc, scs, ar, ai, ml, kl, acc);
-        else apply_tile_acc<WCE_APPLY_PF ? WCE_APPLY_PF : 5>(sc, ar, ai, ml, kl, acc);
-        fprev = 16 * g;
-    }
-    apply_tile_store(acc, Y, ys, fprev, n, ml, kl, skip);
-    return;
-#endif
     for (; g < ng; g += stride) {
         double ar[KSTEPS], ai[KSTEPS];
 #pragma unroll
@@ -3756,39 +3039,7 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
             apply_load(X, xs, n, g + stride, ml, kl, wn, tile_done(skip, 16 * (g + stride), n, lane));
         const int64_t f0 = 16 * g;
         if (tile_done(skip, f0, n, lane)) continue;
-#if WCE_APPLY_3M
-        {
-            ApplyAcc unused;
-            apply_tile_acc3<WCE_APPLY_PF ? WCE_APPLY_PF : 2, true>(sc, scs, ar, ai, ml, kl, unused, Y, ys, f0, n, skip);
-        }
-        continue;
-#endif
-#if WCE_APPLY_PF
-        apply_rows_pf<WCE_APPLY_PF>(sc, ar, ai, Y, ys, f0, n, ml, kl);
-#else
-#pragma unroll 1
-        for (int nt = 0; nt < APPLY_NT; ++nt) {
-            const int i = 16 * nt + ml;
-            v4d accr = {0, 0, 0, 0}, acci = {0, 0, 0, 0};
-#pragma unroll
-            for (int s = 0; s < KSTEPS; ++s) {
-                const double2 c = sc[i * ACS + 4 * s + kl];
-                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, accr, 0, 0, 0);
-                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai[s], c.y, accr, 0, 0, 0);
-                acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.y, acci, 0, 0, 0);
-                acci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.x, acci, 0, 0, 0);
-            }
-            if (i < NSC) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t fr = f0 + kl + 4 * r;
-                    if (fr < n) st2(Y, fr * ys + i, make_double2(accr[r], acci[r]));
-                }
-            }
-        }
-#endif
-        if (WCE_APPLY_TAIL4)
-            tail_rows<false, true>([&](int i, int j) { return sc[i * ACS + j]; }, ar, ai, Y, ys, f0, n, lane);
+        apply_tile3(sc, scs, ar, ai, ml, kl, Y, ys, f0, n, skip);
     }
 }
 
@@ -3799,7 +3050,7 @@ int launch_mmse_apply(const State *st, const double *W, double *H, int64_t strid
     // 256 CUs); below that one wave round of matvec_kernel is as fast or faster
     // (profiles/r02_ab_apply.txt)
     const int64_t tiles = (n + 15) / 16;
-    if (!WCE_APPLY_V2 || tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * WCE_APPLY_WG_PER_CU) {
+    if (tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * WCE_APPLY_WG_PER_CU) {
         const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
         hipLaunchKernelGGL((matvec_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                            st->C, nullptr, W, stride, H, nullptr, stride, n, skip);

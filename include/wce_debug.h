@@ -29,13 +29,13 @@ int wce_debug_set_border_dot(struct wce_ctx *ctx, int on);
  * a smaller multiple of 32 makes tests reach the multi-launch path at small
  * sizes.  0 restores the default.  Process-wide. */
 int wce_debug_set_flat_chunk(long long frames);
-/* Kernel variant knobs for interleaved A/B timing in one process (same
- * buffers, same placement).  which 0: REF PS_MMSE (0 = 512-element chunks,
- * default; 1 = 64-frame tiles; 2 = chunks, uncapped grid).  which 1: LT_LS +
- * PS_Linear in C semantics (0 = 512-element chunks, grid capped at 2,048
- * blocks; 1 = the same uncapped; 2 = one element per thread, default).
- * which 2: REF PS_MMSE with LS outputs in one call (0 = one element per
- * thread, ref_ls_elem_kernel, default; 1 = the wave-per-frame fused solve).
+/* Kernel variant knobs for interleaved A/B timing and the gate's cross-checks
+ * in one process (same buffers, same placement).  which 0: REF PS_MMSE (0 =
+ * 512-element chunks on a capped grid, default; 2 = the same, uncapped grid).
+ * which 1: LT_LS + PS_Linear in C semantics (2 = one element per thread,
+ * ls_elem_kernel, default; 3 = the per-frame LIGHT kernel).  which 2: REF
+ * PS_MMSE with LS outputs in one call (0 = one element per thread,
+ * ref_ls_elem_kernel, default; 1 = the wave-per-frame fused solve).
  * which 3: WCE_MMSE_COV low-rank path (0 = ranks 1..8 one frame per lane in
  * the LDS-staged form, mmse_lr_lane_staged_kernel, ranks 7 and 8 in its
  * two-workgroups-per-CU build past 65,536 units on a 256-CU device, and
@@ -43,9 +43,13 @@ int wce_debug_set_flat_chunk(long long frames);
  * rank one frame per wave; 2 = the lane kernel's direct form,
  * mmse_lr_lane_kernel; 3 / 4 = the staged form with ranks 7 and 8 in the
  * one- / two-workgroups-per-CU build at any size; 2..4: ranks past 8 one
- * frame per wave).
- * Process-wide; variants 0..2 give bit-identical results, variant 3's two
- * kernels sum in different orders and agree to rounding (tests check both). */
+ * frame per wave).  which 4: REF + WCE_MMSE_FRAME_COV in C semantics (0 =
+ * ref_fc_kernel, one launch, default; 1 = the LT_LS pass, two matvec
+ * launches and the REF read-out).
+ * Process-wide; the variants of which 0, 1, 2, 4 give bit-identical results,
+ * which 3's kernels sum in different orders and agree to rounding (tests
+ * check both).  (Round 4 retired ls_flat_kernel -- which 1 = 0, 1 -- and the
+ * REF frame tiles -- which 0 = 1.) */
 int wce_debug_set_variant(int which, int value);
 /* WCE_MMSE_COV solve form for A/B and accuracy probes: 0 = as the state
  * chose (default), 1 = always the dense Ryy solve, 2 = always the low-rank

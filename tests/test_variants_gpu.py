@@ -1,7 +1,10 @@
-"""The HBM kernels' A/B variants (wce_debug_set_variant) are interchangeable:
+"""The HBM kernels' variants (wce_debug_set_variant) are interchangeable:
 bit-identical outputs on ragged batch sizes, across launch splits
-(wce_debug_set_flat_chunk), for fp64 and fp32 outputs.  The product default
-is the last variant of each list (LS: one element per thread; REF: chunks)."""
+(wce_debug_set_flat_chunk), for fp64 and fp32 outputs.  LS configs[1]: one
+element per thread (ls_elem_kernel, default, 2) against the per-frame LIGHT
+kernel (3); REF: 512-element chunks on a capped grid (default, 0) against an
+uncapped grid (2).  (Round 4 retired ls_flat_kernel and the 64-frame REF
+tiles from the library.)"""
 import ctypes
 
 import numpy as np
@@ -31,7 +34,7 @@ def test_ls_variants_identical(gpu_wce, golden, lib, chunk):
     assert lib.wce_debug_set_flat_chunk(ctypes.c_longlong(chunk)) == 0
     for f32, dt in ((0, np.complex128), (gpu_wce.OUT_LS_F32, np.complex64)):
         got = []
-        for v in (0, 1, 2):
+        for v in (2, 3):
             assert lib.wce_debug_set_variant(1, v) == 0
             lt, lin = gpu_wce.DeviceArray((B, N), dt, zero=True), gpu_wce.DeviceArray((B, N), dt, zero=True)
             ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre),
@@ -39,8 +42,7 @@ def test_ls_variants_identical(gpu_wce, golden, lib, chunk):
                          gpu_wce.LT_LS | gpu_wce.PS_LINEAR)
             gpu_wce.synchronize()
             got.append((lt.numpy(), lin.numpy()))
-        for v in (1, 2):
-            assert np.array_equal(got[v][0], got[0][0]) and np.array_equal(got[v][1], got[0][1]), (f32, v)
+        assert np.array_equal(got[1][0], got[0][0]) and np.array_equal(got[1][1], got[0][1]), f32
 
 
 @pytest.mark.parametrize("frame_cov", [False, True])
@@ -53,7 +55,7 @@ def test_ref_variants_identical(gpu_wce, golden, lib, frame_cov):
     ctx.reserve(B)
     mask = gpu_wce.PS_MMSE | (gpu_wce.FRAME_COV if frame_cov else 0)
     got = []
-    for v in (0, 1, 2):
+    for v in (0, 2):
         assert lib.wce_debug_set_variant(0, v) == 0
         H = gpu_wce.DeviceArray((B, N), zero=True)
         ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre if frame_cov else None),
@@ -61,5 +63,4 @@ def test_ref_variants_identical(gpu_wce, golden, lib, frame_cov):
         gpu_wce.synchronize()
         got.append(H.numpy())
     assert np.isfinite(got[0]).all()
-    for v in (1, 2):
-        assert np.array_equal(got[v], got[0]), v
+    assert np.array_equal(got[1], got[0])
