@@ -25,6 +25,7 @@ struct wce_ctx {
     bool bdot = true;           // rank-1 C: second bordered row, no back-solve / GEMM (A/B switch)
     int32_t cov_k0 = -1;        // State::cov_k0 (WCE_MMSE_COV: >= 0 low-rank Gram path, -1 dense)
     int32_t cov_rank = 0;       // State::cov_rank
+    bool cov_taps = false;      // State::cov_taps (diagonal Rhh: the tap-domain Gram)
     int cov_path = 0;           // wce_debug_set_cov_path: 0 auto, 1 dense, 2 low-rank
     bool cm_on = false;         // State::cm_on: a constant-modulus operator is loaded (wce_ctx_set_modulus)
     bool cm_use = true;         // wce_debug_set_cm: A/B switch of that path
@@ -199,6 +200,7 @@ int wce_ctx_mark_ready(wce_ctx *c)
     c->mode = h->mode;
     c->cov_rank = h->cov_rank;
     c->cov_k0 = h->cov_k0;
+    c->cov_taps = h->cov_taps != 0;
     c->cm_on = h->cm_on != 0;
     c->ready = true;
     return WCE_OK;
@@ -215,6 +217,7 @@ int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
     c->mode = st->mode;
     c->cov_k0 = st->cov_k0;
     c->cov_rank = st->cov_rank;
+    c->cov_taps = st->cov_taps != 0;
     c->cm_on = st->cm_on != 0;
     c->ready = true;
     return WCE_OK;
@@ -306,7 +309,7 @@ extern "C" const char *wce_debug_lr_kernel(wce_ctx *c, long long units)
     const int k0 = cov_lr_k0(c);
     if (k0 < 0) return "";
     DeviceGuard g(c->device);   // cu_count() reads the current device
-    return wce::lr_kernel_name(k0, c->cov_rank, units);
+    return wce::lr_kernel_name(k0, c->cov_rank, c->cov_taps, units);
 }
 
 static int check_frames(const wce_frames *in, bool need_blocks)
@@ -663,7 +666,7 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
         sa.skip = flags;
     }
     if (lr_k0 >= 0) {   // H = U s straight from the solve (split: H_b rows, then the block mean)
-        rc = wce::launch_mmse_lr(c->d_state, lr_k0, c->cov_rank, sa, stream);
+        rc = wce::launch_mmse_lr(c->d_state, lr_k0, c->cov_rank, c->cov_taps, sa, stream);
         if (rc) return fail(rc, "mmse_lr launch");
         if (split) rc = wce::launch_avg_blocks(ws, WS_LD, H, out->out_stride, n, stream);
         return rc ? fail(rc, "block average launch") : WCE_OK;

@@ -14,7 +14,7 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
-constexpr int32_t STATE_LAYOUT = 4;   // State layout version: bump with every change to struct State
+constexpr int32_t STATE_LAYOUT = 5;   // State layout version: bump with every change to struct State
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
@@ -71,6 +71,21 @@ struct State {
     double pcm[NPAD];
     int32_t cm_on;
     int32_t cm_reserved[3];
+    // WCE_MMSE_COV with a diagonal Rhh -- a power-delay profile (round 4): C's
+    // eigen-directions are DFT columns, U[:, j] = s_j F[:, t_j], and the Gram
+    // matrix U^H P U (P = diag |x|^2) is s_i s_j Q(t_i - t_j) with Q the DFT of
+    // |x|^2: the tap-domain form of the Gram path (mmse_lr_kernel<K0, true>)
+    // builds it from 53 per-lane sums instead of the 53 x 53 x 53 product.
+    // It runs the exact DFT (dft[], from an 80-bit angle), not main.c's cexp of
+    // a double angle (phase error <= 6e-14): the two models' answers differ by
+    // <= 1.3e-13 norm-relative on the widest PDP (profiles/r04_accuracy_probe.txt).
+    int32_t cov_taps;          // 1: Rhh is diagonal and the tables below are set
+    int32_t taps_reserved[3];
+    int32_t tap_of[NPAD];      // Gram column j -> delay tap t_j (j < cov_rank; 0 past it)
+    int32_t col_of[NPAD];      // delay tap t -> Gram column (-1: dropped, or t >= 53)
+    double col_s[NPAD];        // sqrt(lambda_j) by Gram column (0 past cov_rank)
+    double tap_s[NPAD];        // sqrt(lambda_t) by tap (0 where col_of is -1)
+    double dft[NPAD * 2];      // E[m] = exp(-2 pi i m / 53), m < 53 (0 past it)
 };
 static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
 
@@ -78,13 +93,23 @@ static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
 // build, a known mode, and (WCE_MMSE_COV) a rank and solve form in range.
 // Blobs arrive from other ranks or callers (wce_ctx_load_state,
 // wce_state_validate, wce_ctx_mark_ready after a broadcast).
+inline bool taps_ok(const State *st)
+{
+    if (st->cov_taps == 0) return true;
+    if (st->cov_taps != 1) return false;
+    for (int j = 0; j < NPAD; j++) {   // the kernels index LDS tables with these
+        if (st->tap_of[j] < 0 || st->tap_of[j] >= NSC) return false;
+        if (st->col_of[j] < -1 || st->col_of[j] >= st->cov_rank || (j >= NSC && st->col_of[j] != -1)) return false;
+    }
+    return true;
+}
 inline bool state_ok(const State *st)
 {
     if (st->magic != STATE_MAGIC || st->layout != STATE_LAYOUT || st->bytes != (int32_t)sizeof(State)) return false;
     if (st->mode != WCE_MMSE_REF && st->mode != WCE_MMSE_TEXTBOOK && st->mode != WCE_MMSE_COV) return false;
     if (st->mode == WCE_MMSE_COV)
         return st->cov_rank >= 0 && st->cov_rank <= NSC && st->cov_k0 >= -1 && st->cov_k0 <= COV_K0_MAX &&
-               (st->cov_k0 >= 0 || st->cov_rank == NSC);
+               (st->cov_k0 >= 0 || st->cov_rank == NSC) && taps_ok(st);
     return st->cov_k0 == -1;
 }
 
@@ -184,9 +209,9 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream);
 // WCE_MMSE_COV low-rank path: H (or, split, H_b per (frame, block) row) from
 // the Gram system embedded at block row k0 (State::cov_k0)
 // (rank = State::cov_rank: ranks 1..LRL_RMAX run one frame per lane instead)
-int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream);
+int launch_mmse_lr(const State *st, int k0, int rank, bool taps, const SolveArgs &a, void *stream);
 // the kernel launch_mmse_lr runs for `units` (frame, block) units (wce_debug_lr_kernel)
-const char *lr_kernel_name(int k0, int rank, int64_t units);
+const char *lr_kernel_name(int k0, int rank, bool taps, int64_t units);
 // REF + WCE_MMSE_FRAME_COV (C semantics) in one launch: LT_LS of rx_pre, u = Mu h,
 // w = Mw q(Mg h) at the pilot rows; hout: H = u s to a.w, else u / w rows to uw / ww
 int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
@@ -206,7 +231,9 @@ constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1
                                       // 1 = every rank on mmse_lr_kernel (one frame per wave), 2 = lane kernel
                                       // direct, 3 / 4 = lane kernel staged, ranks 7-8 in the one- / two-
                                       // workgroups-per-CU build at any size; the lane and wave kernels agree
-                                      // to rounding (~1e-15), not bitwise; the staged builds bitwise
+                                      // to rounding (~1e-15), not bitwise; the staged builds bitwise.
+                                      // A diagonal Rhh runs the wave kernel's tap-domain Gram
+                                      // (mmse_lr_kernel<K0, true>); 5 = the product Gram there instead
 constexpr int WCE_VARIANT_REF_FC = 4;  // REF + WCE_MMSE_FRAME_COV, C semantics: 0 = ref_fc_kernel (LT_LS, the
                                       // g / u / w products and the read-out in one launch, default), 1 = the
                                       // LT_LS pass + two matvec launches + the REF read-out; bit-identical

@@ -1497,20 +1497,181 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
     return y;
 }
 
+// ---------------------------------------------------------------------
+// The tap-domain Gram (State::cov_taps, a diagonal Rhh = power-delay profile).
+// U[k][j] = s_j E[k t_j mod 53] (E[m] = exp(-2 pi i m / 53), t_j the tap of
+// column j, s_j = sqrt(lambda_j)), so with p = |x|^2 and v = x o conj(rx)
+//     (U^H P U)_ij = s_i s_j Q((t_i - t_j) mod 53),  Q(d) = sum_k p_k conj(E[k d])
+//     (rx^H X U)_j = s_j D(t_j),                    D(m) = sum_k v_k E[k m]
+// -- two 53-point DFTs on lane d / m (6 FMAs per subcarrier), where the
+// product Gram runs ~100 per subcarrier per lane at K0 = 0.  The read-out
+// y = U t is a third DFT of the tap vector c_t = s_t t_col(t), and the
+// complex-symbol correction U U^H v / b the conjugate DFT of v scaled by
+// lambda_t, then a fourth.  E[k d mod 53] is gathered from LDS by the exact
+// index recurrence (no phase accumulation).
+// ---------------------------------------------------------------------
+// lane m: sum_k c_k E[k m] (CONJ: conj(E[k m])) over LDS vectors e (E) and c
+template <bool CONJ>
+__device__ __forceinline__ double2 lr_dft53(const double2 *e, const double2 *c, int m)
+{
+    double2 y = make_double2(0.0, 0.0);
+    int idx = 0;
+#pragma unroll 8
+    for (int k = 0; k < NSC; ++k) {
+        const double2 w = e[idx], v = c[k];
+        const double wy = CONJ ? -w.y : w.y;
+        y.x = fma(v.x, w.x, fma(-v.y, wy, y.x));
+        y.y = fma(v.x, wy, fma(v.y, w.x, y.y));
+        idx += m;
+        idx = idx >= NSC ? idx - NSC : idx;
+    }
+    return y;
+}
+
+template <int K0>
+__device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB],
+                                             int lane, int p, int q, double ac, double bc)
+{
+    constexpr int RMAX = NSC - 8 * K0;   // Gram column of the border (row 53)
+    constexpr int NB = RB - K0;
+    const bool act = lane < NSC;
+    {   // tables: E, p = |x|^2, v = x o conj(rx)
+        const double2 xl = s.x[lane], rl = s.rx[lane];
+        s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
+        s.u[1][lane] = cmul(xl, cconj(rl));
+        s.rd[lane] = fma(xl.x, xl.x, xl.y * xl.y);
+    }
+    wave_lds_sync();
+    double2 Qd = make_double2(0.0, 0.0), Dd = make_double2(0.0, 0.0);
+    {
+        const int d = act ? lane : 0;
+        int idx = 0;
+#pragma unroll 8
+        for (int k = 0; k < NSC; ++k) {
+            const double2 w = s.u[0][idx], v = s.u[1][k];
+            const double pk = s.rd[k];
+            Qd.x = fma(pk, w.x, Qd.x);
+            Qd.y = fma(-pk, w.y, Qd.y);
+            Dd.x = fma(v.x, w.x, fma(-v.y, w.y, Dd.x));
+            Dd.y = fma(v.x, w.y, fma(v.y, w.x, Dd.y));
+            idx += d;
+            idx = idx >= NSC ? idx - NSC : idx;
+        }
+    }
+    wave_lds_sync();   // every lane's reads of u[1] / rd are done
+    s.blk[lane] = Qd;
+    s.z[lane] = Dd;
+    s.u[1][lane] = make_double2(st->col_s[lane], (double)st->tap_of[lane]);   // column j: {s_j, t_j}
+    wave_lds_sync();
+#pragma unroll
+    for (int m = 0; m < NB; ++m) {
+        const int j1 = p + 8 * m;
+        const double2 c1 = s.u[1][j1];
+        const int t1 = (int)c1.y;
+#pragma unroll
+        for (int n = 0; n <= m; ++n) {
+            const int j2 = q + 8 * n;
+            const double2 c2 = s.u[1][j2];
+            const int t2 = (int)c2.y;
+            int dd = t1 - t2;
+            dd += dd < 0 ? NSC : 0;
+            double2 e;
+            if (j1 < RMAX && j2 < RMAX) {
+                e = cscale(s.blk[dd], ac * c1.x * c2.x);
+                e.x += j1 == j2 ? bc : 0.0;
+            } else if (j1 == RMAX && j2 < RMAX) {
+                e = cscale(s.z[t2], c2.x);
+            } else if (j2 == RMAX && j1 < RMAX) {
+                e = cscale(cconj(s.z[t1]), ac * c1.x);
+            } else {
+                e = make_double2(0.0, 0.0);
+            }
+            A[K0 + m][K0 + n] = e;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one block row's gathers in flight at a time
+    }
+    wave_lds_sync();   // dense_chol reuses u / conv
+}
+
+// lr_solve with the tap-domain Gram and read-out (State::cov_taps)
+template <int K0>
+__device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
+                                                 int64_t base)
+{
+    const int lane = threadIdx.x;
+    const int p = lane >> 3, q = lane & 7;
+    const bool act = lane < NSC;
+    const double ac = st->acoef, bc = st->bcoef;
+    {
+        const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
+        const double2 r = act ? ld2(a.rx, base + lane) : make_double2(0, 0);
+        const bool inx = act && ((st->xmask >> lane) & 1ull);
+        s.x[lane] = inx ? t : make_double2(0, 0);
+        s.rx[lane] = r;
+    }
+    wave_lds_sync();
+    double2 A[RB][RB];
+#pragma unroll
+    for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+        for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
+    lr_gram_taps<K0>(st, s, A, lane, p, q, ac, bc);
+    dense_chol<K0>(A, s, p, q, lane);
+    double rq[RB];
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) rq[bb] = s.rd[q + 8 * bb];
+    double2 P[RB];
+    const bool brow = (p == NSC - 8 * (RB - 1));
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) P[bb] = brow ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
+    back_blocks_from<RB - 1, K0>(A, P, rq, s, p, q, lane);
+    wave_lds_sync();
+    // c_t = s_t t_col(t) on lane t (t_j = z[8 K0 + j]); E back into u[0]
+    const int col = act ? st->col_of[lane] : -1;
+    const double ts = st->tap_s[lane];
+    {
+        const double2 tj = s.z[8 * K0 + (col < 0 ? 0 : col)];
+        s.u[1][lane] = col < 0 ? make_double2(0.0, 0.0) : cscale(tj, ts);
+        s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
+    }
+    wave_lds_sync();
+    const int kk = act ? lane : 0;
+    const double2 xl = s.x[lane];   // re-read: nothing of the frame stays live across the factorisation
+    double2 y = lr_dft53<false>(s.u[0], s.u[1], kk);   // y_k = sum_t c_t E[k t]
+    if (__ballot(act && xl.y != 0.0) != 0) {   // complex symbols: y += U U^H [(x - conj x) o rho] / b
+        const double2 rho = csub(s.rx[lane], cscale(cmul(xl, y), ac));   // b Ryy^-1 rx
+        s.blk[lane] = act ? make_double2(-2.0 * xl.y * rho.y, 2.0 * xl.y * rho.x) : make_double2(0, 0);
+        wave_lds_sync();
+        const double2 w = lr_dft53<true>(s.u[0], s.blk, kk);   // w_t = sum_k conj(E[k t]) v_k
+        wave_lds_sync();   // u[1] (c) is dead once every lane's read-out is done
+        s.u[1][lane] = act ? cscale(w, ts * ts / bc) : make_double2(0.0, 0.0);
+        wave_lds_sync();
+        y = cadd(y, lr_dft53<false>(s.u[0], s.u[1], kk));
+    }
+    return y;
+}
+
 // split (MATLAB averaging): one wave per (frame, block) writes H_b to row g
 // of a.w; avg_blocks_kernel forms the mean.
 // K0 = 0 (r > 45: a Gram system as large as Ryy itself) holds all 28
-// register blocks through the MFMA build: 181 VGPRs, 2 waves/SIMD; K0 = 1: 156
-constexpr int lr_waves(int k0) { return k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD); }
-template <int K0>
-__global__ __launch_bounds__(64, lr_waves(K0)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
+// register blocks through the product build: 2 waves/SIMD; K0 = 1: 156.
+// TAPS: the tap-domain Gram (State::cov_taps), registers as the dense solve's.
+constexpr int lr_waves(int k0, bool taps)
+{
+    return taps ? WCE_DENSE_WAVES_PER_SIMD : (k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD));
+}
+template <int K0, bool TAPS = false>
+__global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
     const int64_t g = blockIdx.x;
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
     if (f >= a.n || (a.skip && a.skip[g])) return;   // skip: H already written (constant-modulus path)
-    const double2 h = lr_solve<K0>(st, a, s, f * a.fs + (int64_t)(a.blk + b) * a.bs);
+    const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
+    double2 h;
+    if constexpr (TAPS) h = lr_solve_taps<K0>(st, a, s, base);
+    else h = lr_solve<K0>(st, a, s, base);
     if (threadIdx.x < NSC) st2(a.w, g * a.ws + threadIdx.x, h);
 }
 
@@ -2751,7 +2912,10 @@ static LrForm lr_form(int rank, int64_t units)
     return LrForm::Wave;
 }
 
-const char *lr_kernel_name(int k0, int rank, int64_t units)
+// a diagonal Rhh's tap-domain Gram on the wave kernel (variant 5: the product Gram)
+static bool lr_taps(bool taps) { return taps && variant(WCE_VARIANT_LR) != 5; }
+
+const char *lr_kernel_name(int k0, int rank, bool taps, int64_t units)
 {
     static const char *lane[2][LRL_RMAX + 1] = {
         {"", "mmse_lr_lane_kernel<1>", "mmse_lr_lane_kernel<2>", "mmse_lr_lane_kernel<3>", "mmse_lr_lane_kernel<4>",
@@ -2762,8 +2926,11 @@ const char *lr_kernel_name(int k0, int rank, int64_t units)
     static const char *quad[] = {"mmse_lr_quad_kernel<9>", "mmse_lr_quad_kernel<10>", "mmse_lr_quad_kernel<11>",
                                  "mmse_lr_quad_kernel<12>", "mmse_lr_quad_kernel<13>", "mmse_lr_quad_kernel<14>",
                                  "mmse_lr_quad_kernel<15>", "mmse_lr_quad_kernel<16>"};
-    static const char *wave[] = {"mmse_lr_kernel<0>", "mmse_lr_kernel<1>", "mmse_lr_kernel<2>", "mmse_lr_kernel<3>",
-                                 "mmse_lr_kernel<4>", "mmse_lr_kernel<5>", "mmse_lr_kernel<6>"};
+    static const char *wave[2][7] = {
+        {"mmse_lr_kernel<0>", "mmse_lr_kernel<1>", "mmse_lr_kernel<2>", "mmse_lr_kernel<3>", "mmse_lr_kernel<4>",
+         "mmse_lr_kernel<5>", "mmse_lr_kernel<6>"},
+        {"mmse_lr_kernel<0, true>", "mmse_lr_kernel<1, true>", "mmse_lr_kernel<2, true>", "mmse_lr_kernel<3, true>",
+         "mmse_lr_kernel<4, true>", "mmse_lr_kernel<5, true>", "mmse_lr_kernel<6, true>"}};
     static const char *mw[] = {"mmse_lr_lane_staged_kernel<7, 2>", "mmse_lr_lane_staged_kernel<8, 2>"};
     static_assert(WCE_LR_STAGED_MINWG == 2 || WCE_LR_STAGED_MINWG <= 1, "lr_kernel_name spells MW = 2");
     const int r = rank < 1 ? 1 : (rank > LRL_RMAX ? LRL_RMAX : rank);
@@ -2773,11 +2940,11 @@ const char *lr_kernel_name(int k0, int rank, int64_t units)
     case LrForm::Staged: return lane[1][r];
     case LrForm::StagedMW: return mw[r >= 8 ? 1 : 0];
     case LrForm::Quad: return quad[(rank > 16 ? 16 : rank) - 9];
-    default: return k0 >= 0 && k0 <= 6 ? wave[k0] : "";
+    default: return k0 >= 0 && k0 <= 6 ? wave[lr_taps(taps) ? 1 : 0][k0] : "";
     }
 }
 
-int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *stream)
+int launch_mmse_lr(const State *st, int k0, int rank, bool taps, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
     const int64_t waves = a.split ? a.n * a.nblk : a.n;
@@ -2825,16 +2992,17 @@ int launch_mmse_lr(const State *st, int k0, int rank, const SolveArgs &a, void *
         return hip_status(hipGetLastError());
     }
     const dim3 g((unsigned)waves), b(64);
+    const bool tp = lr_taps(taps);
+#define WCE_LRW(K)                                                                               \
+    case K:                                                                                      \
+        if (tp) hipLaunchKernelGGL((mmse_lr_kernel<K, true>), g, b, 0, s, st, a);                \
+        else hipLaunchKernelGGL((mmse_lr_kernel<K, false>), g, b, 0, s, st, a);                  \
+        break;
     switch (k0) {
-    case 0: hipLaunchKernelGGL(mmse_lr_kernel<0>, g, b, 0, s, st, a); break;
-    case 1: hipLaunchKernelGGL(mmse_lr_kernel<1>, g, b, 0, s, st, a); break;
-    case 2: hipLaunchKernelGGL(mmse_lr_kernel<2>, g, b, 0, s, st, a); break;
-    case 3: hipLaunchKernelGGL(mmse_lr_kernel<3>, g, b, 0, s, st, a); break;
-    case 4: hipLaunchKernelGGL(mmse_lr_kernel<4>, g, b, 0, s, st, a); break;
-    case 5: hipLaunchKernelGGL(mmse_lr_kernel<5>, g, b, 0, s, st, a); break;
-    case 6: hipLaunchKernelGGL(mmse_lr_kernel<6>, g, b, 0, s, st, a); break;
+        WCE_LRW(0) WCE_LRW(1) WCE_LRW(2) WCE_LRW(3) WCE_LRW(4) WCE_LRW(5) WCE_LRW(6)
     default: return WCE_EINVAL;
     }
+#undef WCE_LRW
     return hip_status(hipGetLastError());
 }
 

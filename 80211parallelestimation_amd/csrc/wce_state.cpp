@@ -445,6 +445,37 @@ int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
                         st->Pk[e] = (double)__real__ v;
                         st->Pk[e + 1] = i == j ? 0.0 : (double)__imag__ v;
                     }
+        // a diagonal Rhh (every off-diagonal entry exactly zero): the tap-domain
+        // tables (State::cov_taps).  The Jacobi sweep took no rotation, so column
+        // j of U is the DFT column of tap ord[j]; the kernels evaluate it from
+        // the exact DFT E[m] = exp(-2 pi i m / 53), rounded once from 80 bits.
+        bool diag = true;
+        for (int i = 0; i < n && diag; i++)
+            for (int j = 0; j < n; j++)
+                if (i != j && (Rhh[i * n + j].re != 0.0 || Rhh[i * n + j].im != 0.0)) { diag = false; break; }
+        st->cov_taps = 0;
+        std::memset(st->tap_of, 0, sizeof(st->tap_of));
+        std::memset(st->col_s, 0, sizeof(st->col_s));
+        std::memset(st->tap_s, 0, sizeof(st->tap_s));
+        std::memset(st->dft, 0, sizeof(st->dft));
+        for (int t = 0; t < NPAD; t++) st->col_of[t] = -1;
+        if (diag) {
+            const long double pi = acosl(-1.0L);
+            for (int m = 0; m < n; m++) {
+                const long double ang = -2.0L * pi * (long double)m / (long double)n;
+                st->dft[2 * m] = (double)cosl(ang);
+                st->dft[2 * m + 1] = (double)sinl(ang);
+            }
+            for (int j = 0; j < r; j++) {
+                const int t = ord[j];
+                const double sl = (double)sqrtl(lam[t]);
+                st->tap_of[j] = t;
+                st->col_of[t] = j;
+                st->col_s[j] = sl;
+                st->tap_s[t] = sl;
+            }
+            st->cov_taps = 1;
+        }
         st->cov_rank = r;
         st->cov_lmax = (double)(n * lmax);
         st->cov_lmin = r ? (double)(n * lam[ord[r - 1]]) : 0.0;

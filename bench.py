@@ -1015,7 +1015,7 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
     fr = wce.Context.frames(tx, rx, B)
     o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
     out = {"workload": f"{B} frames, PS_MMSE, Rhh = L-tap exponential PDP (rank L)"}
-    for L in (4, 8, 16, 53):
+    for L in (4, 8, 16, 24, 53):
         p = np.exp(-0.5 * np.arange(L))
         Rhh = np.zeros((N, N), np.complex128)
         Rhh[np.arange(L), np.arange(L)] = p / p.sum() * 1.1e-4
@@ -1042,6 +1042,30 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
                 leg.update({"wave_kernel": c.lr_kernel(B), "wave_kernel_ms_per_step": tw})
             finally:
                 assert lib.wce_debug_set_variant(3, 0) == 0
+        if lr and r > 16:
+            # the wave kernel's tap-domain Gram (diagonal Rhh, round 4) against the
+            # product Gram on the same ctx (variant 5); FP64-VALU bound, priced at
+            # the tap form's algorithmic flops: r x r Cholesky +
+            # triangular solves + the Q / D / read-out DFTs (20 N^2)
+            assert lib.wce_debug_set_variant(3, 5) == 0
+            try:
+                for _ in range(2):
+                    f()
+                tp = time_events(wce, stream, f, reps)
+                leg.update({"product_gram_kernel": c.lr_kernel(B), "product_gram_ms_per_step": tp,
+                            "taps_speedup": tp / t})
+            finally:
+                assert lib.wce_debug_set_variant(3, 0) == 0
+            fl = flop_lr_taps(r)
+            ach = fl * B / (t * 1e-3) / 1e12
+            kw, wsrc = pmc_leg("lowrank%d" % L, B, N * 16.0 * B, waves=B)
+            leg["roofline"] = {"bound": "valu-f64", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                               "frac": ach / PEAK_FP64_TFLOPS, "flops_per_frame": fl,
+                               "traffic": hbm_bytes(kw) if kw else None, "pmc_source": wsrc}
+            if kw:
+                leg["pmc_per_wave"] = {k: kw[k] / B for k in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_LDS",
+                                                              "SQ_WAIT_INST_LDS", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES")
+                                       if k in kw}
         if L in (16, 53):
             # constant-modulus frames (the synthetic BPSK: +-A, DC null) on the shared
             # operator K = (a C P + b I)^-1 C (wce_ctx_set_modulus): two f64-MFMA
@@ -1089,6 +1113,15 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
         out[f"L{L}"] = leg
         del c
     return out
+
+
+def flop_lr_taps(r):
+    """Algorithmic flops of one frame on the tap-domain Gram path: the r x r
+    Cholesky and the bordered / back substitutions (as the dense solve's, at
+    size r) plus the three 53-point DFTs of the Gram row Q (real weights,
+    4 N^2), the border D and the read-out (8 N^2 each); real symbols (no
+    correction DFTs), as the bench's BPSK frames."""
+    return 4.0 / 3.0 * r ** 3 + 8.0 * r * r + 20.0 * N * N
 
 
 def ctx_scan(c, H, n, s):

@@ -116,6 +116,7 @@ def test_no_device_fails_loudly(wce):
 
 
 CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16     # State's constant-modulus operator Kcm, pattern pcm, cm_on (+ 12 B)
+TAPS_TAIL = 16 + 2 * 64 * 4 + 2 * 64 * 8 + 64 * 16   # cov_taps (+ 12 B), tap_of, col_of, col_s, tap_s, dft
 
 
 def _pdp_cov(L=53, decay=0.12):
@@ -139,8 +140,9 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
     # State tail: a, b, ow2, xmask, mode, magic, then the low-rank factor
     # U, UT (64 x 64 complex each), cov_lmax, cov_lmin, cov_rank, cov_k0,
     # the layout version and size (+ 8 B reserved), the lane kernel's P_k
-    # (53 x 36 complex) and the constant-modulus operator (CM_TAIL)
-    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 16 + 53 * 36 * 16 + CM_TAIL)]
+    # (53 x 36 complex), the constant-modulus operator (CM_TAIL) and the
+    # tap-domain tables (TAPS_TAIL)
+    t = blob[:len(blob) - (2 * 64 * 64 * 16 + 16 + 8 + 16 + 53 * 36 * 16 + CM_TAIL + TAPS_TAIL)]
     a, b, ow2 = t[-40:-16].view(np.float64)
     mode, magic = t[-8:].view(np.int32)
     assert (a, b, ow2, mode, magic) == (1.0, inp["ow2"], inp["ow2"], wce.MMSE_COV, 0x80211)
@@ -150,7 +152,7 @@ def test_cov_state_C_is_F_Rhh_FH(wce, golden):
 
 def _state_field_offset(blob):
     """byte offset of (cov_rank, cov_k0, layout, bytes) in a state blob"""
-    return len(blob) - (53 * 36 * 16 + 24 + CM_TAIL)
+    return len(blob) - (53 * 36 * 16 + 24 + CM_TAIL + TAPS_TAIL)
 
 
 def test_state_validation_rejects_foreign_blobs(wce, golden):

@@ -8,6 +8,22 @@ import pytest
 from oracle_py import N, normrel
 
 
+CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16               # State: Kcm, pcm, cm_on (+ 12 B)
+TAPS_TAIL = 16 + 2 * 64 * 4 + 2 * 64 * 8 + 64 * 16   # State: cov_taps (+ 12 B), tap_of, col_of, col_s, tap_s, dft
+
+
+def taps_tables(blob):
+    """State's tap-domain tables (the blob's last TAPS_TAIL bytes)."""
+    t = blob[len(blob) - TAPS_TAIL:]
+    on = int(t[:4].view(np.int32)[0])
+    tap_of = t[16:272].view(np.int32)
+    col_of = t[272:528].view(np.int32)
+    col_s = t[528:1040].view(np.float64)
+    tap_s = t[1040:1552].view(np.float64)
+    dft = t[1552:].view(np.complex128)
+    return on, tap_of, col_of, col_s, tap_s, dft
+
+
 def pdp_rhh(L, decay):
     p = np.exp(-decay * np.arange(L))
     R = np.zeros((N, N), np.complex128)
@@ -127,8 +143,7 @@ def test_lane_gram_factors(wce, oracle, inp, L, rot):
     blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
     U, r, _, _, _ = wce.cov_factor(blob)
     assert r == L
-    CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16   # the constant-modulus members after P_k (round 4)
-    end = len(blob) - CM_TAIL
+    end = len(blob) - CM_TAIL - TAPS_TAIL   # the round-4 members after P_k
     P = blob[end - N * 36 * 16:end].view(np.complex128).reshape(N, 36)
     if L > 8:
         assert not np.any(P)
@@ -152,7 +167,7 @@ def _cm_operator(wce, blob, R, x_ref):
     rc = lib.wce_state_set_modulus(blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes, Rc.ctypes.data_as(ctypes.c_void_p),
                                    x.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0, rc
-    tail = blob[len(blob) - (64 * 64 * 16 + 64 * 8 + 16):]
+    tail = blob[len(blob) - (CM_TAIL + TAPS_TAIL):len(blob) - TAPS_TAIL]
     K = tail[:64 * 64 * 16].view(np.complex128).reshape(64, 64)[:N, :N]
     p = tail[64 * 64 * 16:64 * 64 * 16 + 64 * 8].view(np.float64)[:N]
     on = int(tail[-16:-12].view(np.int32)[0])
@@ -215,3 +230,96 @@ def test_constant_modulus_rejects_mismatch(wce, inp):
     rc = lib.wce_state_set_modulus(blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes,
                                    R.ctypes.data_as(ctypes.c_void_p), x.ctypes.data_as(ctypes.c_void_p))
     assert rc != 0
+
+
+@pytest.mark.parametrize("L,decay,spread", [(53, 0.5, False), (24, 0.3, False), (20, 0.2, True)])
+def test_tap_tables(wce, oracle, inp, L, decay, spread):
+    """A diagonal Rhh sets State's tap-domain tables (mmse_lr_kernel<K0, true>):
+    column j <-> tap t_j in descending power, sqrt(lambda) by column and by
+    tap, and the exact DFT E[m] = exp(-2 pi i m / 53); U[:, j] of the same
+    state is s_j F[:, t_j] with the reference's F (main.c:18-26), which the
+    exact DFT matches to the reference F's own phase error (<= 1e-13)."""
+    R = pdp_rhh(L, decay)
+    if spread:                                   # taps not at 0..L-1, not in power order
+        perm = np.random.default_rng(3).permutation(N)
+        R = R[np.ix_(perm, perm)]
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    U, r, _, _, _ = wce.cov_factor(blob)
+    on, tap_of, col_of, col_s, tap_s, dft = taps_tables(blob)
+    assert on == 1 and r == L
+    lam = np.diag(R).real
+    t = tap_of[:r]
+    assert np.all(np.diff(lam[t]) <= 0) and len(set(t)) == r        # descending power, distinct taps
+    assert np.array_equal(col_of[t], np.arange(r)) and np.sum(col_of >= 0) == r
+    assert np.allclose(col_s[:r], np.sqrt(lam[t]), rtol=1e-15, atol=0) and not np.any(col_s[r:])
+    assert np.array_equal(tap_s[t], col_s[:r]) and np.sum(tap_s != 0) == r
+    m = np.arange(N)
+    ang = np.longdouble(-2) * np.longdouble("3.14159265358979323846264338327950288") * m / N
+    ex = np.cos(ang) + 1j * np.sin(ang)
+    assert np.max(np.abs(dft[:N] - ex.astype(np.complex128))) <= 1.6e-16 and not np.any(dft[N:])   # rounded once
+    E = dft[:N]
+    Ut = E[np.outer(m, t) % N] * col_s[:r]      # the kernel's U
+    assert np.max(np.abs(Ut - U[:, :r])) <= 1e-13 * np.max(col_s)
+
+
+def test_tap_tables_off_for_non_diagonal(wce, inp):
+    R = pdp_rhh(24, 0.3)
+    R[2, 5] = R[5, 2] = 1e-9
+    on, tap_of, col_of, _, _, _ = taps_tables(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R))
+    assert on == 0 and not np.any(tap_of) and np.all(col_of == -1)
+
+
+def _taps_np(blob, tx, rx, a, b):
+    """The tap-domain Gram path's algebra in fp64 (mmse_lr_kernel<K0, true>
+    without its register layout): Q / D DFTs, Gram s_i s_j Q(t_i - t_j), the
+    read-out and correction as DFTs over the taps."""
+    on, tap_of, col_of, col_s, tap_s, dft = taps_tables(blob)
+    r = int(np.sum(col_of >= 0))
+    E = dft[:N]
+    k = np.arange(N)
+    Ekm = E[np.outer(k, k) % N]                       # E[k m]
+    p = np.abs(tx) ** 2
+    Q = (p[:, None] * Ekm.conj()).sum(0)              # Q(d) = sum_k p_k conj(E[k d])
+    D = ((tx * rx.conj())[:, None] * Ekm).sum(0)      # D(m) = sum_k v_k E[k m]
+    t, s = tap_of[:r], col_s[:r]
+    G = a * np.outer(s, s) * Q[(t[:, None] - t[None, :]) % N] + b * np.eye(r)
+    beta = np.conj(s * D[t])                          # G^H rx (the border row is its conjugate)
+    L = np.linalg.cholesky(G)
+    tt = np.linalg.solve(L.conj().T, np.linalg.solve(L, beta))
+    c = np.zeros(N, complex)
+    c[t] = s * tt
+    y = Ekm @ c
+    if np.any(tx.imag != 0):
+        v = (tx - tx.conj()) * (rx - a * tx * y)
+        w = Ekm.conj().T @ v
+        y = y + Ekm @ (tap_s ** 2 * np.pad(w, (0, 64 - N)))[:N] / b
+    return y
+
+
+@pytest.mark.parametrize("L,decay", [(53, 0.5), (46, 0.1), (24, 0.3), (16, 0.5)])
+def test_taps_algebra_vs_long_double(wce, oracle, inp, L, decay):
+    """The tap-domain form runs the exact DFT, not main.c's F: its answers
+    stay within ~1e-13 of the long double solve with the reference's F
+    (profiles/r04_accuracy_probe.txt: 1.3e-13 on the widest PDP); fp64 numpy
+    here adds its own ~eps cond rounding."""
+    R = pdp_rhh(L, decay)
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    F = oracle.fmatrix()
+    C = F @ oracle._ld(R) @ F.conj().T
+    rng = np.random.default_rng(L)
+    ow2 = inp["ow2"]
+    worst = 0.0
+    for i in range(12):
+        if i % 3 == 0:
+            tx = 8.8753 * rng.choice([-1.0, 1.0], N).astype(complex)
+        else:
+            lv = np.array([-3, -1, 1, 3]) * 8.8753 / np.sqrt(10)
+            tx = lv[rng.integers(0, 4, N)] + 1j * lv[rng.integers(0, 4, N)]
+        tx[26] = 0
+        h = (rng.standard_normal(N) + 1j * rng.standard_normal(N)) * 0.007
+        h = np.fft.fft(np.fft.ifft(h) * (np.arange(N) < 6))
+        rx = h * tx + np.sqrt(ow2 / 2) * (rng.standard_normal(N) + 1j * rng.standard_normal(N))
+        got = _taps_np(blob, tx, rx, 1.0, ow2)
+        exp = oracle.mmse_unified(C, np.ones(N, np.uint8), 1.0, ow2, tx, rx)
+        worst = max(worst, float(normrel(got, exp)))
+    assert worst < 1e-11, worst

@@ -62,6 +62,15 @@ for L, decay in ((1, 0.5), (4, 0.5), (6, 0.5), (8, 0.5), (16, 0.5), (24, 0.3), (
         err = orc.normrel(c.estimate_host(txh, rxh, mask=wce.PS_MMSE)["ps_mmse"], ref)
         mark = "*" if (path == 2) == lr else " "
         row.append(f"{name}{mark} max {err.max():.2e} median {np.median(err):.2e}")
+        if path == 2 and lr and r > 16:   # round 4: the wave kernel runs the tap-domain Gram; the product Gram beside it
+            lib = wce.load()
+            assert lib.wce_debug_set_variant(3, 5) == 0
+            try:
+                errp = orc.normrel(c.estimate_host(txh, rxh, mask=wce.PS_MMSE)["ps_mmse"], ref)
+            finally:
+                assert lib.wce_debug_set_variant(3, 0) == 0
+            row[-1] = row[-1].replace("low-rank", "low-rank(taps)")
+            row.append(f"product-Gram max {errp.max():.2e} median {np.median(errp):.2e}")
     print(f"L={L:2d} decay={decay:4.2f} rank={r:2d} spectrum {lmax / lmin if lmin else float('inf'):8.1e}: "
           + "   ".join(row))
     del c

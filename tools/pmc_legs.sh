@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc_legs
 mkdir -p "$OUT"
-LEGS=${*:-"headline apply apply1m cov_solve ref ls ls_pilots front_blocks front_preamble config5 config5_ref config5_ref_f32 lowrank4 lowrank8 lowrank16 lowrank8_1m config5_ref_fc config5_ref_fc_factors frame_cov_ref cm16 cm53"}
+LEGS=${*:-"headline apply apply1m cov_solve ref ls ls_pilots front_blocks front_preamble config5 config5_ref config5_ref_f32 lowrank4 lowrank8 lowrank16 lowrank24 lowrank53 lowrank8_1m config5_ref_fc config5_ref_fc_factors frame_cov_ref cm16 cm53"}
 run() {
   local leg=$1 name=$2; shift 2
   mkdir -p "$OUT/$leg"
