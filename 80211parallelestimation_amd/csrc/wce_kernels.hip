@@ -549,8 +549,15 @@ struct SolveLds {
             double rd[64];    // r_k = 1 / d_k, 0 past 52
         };
         double2 conv[56 * CVS];   // row-per-lane panels: block column -> rows (to_rows)
+        struct {                  // the tap-domain Gram's DFT pair tables (lr_dft53p), past blk / z / rd
+            double2 pad_bzr[160];
+            double2 pa[32], pb[32];   // c_k + c_{53-k}, c_k - c_{53-k}, k = 1..26 (complex vectors)
+            double2 rp[32];           // the same for the real vector |x|^2, {sum, difference}
+        } tp;
     };
 };
+static_assert(sizeof(SolveLds::tp.pad_bzr) == 2 * sizeof(SolveLds::blk) + sizeof(SolveLds::rd),
+              "the tap pair tables start past blk / z / rd");
 // conv element (row, c) at row * 9 + c: the odd row stride keeps both the
 // block-cyclic stores and the row reads bank-conflict free (an XOR swizzle of
 // an unpadded buffer measured 1% slower: address VALU).
@@ -1510,20 +1517,46 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
 // lambda_t, then a fourth.  E[k d mod 53] is gathered from LDS by the exact
 // index recurrence (no phase accumulation).
 // ---------------------------------------------------------------------
-// lane m: sum_k c_k E[k m] (CONJ: conj(E[k m])) over LDS vectors e (E) and c
-template <bool CONJ>
-__device__ __forceinline__ double2 lr_dft53(const double2 *e, const double2 *c, int m)
+#ifndef WCE_TAPS_UNROLL
+#define WCE_TAPS_UNROLL 2
+#endif
+// Every DFT here runs over pairs (k, 53 - k): E[(53 - k) m] = conj(E[k m]), so
+//     c_k E[km] + c_{53-k} conj(E[km]) = (c_k + c_{53-k}) Re E[km] + i (c_k - c_{53-k}) Im E[km]
+// -- one gather and half the FMAs and index steps of the plain sum.
+// pair tables of the LDS vector c (53 complex) on lanes 1..26
+__device__ __forceinline__ void dft_pairs(const double2 *c, double2 *pa, double2 *pb, int lane)
 {
-    double2 y = make_double2(0.0, 0.0);
-    int idx = 0;
-#pragma unroll 8
-    for (int k = 0; k < NSC; ++k) {
-        const double2 w = e[idx], v = c[k];
+    if (lane >= 1 && lane <= NSC / 2) {
+        const double2 u = c[lane], w = c[NSC - lane];
+        pa[lane] = cadd(u, w);
+        pb[lane] = csub(u, w);
+    }
+}
+// lane m: sum_k c_k E[k m] (CONJ: conj(E[k m])) = c_0 + sum over the pairs
+// E[k m mod 53] by byte offset: the step m * 16 added, 848 subtracted when it
+// wraps -- min_u32(o + s, o + s - 848) (the wrapped value underflows to a huge
+// unsigned when no wrap is due): three integer ops and no shift per gather
+__device__ __forceinline__ uint32_t dft_step(uint32_t o, uint32_t s, uint32_t s_wrap)
+{
+    return min(o + s, o + s_wrap);
+}
+__device__ __forceinline__ double2 ld_e(const double2 *e, uint32_t o)
+{
+    return *reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(e) + o);
+}
+template <bool CONJ>
+__device__ __forceinline__ double2 lr_dft53p(const double2 *e, const double2 *pa, const double2 *pb, double2 c0, int m)
+{
+    double2 y = c0;
+    const uint32_t st = 16u * (uint32_t)m, sw = st - 16u * NSC;
+    uint32_t o = st;   // 16 (k m mod 53) at k = 1 (m < 53)
+#pragma unroll WCE_TAPS_UNROLL
+    for (int k = 1; k <= NSC / 2; ++k) {
+        const double2 w = ld_e(e, o), A = pa[k], B = pb[k];
         const double wy = CONJ ? -w.y : w.y;
-        y.x = fma(v.x, w.x, fma(-v.y, wy, y.x));
-        y.y = fma(v.x, wy, fma(v.y, w.x, y.y));
-        idx += m;
-        idx = idx >= NSC ? idx - NSC : idx;
+        y.x = fma(A.x, w.x, fma(-B.y, wy, y.x));
+        y.y = fma(A.y, w.x, fma(B.x, wy, y.y));
+        o = dft_step(o, st, sw);
     }
     return y;
 }
@@ -1542,23 +1575,34 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, Solve
         s.rd[lane] = fma(xl.x, xl.x, xl.y * xl.y);
     }
     wave_lds_sync();
-    double2 Qd = make_double2(0.0, 0.0), Dd = make_double2(0.0, 0.0);
+    dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
+    if (lane >= 1 && lane <= NSC / 2) {
+        const double u = s.rd[lane], w = s.rd[NSC - lane];
+        s.tp.rp[lane] = make_double2(u + w, u - w);
+    }
+    wave_lds_sync();
+    // Q(d) = sum_k p_k conj(E[k d]), D(d) = sum_k v_k E[k d] on lane d
+    double2 Qd = make_double2(s.rd[0], 0.0), Dd = s.u[1][0];
+#ifdef WCE_ABLATE_TAPS_DFT   // timing-only: no Q / D DFTs
+    Qd = make_double2(s.rd[lane], 0.0);
+    Dd = s.u[1][lane];
+#else
     {
-        const int d = act ? lane : 0;
-        int idx = 0;
-#pragma unroll 8
-        for (int k = 0; k < NSC; ++k) {
-            const double2 w = s.u[0][idx], v = s.u[1][k];
-            const double pk = s.rd[k];
-            Qd.x = fma(pk, w.x, Qd.x);
-            Qd.y = fma(-pk, w.y, Qd.y);
-            Dd.x = fma(v.x, w.x, fma(-v.y, w.y, Dd.x));
-            Dd.y = fma(v.x, w.y, fma(v.y, w.x, Dd.y));
-            idx += d;
-            idx = idx >= NSC ? idx - NSC : idx;
+        const uint32_t st = 16u * (uint32_t)(act ? lane : 0), sw = st - 16u * NSC;
+        uint32_t o = st;
+#pragma unroll WCE_TAPS_UNROLL
+        for (int k = 1; k <= NSC / 2; ++k) {
+            const double2 w = ld_e(s.u[0], o), va = s.tp.pa[k], vb = s.tp.pb[k];
+            const double2 pp = s.tp.rp[k];   // {p_k + p_{53-k}, p_k - p_{53-k}}
+            Qd.x = fma(pp.x, w.x, Qd.x);
+            Qd.y = fma(-pp.y, w.y, Qd.y);
+            Dd.x = fma(va.x, w.x, fma(-vb.y, w.y, Dd.x));
+            Dd.y = fma(va.y, w.x, fma(vb.x, w.y, Dd.y));
+            o = dft_step(o, st, sw);
         }
     }
-    wave_lds_sync();   // every lane's reads of u[1] / rd are done
+#endif
+    wave_lds_sync();   // every lane's reads of u[1] / the pair tables are done
     s.blk[lane] = Qd;
     s.z[lane] = Dd;
     s.u[1][lane] = make_double2(st->col_s[lane], (double)st->tap_of[lane]);   // column j: {s_j, t_j}
@@ -1635,18 +1679,27 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
         s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
     }
     wave_lds_sync();
+    dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
+    wave_lds_sync();
     const int kk = act ? lane : 0;
     const double2 xl = s.x[lane];   // re-read: nothing of the frame stays live across the factorisation
-    double2 y = lr_dft53<false>(s.u[0], s.u[1], kk);   // y_k = sum_t c_t E[k t]
+#ifdef WCE_ABLATE_TAPS_OUT   // timing-only: no read-out DFT
+    double2 y = s.u[1][kk];
+#else
+    double2 y = lr_dft53p<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], kk);   // y_k = sum_t c_t E[k t]
+#endif
     if (__ballot(act && xl.y != 0.0) != 0) {   // complex symbols: y += U U^H [(x - conj x) o rho] / b
         const double2 rho = csub(s.rx[lane], cscale(cmul(xl, y), ac));   // b Ryy^-1 rx
         s.blk[lane] = act ? make_double2(-2.0 * xl.y * rho.y, 2.0 * xl.y * rho.x) : make_double2(0, 0);
+        wave_lds_sync();   // (also: every lane's read-out reads of the pair tables are done)
+        dft_pairs(s.blk, s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
-        const double2 w = lr_dft53<true>(s.u[0], s.blk, kk);   // w_t = sum_k conj(E[k t]) v_k
-        wave_lds_sync();   // u[1] (c) is dead once every lane's read-out is done
+        const double2 w = lr_dft53p<true>(s.u[0], s.tp.pa, s.tp.pb, s.blk[0], kk);   // w_t = sum_k conj(E[k t]) v_k
         s.u[1][lane] = act ? cscale(w, ts * ts / bc) : make_double2(0.0, 0.0);
         wave_lds_sync();
-        y = cadd(y, lr_dft53<false>(s.u[0], s.u[1], kk));
+        dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
+        wave_lds_sync();
+        y = cadd(y, lr_dft53p<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], kk));
     }
     return y;
 }
@@ -1656,9 +1709,13 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
 // K0 = 0 (r > 45: a Gram system as large as Ryy itself) holds all 28
 // register blocks through the product build: 2 waves/SIMD; K0 = 1: 156.
 // TAPS: the tap-domain Gram (State::cov_taps), registers as the dense solve's.
+#ifndef WCE_TAPS_WAVES_K0   // the tap form at K0 = 0 (168 VGPRs, 13 spilled at 3 waves/SIMD)
+#define WCE_TAPS_WAVES_K0 WCE_DENSE_WAVES_PER_SIMD
+#endif
 constexpr int lr_waves(int k0, bool taps)
 {
-    return taps ? WCE_DENSE_WAVES_PER_SIMD : (k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD));
+    return taps ? (k0 == 0 ? WCE_TAPS_WAVES_K0 : WCE_DENSE_WAVES_PER_SIMD)
+                : (k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD));
 }
 template <int K0, bool TAPS = false>
 __global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)

@@ -567,12 +567,29 @@ def bench_config5_sharded(wce, ctx, dist, stream, steps, total=1 << 20, prewarm_
     # outputs, the fp64 MMSE, the 15 fp32 equalized blocks); max over ranks
     bad = sum(ctx.nonfinite_scan(h, count, f32=(i < 4), stream=s)[1] for i, h in enumerate(outs))
     bad += ctx.nonfinite_scan(eq, count * NBLK, f32=True, stream=s)[1]
-    return {"workload": "BASELINE configs[4]: all 5 estimators + equalization fused, fp64 solve / fp32 LS and eq "
-                        "outputs, per-frame preambles, 1,048,576 frames sharded over the ranks",
-            "global_frames": total, "frames_per_gpu": count, "n_gpus": dist.world, "steps": steps,
-            "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong",
-            "nonfinite_outputs": int(dist.max(float(bad))),
-            **config5_traffic(count, dt)}
+    res = {"workload": "BASELINE configs[4]: all 5 estimators + equalization fused, fp64 solve / fp32 LS and eq "
+                       "outputs, per-frame preambles, 1,048,576 frames sharded over the ranks",
+           "global_frames": total, "frames_per_gpu": count, "n_gpus": dist.world, "steps": steps,
+           "ms_per_step": dt * 1e3, "frames_per_s": total / dt, "scaling": "strong",
+           "nonfinite_outputs": int(dist.max(float(bad))),
+           **config5_traffic(count, dt)}
+    if dist.world == 1:
+        # where the time goes (untimed, N = 1 only): the same frames' PS_MMSE
+        # alone (the fused kernel's solve), and board power / shader clock
+        # under each -- the FP64 solve holds the board at its power cap, and
+        # the epilogue's HBM stream shares that budget
+        Hm = wce.DeviceArray((count, N))
+        om = wce.Outputs(None, None, None, None, Hm.addr, None, N, 0, 0, 0, 0)
+        solo = lambda: ctx.estimate(fr, om, wce.PS_MMSE, s)
+        for _ in range(3):
+            solo()
+        t_solo = time_events(wce, stream, solo, 5)
+        res["solve_only_ms"] = t_solo
+        res["epilogue_ms"] = dt * 1e3 - t_solo
+        res["board_fused"] = power_clock(stream, lambda: ctx.estimate(fr, o, wce.ALL, s), seconds=2.0)
+        res["board_solve_only"] = power_clock(stream, solo, seconds=2.0)
+        del Hm
+    return res
 
 
 def config5_traffic(count, dt):
