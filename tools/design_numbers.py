@@ -33,8 +33,16 @@ if c4:
     row(f"BASELINE configs[3] batch (1,048,576 frames, sharded over {c4['n_gpus']} GPU(s), strong scaling)",
         f"{c4['frames_per_s']:.3g} frames/s")
 if c5s:
+    extra = ""
+    if c5s.get("solve_only_ms"):
+        extra = f"; {c5s['ms_per_step']:.2f} ms per step, PS_MMSE alone on the same frames {c5s['solve_only_ms']:.2f} ms"
+        bf, bs = c5s.get("board_fused"), c5s.get("board_solve_only")
+        if bf and bs:
+            extra += (f"; board {bf['socket_power_W']:.0f} W / {bf['gfx_clock_MHz']:.0f} MHz fused, "
+                      f"{bs['socket_power_W']:.0f} W / {bs['gfx_clock_MHz']:.0f} MHz solve alone")
     row(f"BASELINE configs[4] as named (1,048,576 frames, all 5 + eq fused, fp64 solve / fp32 LS, sharded over "
-        f"{c5s['n_gpus']} GPU(s))", f"{c5s['frames_per_s']:.3g} frames/s; non-finite outputs: {c5s.get('nonfinite_outputs')}")
+        f"{c5s['n_gpus']} GPU(s))",
+        f"{c5s['frames_per_s']:.3g} frames/s; non-finite outputs: {c5s.get('nonfinite_outputs')}" + extra)
 row("MMSE frames/s, REF (diagonal Ryy: no factorisation), 65,536 frames (MALL-resident)",
     f"{d['ref_mode']['frames_per_s_per_gpu']:.3g}")
 rb = d["ref_mode"].get("b1048576")
@@ -48,6 +56,34 @@ cv = d["cov_mode"]
 row("MMSE with a dense model covariance (COV: Cholesky keeping L + back-substitution, then MFMA `C·W`)",
     f"{cv['frames_per_s_per_gpu']:.3g} frames/s; solve {cv['solve_tflops']:.1f} TFLOP/s = "
     f"{100 * cv['solve_frac_fp64_peak']:.0f}% of FP64 peak")
+cm = cv.get("constant_modulus")
+if cm:
+    row("the same on constant-modulus frames (`wce_ctx_set_modulus`: K = (a C P + b I)⁻¹ C once, H = K (x̄ ∘ rx) on "
+        "f64 MFMA; never the headline)",
+        f"{cm['frames_per_s_per_gpu']:.3g} frames/s ({cm['speedup_vs_per_frame']:.1f}× the per-frame path), "
+        f"{cm['achieved_GBs'] / 1000:.2f} TB/s of the 2,544 B a frame moves")
+lr = d.get("cov_lowrank")
+if lr:
+    parts = []
+    for L in ("L4", "L8", "L16", "L24", "L53"):
+        if L in lr:
+            x = lr[L]
+            parts.append(f"{L[1:]} taps `{x['kernel']}` {x['ms_per_step']:.3f} ms ({x['frames_per_s']:.3g} frames/s)"
+                         + (f", product Gram {x['product_gram_ms_per_step']:.3f} ms" if "product_gram_ms_per_step" in x
+                            else "")
+                         + (f", {100 * x['roofline']['frac']:.0f}% of FP64 peak by its algorithmic flops"
+                            if "roofline" in x else ""))
+    row("MMSE with an L-tap power-delay profile (COV low-rank paths, 65,536 frames)", "; ".join(parts))
+    for L in ("L16", "L53"):
+        c = lr.get(L, {}).get("constant_modulus")
+        if c:
+            row(f"the same, {L[1:]} taps, constant-modulus frames (operator path)",
+                f"{c['ms_per_step']:.3f} ms ({c['frames_per_s']:.3g} frames/s, {c['speedup_vs_per_frame']:.1f}× "
+                f"the per-frame path; {100 * c['roofline']['frac']:.0f}% of HBM)")
+    b8 = lr.get("L8", {}).get("frames_1048576")
+    if b8:
+        row("rank 8 at 1,048,576 frames (two-workgroups-per-CU build)",
+            f"{b8['ms_per_step']:.3f} ms ({b8['frames_per_s']:.3g} frames/s, {100 * b8['roofline']['frac']:.0f}% of HBM)")
 ap = d["apply_kernel"]
 row("`matvec_kernel` as `H = C·W` (f64 MFMA, COV mode, 65,536 frames = 4,096 waves)",
     f"{ap['achieved_tflops']:.1f} TFLOP/s algorithmic = {100 * ap['frac_fp64_peak']:.0f}% of FP64 peak; "
@@ -67,6 +103,16 @@ if "frames_1M" in ap:
            if "executed_tflops" in ab else ""))
 row("per-frame covariance MMSE (`FRAME_COV`)",
     f"{d['frame_cov']['textbook']['frames_per_s']:.3g} frames/s TEXTBOOK, {d['frame_cov']['ref']['frames_per_s']:.3g} REF")
+c5r = d.get("config5_ref")
+if c5r:
+    txt = []
+    for k, lab in (("fp64", "fp64"), ("mixed_fp64_solve_fp32_ls", "fp32 LS / eq"),
+                   ("frame_cov_fp64", "FRAME_COV fp64"), ("frame_cov_mixed_fp32_ls", "FRAME_COV fp32 LS / eq")):
+        if k in c5r:
+            x = c5r[k]
+            txt.append(f"{lab} {x['frames_per_s']:.3g} frames/s ({x['roofline']['achieved'] / 1000:.2f} TB/s)")
+    row("configs[4] in `main.c` semantics (REF + LS family + eq, 1,048,576 frames; FRAME_COV: each frame's PS_MMSE "
+        "on its own LT_LS, as main.c:37-53)", "; ".join(txt))
 row("config 5 share (131,072 frames, all 5 + equalization, fused)",
     f"{d['config5']['fp64']['frames_per_s']:.3g} frames/s fp64; "
     f"{d['config5']['mixed_fp64_solve_fp32_ls']['frames_per_s']:.3g} with fp32 LS outputs")
@@ -109,6 +155,13 @@ if refc:
     row("the reference's own code (`oracle/_ref`, 1 core)",
         f"LT_LS + PS_Linear {refc['ls_config2']['value']:.2g} frames/s; REF-mode PS_MMSE through its matrix routines "
         f"{refc['mmse_ref_mode']['value']:.0f} frames/s (NaN inverse repaired, per-frame 4-s `inverse(F)` hoisted)")
+    if "mmse_textbook" in refc:
+        mt = refc["mmse_textbook"]
+        fp = mt.get("frames_parallel", {})
+        row("the reference's own routines composing the TEXTBOOK (headline) formula (`multiply()` + cofactor "
+            "`inverse()`, `refh_mmse_formula`)",
+            f"{mt['value']:.3g} frames/s on 1 core ({mt['sample']})"
+            + (f"; {fp['value']:.3g} frames/s frames-parallel on {fp['cores']} cores" if fp else ""))
     if "ls_config2_omp" in refc:
         row(f"the reference's own functions, frames-parallel OpenMP loop ({refc['ls_config2_omp']['cores']} host "
             f"cores; its own OpenMP driver crashes)",
