@@ -25,7 +25,7 @@ struct wce_ctx {
     bool bdot = true;           // rank-1 C: second bordered row, no back-solve / GEMM (A/B switch)
     int32_t cov_k0 = -1;        // State::cov_k0 (WCE_MMSE_COV: >= 0 low-rank Gram path, -1 dense)
     int32_t cov_rank = 0;       // State::cov_rank
-    bool cov_taps = false;      // State::cov_taps (diagonal Rhh: the tap-domain Gram)
+    int cov_taps = 0;           // State::cov_taps | State::taps_contig << 1 (diagonal Rhh: the tap-domain forms)
     int cov_path = 0;           // wce_debug_set_cov_path: 0 auto, 1 dense, 2 low-rank
     bool cm_on = false;         // State::cm_on: a constant-modulus operator is loaded (wce_ctx_set_modulus)
     bool cm_use = true;         // wce_debug_set_cm: A/B switch of that path
@@ -200,7 +200,7 @@ int wce_ctx_mark_ready(wce_ctx *c)
     c->mode = h->mode;
     c->cov_rank = h->cov_rank;
     c->cov_k0 = h->cov_k0;
-    c->cov_taps = h->cov_taps != 0;
+    c->cov_taps = (h->cov_taps ? 1 : 0) | (h->taps_contig ? 2 : 0);
     c->cm_on = h->cm_on != 0;
     c->ready = true;
     return WCE_OK;
@@ -217,7 +217,7 @@ int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
     c->mode = st->mode;
     c->cov_k0 = st->cov_k0;
     c->cov_rank = st->cov_rank;
-    c->cov_taps = st->cov_taps != 0;
+    c->cov_taps = (st->cov_taps ? 1 : 0) | (st->taps_contig ? 2 : 0);
     c->cm_on = st->cm_on != 0;
     c->ready = true;
     return WCE_OK;

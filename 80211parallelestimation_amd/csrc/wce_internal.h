@@ -14,7 +14,7 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
-constexpr int32_t STATE_LAYOUT = 5;   // State layout version: bump with every change to struct State
+constexpr int32_t STATE_LAYOUT = 6;   // State layout version: bump with every change to struct State
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
@@ -80,7 +80,8 @@ struct State {
     // a double angle (phase error <= 6e-14): the two models' answers differ by
     // <= 1.3e-13 norm-relative on the widest PDP (profiles/r04_accuracy_probe.txt).
     int32_t cov_taps;          // 1: Rhh is diagonal and the tables below are set
-    int32_t taps_reserved[3];
+    int32_t taps_contig;       // 1: ... and its kept taps are 0..r-1, column j = tap j
+    int32_t taps_reserved[2];
     int32_t tap_of[NPAD];      // Gram column j -> delay tap t_j (j < cov_rank; 0 past it)
     int32_t col_of[NPAD];      // delay tap t -> Gram column (-1: dropped, or t >= 53)
     double col_s[NPAD];        // sqrt(lambda_j) by Gram column (0 past cov_rank)
@@ -95,11 +96,12 @@ static_assert(sizeof(State) % 16 == 0, "State must keep 16-B alignment");
 // wce_state_validate, wce_ctx_mark_ready after a broadcast).
 inline bool taps_ok(const State *st)
 {
-    if (st->cov_taps == 0) return true;
-    if (st->cov_taps != 1) return false;
+    if (st->cov_taps == 0) return st->taps_contig == 0;
+    if (st->cov_taps != 1 || (st->taps_contig != 0 && st->taps_contig != 1)) return false;
     for (int j = 0; j < NPAD; j++) {   // the kernels index LDS tables with these
         if (st->tap_of[j] < 0 || st->tap_of[j] >= NSC) return false;
         if (st->col_of[j] < -1 || st->col_of[j] >= st->cov_rank || (j >= NSC && st->col_of[j] != -1)) return false;
+        if (st->taps_contig && j < st->cov_rank && st->tap_of[j] != j) return false;
     }
     return true;
 }
@@ -209,9 +211,9 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream);
 // WCE_MMSE_COV low-rank path: H (or, split, H_b per (frame, block) row) from
 // the Gram system embedded at block row k0 (State::cov_k0)
 // (rank = State::cov_rank: ranks 1..LRL_RMAX run one frame per lane instead)
-int launch_mmse_lr(const State *st, int k0, int rank, bool taps, const SolveArgs &a, void *stream);
+int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs &a, void *stream);
 // the kernel launch_mmse_lr runs for `units` (frame, block) units (wce_debug_lr_kernel)
-const char *lr_kernel_name(int k0, int rank, bool taps, int64_t units);
+const char *lr_kernel_name(int k0, int rank, int taps, int64_t units);
 // REF + WCE_MMSE_FRAME_COV (C semantics) in one launch: LT_LS of rx_pre, u = Mu h,
 // w = Mw q(Mg h) at the pilot rows; hout: H = u s to a.w, else u / w rows to uw / ww
 int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,

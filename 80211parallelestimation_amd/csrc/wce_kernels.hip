@@ -1837,10 +1837,15 @@ __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, con
 }
 // Pl / Ul (WCE_LR_LDS_P, direct form): the workgroup's LDS copies of P_k
 // (R (R + 1) / 2 entries per k) and U (R per k); else State::Pk / State::U
-template <int R, bool STAGED, bool LP = false>
+// TQ (State::taps_contig, staged form with LDS tables): Pl holds E[k s mod 53]
+// (R per k) instead of P_k, and pass 1 accumulates the Toeplitz Gram's R
+// values Q(s) = sum_k |x_k|^2 conj(E[k s]) (2 FMAs each per subcarrier) instead
+// of its R (R + 1) / 2 products; Gamma_ij = s_i s_j Q(i - j) afterwards.
+template <int R, bool STAGED, bool LP = false, bool TQ = false>
 __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const SolveArgs &a, LrLaneLds *sp,
                                              int fpw, const double2 *Pl = nullptr, const double2 *Ul = nullptr)
 {
+    static_assert(!TQ || LP, "the Toeplitz pass reads its E table from LDS");
     constexpr int NO = R * (R - 1) / 2;   // strictly-lower Gram entries
     const int lane = threadIdx.x & 63;
     const int64_t units = a.split ? a.n * a.nblk : a.n;
@@ -1882,6 +1887,40 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
     for (int e = 0; e < NO; ++e) go[e] = make_double2(0.0, 0.0);
     bool cplx = false;
     constexpr int UN = R <= 4 ? WCE_LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
+    if constexpr (TQ) {
+        double q0 = 0.0;                      // Q(0) (real)
+        double2 qs[R > 1 ? R - 1 : 1];        // Q(1..R-1)
+#pragma unroll
+        for (int e = 0; e < R - 1; ++e) qs[e] = make_double2(0.0, 0.0);
+        lrl_sweep<STAGED, UN>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
+            if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+            cplx |= x.y != 0.0;
+            const double w = fma(x.x, x.x, x.y * x.y);
+            const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+            const double2 *Ek = P + k * R;   // E[k s mod 53], s < R
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const double2 u = U[k * uld + i];   // beta_i += conj(u) v
+                bt[i].x = fma(u.x, v.x, fma(u.y, v.y, bt[i].x));
+                bt[i].y = fma(u.x, v.y, fma(-u.y, v.x, bt[i].y));
+            }
+            q0 += w;
+#pragma unroll
+            for (int e = 1; e < R; ++e) {   // += w conj(E[k e])
+                const double2 ee = Ek[e];
+                qs[e - 1].x = fma(w, ee.x, qs[e - 1].x);
+                qs[e - 1].y = fma(-w, ee.y, qs[e - 1].y);
+            }
+        });
+        // Gamma_ij = s_i s_j Q(i - j): s wave-uniform (scalar loads)
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const double si = st->col_s[i];
+            gd[i] = si * si * q0;
+#pragma unroll
+            for (int j = 0; j < i; ++j) go[i * (i - 1) / 2 + j] = cscale(qs[i - j - 1], si * st->col_s[j]);
+        }
+    } else {
     lrl_sweep<STAGED, UN>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
         if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
         cplx |= x.y != 0.0;
@@ -1903,6 +1942,7 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
             }
         }
     });
+    }
     // A = a Gamma + b I = L L^H (lower L in place: ld = 1 / L_ii, lo = L_ij)
     double ld[R];
     double2 lo[NO > 0 ? NO : 1];
@@ -2038,20 +2078,26 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
 #define WCE_LR_STAGED_MINWG 2   // 1,048,576 frames: rank 7 898 -> 858 us, rank 8 955 -> 896 (2 waves/SIMD instead of 1; rank 8
 #endif                          // spills 52 B); at 65,536 frames (one wave per SIMD anyway) rank 8 63.3 -> 67.5, so MW = 1 there
 constexpr int lr_staged_threads(int r) { return ((WCE_LR_STAGED_LDS_P >> r) & 1) ? 256 : 64; }
-template <int R, int MW = 1>
+template <int R, int MW = 1, bool TQ = false>
 __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
 {
     if constexpr (lr_staged_threads(R) == 256) {
-        constexpr int NPR = R * (R + 1) / 2;
+        constexpr int NPR = TQ ? R : R * (R + 1) / 2;   // TQ: E[k s mod 53], s < R
         __shared__ double2 sP[NSC * NPR], sU[NSC * R];
         __shared__ LrLaneLds s[4];
         const double2 *Pg = reinterpret_cast<const double2 *>(st->Pk);
         const double2 *Ug = reinterpret_cast<const double2 *>(st->U);
-        for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x) sP[e] = Pg[(e / NPR) * LRL_NP + e % NPR];
+        if constexpr (TQ) {
+            for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x)
+                sP[e] = ld2(st->dft, ((e / NPR) * (e % NPR)) % NSC);
+        } else {
+            for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x) sP[e] = Pg[(e / NPR) * LRL_NP + e % NPR];
+        }
         for (int e = threadIdx.x; e < NSC * R; e += blockDim.x) sU[e] = Ug[(e / R) * CLD + e % R];
         __syncthreads();
-        lr_lane_body<R, true, true>(st, a, &s[threadIdx.x >> 6], 64, sP, sU);
+        lr_lane_body<R, true, true, TQ>(st, a, &s[threadIdx.x >> 6], 64, sP, sU);
     } else {
+        static_assert(!TQ, "the Toeplitz form runs in the 4-wave LDS-table build");
         __shared__ LrLaneLds s;
         lr_lane_body<R, true>(st, a, &s, 64);
     }
@@ -2139,7 +2185,13 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
 // rank 16 237 -> 271 us at 65,536 frames, 3.82 -> 4.39 ms at 1M; retired in
 // round 4, profiles/r03_ab_lowrank_ldsp.txt: U, 13.6 KB at rank 16, stays in
 // the scalar cache, and 3 waves/SIMD hide its latency)
-template <int R>
+// TQ (State::taps_contig: a power-delay profile whose kept taps are 0..R-1,
+// column j = tap j): Gamma = S Q S with Q(i - j) = sum_k p_k conj(E[k (i - j)])
+// Toeplitz, so pass 1 accumulates ONE Gram value per lane, Q(i) (2 FMAs per
+// subcarrier, E[k i mod 53] from an LDS copy of State::dft by the exact index
+// recurrence), instead of its row of R products (4R FMAs): the row's values
+// meet in LDS and lane i reads Q(|i - j|) (conjugated for j > i).
+template <int R, bool TQ = false>
 __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restrict__ st, SolveArgs a)
 {
     const int i = threadIdx.x & 15;   // the row of the R x R system this lane holds
@@ -2147,6 +2199,14 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // (frame, block) unit of the row
     const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);   // wave-uniform: scalar loads
     constexpr int uld = CLD;
+    __shared__ double2 sE[TQ ? 64 : 1];
+    __shared__ double2 sQ[TQ ? 16 : 1][TQ ? 16 : 1];   // one 16-lane row's Q(0..15)
+    __shared__ double2 sV[TQ ? 16 : 1][TQ ? 56 : 1];   // the row's frame: conj(x_k) rx_k ...
+    __shared__ double sW[TQ ? 16 : 1][TQ ? 56 : 1];    // ... and |x_k|^2
+    if constexpr (TQ) {
+        if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
+        __syncthreads();
+    }
     if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows (skip: the constant-modulus path wrote H)
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
@@ -2160,29 +2220,72 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     for (int j = 0; j < R; ++j) Ar[j] = make_double2(0.0, 0.0);
     double2 bt = make_double2(0.0, 0.0);
     bool cplx = false;
-#pragma unroll 1
-    for (int k = 0; k < NSC; ++k) {
-        double2 x = ld2(a.tx, base + k);   // the same 16 B in the row's 16 lanes
-        const double2 r = ld2(a.rx, base + k);
-        if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
-        cplx |= x.y != 0.0;
-        const double w = fma(x.x, x.x, x.y * x.y);
-        const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
-        const double2 ui = row ? U1[k * uld + i] : make_double2(0.0, 0.0);
-        bt.x = fma(ui.x, v.x, fma(ui.y, v.y, bt.x));   // += conj(u_i) v
-        bt.y = fma(ui.x, v.y, fma(-ui.y, v.x, bt.y));
-        const double2 wi = make_double2(w * ui.x, -w * ui.y);   // w conj(u_i)
+    if constexpr (TQ) {
+        // the row's frame through LDS: lane i loads subcarriers i, i + 16, ... (256 B
+        // per row and instruction), then every lane sweeps k from broadcast reads
+        const int rw = (threadIdx.x >> 4) & 15;
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const double2 uj = U1[k * uld + j];   // wave-uniform: scalar loads (or an LDS broadcast)
-            Ar[j].x = fma(wi.x, uj.x, fma(-wi.y, uj.y, Ar[j].x));
-            Ar[j].y = fma(wi.x, uj.y, fma(wi.y, uj.x, Ar[j].y));
+        for (int m = 0; m < 4; ++m) {
+            const int k = i + 16 * m;
+            if (k < NSC) {
+                double2 x = ld2(a.tx, base + k);
+                const double2 r = ld2(a.rx, base + k);
+                if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+                cplx |= x.y != 0.0;
+                sW[rw][k] = fma(x.x, x.x, x.y * x.y);
+                sV[rw][k] = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+            }
         }
-    }
+        wave_lds_sync();   // the row's 16 lanes are one wave's
+        // Q(i) = sum_k p_k conj(E[k i]), beta_i = s_i sum_k v_k conj(E[k i]) (U[k][i] = s_i E[k i])
+        double2 q = make_double2(0.0, 0.0), bq = make_double2(0.0, 0.0);
+        const uint32_t qs = 16u * (uint32_t)i, qw = qs - 16u * NSC;
+        uint32_t qo = 0;   // 16 (k i mod 53)
+#pragma unroll 4
+        for (int k = 0; k < NSC; ++k) {
+            const double2 e = ld_e(sE, qo), v = sV[rw][k];
+            const double w = sW[rw][k];
+            q.x = fma(w, e.x, q.x);                        // += p_k conj(E[k i])
+            q.y = fma(-w, e.y, q.y);
+            bq.x = fma(v.x, e.x, fma(v.y, e.y, bq.x));     // += v_k conj(E[k i])
+            bq.y = fma(v.y, e.x, fma(-v.x, e.y, bq.y));
+            qo = dft_step(qo, qs, qw);
+        }
+        const double si = row ? st->col_s[i] : 0.0;
+        bt = cscale(bq, si);
+        sQ[rw][i] = q;
+        wave_lds_sync();
 #pragma unroll
-    for (int j = 0; j < R; ++j) {   // a Gamma + b I; rows past R: the identity (never read)
-        Ar[j] = cscale(Ar[j], ac);
-        Ar[j].x += (i == j || (!row && j == 0)) ? bc : 0.0;
+        for (int j = 0; j < R; ++j) {   // a s_i s_j Q(i - j) + b [i == j]; rows past R: the identity (never read)
+            const double2 qd = j <= i ? sQ[rw][(i - j) & 15] : cconj(sQ[rw][(j - i) & 15]);
+            Ar[j] = cscale(qd, ac * si * st->col_s[j]);
+            Ar[j].x += (i == j || (!row && j == 0)) ? bc : 0.0;
+        }
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < NSC; ++k) {
+            double2 x = ld2(a.tx, base + k);   // the same 16 B in the row's 16 lanes
+            const double2 r = ld2(a.rx, base + k);
+            if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+            cplx |= x.y != 0.0;
+            const double w = fma(x.x, x.x, x.y * x.y);
+            const double2 v = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+            const double2 ui = row ? U1[k * uld + i] : make_double2(0.0, 0.0);
+            bt.x = fma(ui.x, v.x, fma(ui.y, v.y, bt.x));   // += conj(u_i) v
+            bt.y = fma(ui.x, v.y, fma(-ui.y, v.x, bt.y));
+            const double2 wi = make_double2(w * ui.x, -w * ui.y);   // w conj(u_i)
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const double2 uj = U1[k * uld + j];   // wave-uniform: scalar loads (or an LDS broadcast)
+                Ar[j].x = fma(wi.x, uj.x, fma(-wi.y, uj.y, Ar[j].x));
+                Ar[j].y = fma(wi.x, uj.y, fma(wi.y, uj.x, Ar[j].y));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {   // a Gamma + b I; rows past R: the identity (never read)
+            Ar[j] = cscale(Ar[j], ac);
+            Ar[j].x += (i == j || (!row && j == 0)) ? bc : 0.0;
+        }
     }
     double ldi = 1.0;
     lrq_chol<R, 0>(Ar, ldi, i);
@@ -2247,6 +2350,29 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     double2 y[4];   // H_k = U_k s at k = i + 16 m: t_j broadcast once per j
 #pragma unroll
     for (int m = 0; m < 4; ++m) y[m] = make_double2(0.0, 0.0);
+    if constexpr (TQ) {   // U[k][j] = s_j E[k j]: E from LDS by the index recurrence over j
+        uint32_t eo[4], es[4], ew[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = i + 16 * m;
+            es[m] = 16u * (uint32_t)(k < NSC ? k : 0);
+            ew[m] = es[m] - 16u * NSC;
+            eo[m] = 0;
+        }
+        const double ts = row ? st->col_s[i] : 0.0;
+        const double2 c = cscale(t, ts);   // s_i t_i on lane i
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double2 cj = row_bcast_n(c, j);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const double2 u = ld_e(sE, eo[m]);
+                y[m].x = fma(u.x, cj.x, fma(-u.y, cj.y, y[m].x));
+                y[m].y = fma(u.x, cj.y, fma(u.y, cj.x, y[m].y));
+                eo[m] = dft_step(eo[m], es[m], ew[m]);
+            }
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const double2 tj = row_bcast_n(t, j);
@@ -2257,6 +2383,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
             y[m].x = fma(u.x, tj.x, fma(-u.y, tj.y, y[m].x));
             y[m].y = fma(u.x, tj.y, fma(u.y, tj.x, y[m].y));
         }
+    }
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)   // the row stores 256 B of its frame per m
@@ -2951,7 +3078,8 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 enum class LrForm { Direct, Staged64, Staged, StagedMW, Quad, Wave };
 static LrForm lr_form(int rank, int64_t units)
 {
-    const int lv = variant(WCE_VARIANT_LR);
+    int lv = variant(WCE_VARIANT_LR);
+    if (lv == 5) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), not the kernel form
     if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
         // the LDS-staged form at every size by default (WCE_LR_STAGE_FROM = 0);
         // the direct form runs only as variant 2, the gate's independent check
@@ -2969,10 +3097,13 @@ static LrForm lr_form(int rank, int64_t units)
     return LrForm::Wave;
 }
 
-// a diagonal Rhh's tap-domain Gram on the wave kernel (variant 5: the product Gram)
-static bool lr_taps(bool taps) { return taps && variant(WCE_VARIANT_LR) != 5; }
+// taps: bit 0 State::cov_taps (a diagonal Rhh: the wave kernel's tap-domain
+// Gram), bit 1 State::taps_contig (kept taps 0..r-1: the quad and lane
+// kernels' Toeplitz form).  Variant 5 runs the product Gram everywhere (A/B).
+static bool lr_taps(int taps) { return (taps & 1) && variant(WCE_VARIANT_LR) != 5; }
+static bool lr_contig(int taps) { return (taps & 2) && variant(WCE_VARIANT_LR) != 5; }
 
-const char *lr_kernel_name(int k0, int rank, bool taps, int64_t units)
+const char *lr_kernel_name(int k0, int rank, int taps, int64_t units)
 {
     static const char *lane[2][LRL_RMAX + 1] = {
         {"", "mmse_lr_lane_kernel<1>", "mmse_lr_lane_kernel<2>", "mmse_lr_lane_kernel<3>", "mmse_lr_lane_kernel<4>",
@@ -2980,28 +3111,37 @@ const char *lr_kernel_name(int k0, int rank, bool taps, int64_t units)
         {"", "mmse_lr_lane_staged_kernel<1>", "mmse_lr_lane_staged_kernel<2>", "mmse_lr_lane_staged_kernel<3>",
          "mmse_lr_lane_staged_kernel<4>", "mmse_lr_lane_staged_kernel<5>", "mmse_lr_lane_staged_kernel<6>",
          "mmse_lr_lane_staged_kernel<7>", "mmse_lr_lane_staged_kernel<8>"}};
-    static const char *quad[] = {"mmse_lr_quad_kernel<9>", "mmse_lr_quad_kernel<10>", "mmse_lr_quad_kernel<11>",
-                                 "mmse_lr_quad_kernel<12>", "mmse_lr_quad_kernel<13>", "mmse_lr_quad_kernel<14>",
-                                 "mmse_lr_quad_kernel<15>", "mmse_lr_quad_kernel<16>"};
+    static const char *quad[2][8] = {
+        {"mmse_lr_quad_kernel<9>", "mmse_lr_quad_kernel<10>", "mmse_lr_quad_kernel<11>", "mmse_lr_quad_kernel<12>",
+         "mmse_lr_quad_kernel<13>", "mmse_lr_quad_kernel<14>", "mmse_lr_quad_kernel<15>", "mmse_lr_quad_kernel<16>"},
+        {"mmse_lr_quad_kernel<9, true>", "mmse_lr_quad_kernel<10, true>", "mmse_lr_quad_kernel<11, true>",
+         "mmse_lr_quad_kernel<12, true>", "mmse_lr_quad_kernel<13, true>", "mmse_lr_quad_kernel<14, true>",
+         "mmse_lr_quad_kernel<15, true>", "mmse_lr_quad_kernel<16, true>"}};
     static const char *wave[2][7] = {
         {"mmse_lr_kernel<0>", "mmse_lr_kernel<1>", "mmse_lr_kernel<2>", "mmse_lr_kernel<3>", "mmse_lr_kernel<4>",
          "mmse_lr_kernel<5>", "mmse_lr_kernel<6>"},
         {"mmse_lr_kernel<0, true>", "mmse_lr_kernel<1, true>", "mmse_lr_kernel<2, true>", "mmse_lr_kernel<3, true>",
          "mmse_lr_kernel<4, true>", "mmse_lr_kernel<5, true>", "mmse_lr_kernel<6, true>"}};
-    static const char *mw[] = {"mmse_lr_lane_staged_kernel<7, 2>", "mmse_lr_lane_staged_kernel<8, 2>"};
+    static const char *mw[2][2] = {{"mmse_lr_lane_staged_kernel<7, 2>", "mmse_lr_lane_staged_kernel<8, 2>"},
+                                   {"mmse_lr_lane_staged_kernel<7, 2, true>", "mmse_lr_lane_staged_kernel<8, 2, true>"}};
+    static const char *lanetq[LRL_RMAX + 1] = {
+        "", "mmse_lr_lane_staged_kernel<1, 1, true>", "mmse_lr_lane_staged_kernel<2, 1, true>",
+        "mmse_lr_lane_staged_kernel<3, 1, true>", "mmse_lr_lane_staged_kernel<4, 1, true>",
+        "mmse_lr_lane_staged_kernel<5, 1, true>", "mmse_lr_lane_staged_kernel<6, 1, true>",
+        "mmse_lr_lane_staged_kernel<7, 1, true>", "mmse_lr_lane_staged_kernel<8, 1, true>"};
     static_assert(WCE_LR_STAGED_MINWG == 2 || WCE_LR_STAGED_MINWG <= 1, "lr_kernel_name spells MW = 2");
     const int r = rank < 1 ? 1 : (rank > LRL_RMAX ? LRL_RMAX : rank);
     switch (lr_form(rank, units)) {
     case LrForm::Direct: return lane[0][r];
     case LrForm::Staged64:
-    case LrForm::Staged: return lane[1][r];
-    case LrForm::StagedMW: return mw[r >= 8 ? 1 : 0];
-    case LrForm::Quad: return quad[(rank > 16 ? 16 : rank) - 9];
+    case LrForm::Staged: return lr_contig(taps) && lr_staged_threads(r) == 256 ? lanetq[r] : lane[1][r];
+    case LrForm::StagedMW: return mw[lr_contig(taps) ? 1 : 0][r >= 8 ? 1 : 0];
+    case LrForm::Quad: return quad[lr_contig(taps) ? 1 : 0][(rank > 16 ? 16 : rank) - 9];
     default: return k0 >= 0 && k0 <= 6 ? wave[lr_taps(taps) ? 1 : 0][k0] : "";
     }
 }
 
-int launch_mmse_lr(const State *st, int k0, int rank, bool taps, const SolveArgs &a, void *stream)
+int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs &a, void *stream)
 {
     if (a.n <= 0) return WCE_OK;
     const int64_t waves = a.split ? a.n * a.nblk : a.n;
@@ -3015,11 +3155,19 @@ int launch_mmse_lr(const State *st, int k0, int rank, bool taps, const SolveArgs
         const int64_t dw = (waves + fpw - 1) / fpw;
         const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((dw + 3) / 4)), bd(256);
         const dim3 gs4((unsigned)((waves + 255) / 256)), bs4(256);   // staged, 4-wave workgroups (WCE_LR_STAGED_LDS_P)
+        const bool tq = lr_contig(taps);
 #define WCE_LRL(RR)                                                                                         \
     case RR:                                                                                                \
         if constexpr (RR >= 7 && lr_staged_threads(RR) == 256 && WCE_LR_STAGED_MINWG > 1) {                \
             if (form == LrForm::StagedMW) {                                                                 \
-                hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
+                if (tq) hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG, true>), gs4, bs4, 0, s, st, a); \
+                else hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
+                break;                                                                                      \
+            }                                                                                               \
+        }                                                                                                   \
+        if constexpr (lr_staged_threads(RR) == 256) {                                                      \
+            if (form == LrForm::Staged && tq) {                                                             \
+                hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, 1, true>), gs4, bs4, 0, s, st, a);       \
                 break;                                                                                      \
             }                                                                                               \
         }                                                                                                   \
@@ -3036,16 +3184,17 @@ int launch_mmse_lr(const State *st, int k0, int rank, bool taps, const SolveArgs
     }
     if (form == LrForm::Quad) {
         const dim3 gq((unsigned)((waves + 15) / 16)), bq(256);
+        const bool tq = lr_contig(taps);
+#define WCE_LRQ(RR)                                                                              \
+    case RR:                                                                                     \
+        if (tq) hipLaunchKernelGGL((mmse_lr_quad_kernel<RR, true>), gq, bq, 0, s, st, a);        \
+        else hipLaunchKernelGGL((mmse_lr_quad_kernel<RR, false>), gq, bq, 0, s, st, a);          \
+        break;
         switch (rank) {
-        case 9: hipLaunchKernelGGL(mmse_lr_quad_kernel<9>, gq, bq, 0, s, st, a); break;
-        case 10: hipLaunchKernelGGL(mmse_lr_quad_kernel<10>, gq, bq, 0, s, st, a); break;
-        case 11: hipLaunchKernelGGL(mmse_lr_quad_kernel<11>, gq, bq, 0, s, st, a); break;
-        case 12: hipLaunchKernelGGL(mmse_lr_quad_kernel<12>, gq, bq, 0, s, st, a); break;
-        case 13: hipLaunchKernelGGL(mmse_lr_quad_kernel<13>, gq, bq, 0, s, st, a); break;
-        case 14: hipLaunchKernelGGL(mmse_lr_quad_kernel<14>, gq, bq, 0, s, st, a); break;
-        case 15: hipLaunchKernelGGL(mmse_lr_quad_kernel<15>, gq, bq, 0, s, st, a); break;
-        default: hipLaunchKernelGGL(mmse_lr_quad_kernel<16>, gq, bq, 0, s, st, a); break;
+            WCE_LRQ(9) WCE_LRQ(10) WCE_LRQ(11) WCE_LRQ(12) WCE_LRQ(13) WCE_LRQ(14) WCE_LRQ(15)
+            default: WCE_LRQ(16)
         }
+#undef WCE_LRQ
         return hip_status(hipGetLastError());
     }
     const dim3 g((unsigned)waves), b(64);

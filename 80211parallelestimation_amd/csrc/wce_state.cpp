@@ -379,6 +379,95 @@ constexpr long double kCovRankTol = 1.0L / (1ull << 46);
 // path: the dense Ryy solve loses ~eps cond(Ryy) there.
 constexpr long double kCovDenseKappa = 1e5L;
 
+// The 80-bit factor C = F Rhh F' = U U^H of a caller's Rhh, shared by the
+// state build and the constant-modulus operator (so both see the same U).
+//  - general Rhh: U = F V_r sqrt(Lambda_r) from the Jacobi eigendecomposition
+//    of its Hermitian part, columns in descending eigenvalue order;
+//  - diagonal Rhh (every off-diagonal entry exactly zero: a power-delay
+//    profile): column j is tap t_j's DFT column scaled by sqrt(p_t), from the
+//    EXACT DFT E[m] = exp(-2 pi i m / 53) (80-bit angle) -- the model the
+//    tap-domain kernels evaluate, within the reference F's own phase error
+//    (<= 6.1e-14) of F Rhh F' (DESIGN.md s2).  Columns in descending power,
+//    or by tap index when the kept taps are exactly 0..r-1 ('contig': the
+//    lane and quad kernels' tap form reads Q(t_i - t_j) at i - j).
+// Eigenvalues at or below kCovRankTol lambda_max count as zero.
+struct CovFactor {
+    int r = 0;
+    bool diag = false, contig = false;
+    long double lmax = 0.0L, lmin_kept = 0.0L;
+    std::vector<int> tap;              // diagonal: the tap of column j
+    std::vector<long double> lam;      // kept eigenvalues (of Rhh) by column
+    std::vector<cld> U;                // n x r, row-major
+    cld E[NSC];                        // the exact DFT (diagonal only)
+};
+static int cov_factor(const ldc *Fl, const wce_complex *Rhh, CovFactor &cf)
+{
+    const int n = NSC;
+    std::vector<ldc> Rh(n * n), V(n * n);
+    std::vector<long double> lam(n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            Rh[i * n + j].re = 0.5L * ((long double)Rhh[i * n + j].re + Rhh[j * n + i].re);
+            Rh[i * n + j].im = 0.5L * ((long double)Rhh[i * n + j].im - Rhh[j * n + i].im);
+        }
+    host_hermitian_eig(Rh.data(), n, lam.data(), V.data());
+    long double lmax = 0.0L, lmin = 0.0L;
+    for (int j = 0; j < n; j++) { lmax = std::max(lmax, lam[j]); lmin = std::min(lmin, lam[j]); }
+    // positive semidefinite: the Hermitian part's eigenvalues >= -1e-12 lambda_max
+    if (lmin < -1e-12L * lmax || (lmax == 0.0L && lmin < 0.0L)) return WCE_EINVAL;
+    cf.diag = true;
+    for (int i = 0; i < n && cf.diag; i++)
+        for (int j = 0; j < n; j++)
+            if (i != j && (Rhh[i * n + j].re != 0.0 || Rhh[i * n + j].im != 0.0)) { cf.diag = false; break; }
+    std::vector<int> ord(n);
+    for (int j = 0; j < n; j++) ord[j] = j;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lam[x] > lam[y]; });
+    int r = 0;
+    while (r < n && lam[ord[r]] > kCovRankTol * lmax && lmax > 0.0L) r++;
+    cf.r = r;
+    cf.lmax = lmax;
+    cf.contig = false;
+    if (cf.diag) {   // a diagonal input took no rotation: eigenvector ord[j] is e_{ord[j]}, lam = diag
+        int mx = -1;
+        for (int j = 0; j < r; j++) mx = std::max(mx, ord[j]);
+        cf.contig = r > 0 && mx == r - 1;
+        if (cf.contig) std::sort(ord.begin(), ord.begin() + r);
+    }
+    cf.tap.assign(r, 0);
+    cf.lam.assign(r, 0.0L);
+    cf.U.assign((size_t)n * r, mk(0, 0));
+    cf.lmin_kept = 0.0L;
+    for (int j = 0; j < r; j++) {
+        cf.lam[j] = lam[ord[j]];
+        cf.lmin_kept = j == 0 ? cf.lam[j] : std::min(cf.lmin_kept, cf.lam[j]);
+    }
+    if (cf.diag) {
+        const long double pi = acosl(-1.0L);
+        for (int m = 0; m < n; m++) {
+            const long double ang = -2.0L * pi * (long double)m / (long double)n;
+            cf.E[m] = mk(cosl(ang), sinl(ang));
+        }
+        for (int j = 0; j < r; j++) {
+            const int t = ord[j];
+            const long double sl = sqrtl(lam[t]);
+            cf.tap[j] = t;
+            for (int k = 0; k < n; k++) cf.U[(size_t)k * r + j] = cf.E[(k * t) % n] * mk(sl, 0.0L);
+        }
+    } else {
+        std::vector<cld> F(n * n);
+        for (int i = 0; i < n * n; i++) F[i] = from(Fl[i]);
+        for (int j = 0; j < r; j++) {
+            const long double sl = sqrtl(lam[ord[j]]);
+            for (int k = 0; k < n; k++) {
+                cld u = mk(0, 0);
+                for (int t = 0; t < n; t++) u = u + F[k * n + t] * from(V[t * n + ord[j]]);
+                cf.U[(size_t)k * r + j] = u * mk(sl, 0.0L);
+            }
+        }
+    }
+    return WCE_OK;
+}
+
 // WCE_MMSE_COV: the TEXTBOOK state with C = F Rhh F' from a caller's Rhh (80-bit products)
 int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
 {
@@ -400,86 +489,58 @@ int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
         F[i] = from(Fl[i]);
         R[i] = mk((long double)Rhh[i].re, (long double)Rhh[i].im);
     }
-    {   // ... and positive semidefinite: its Hermitian part's eigenvalues >= -1e-12 lambda_max
-        std::vector<ldc> Rh(n * n), V(n * n);
-        std::vector<long double> lam(n);
-        for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) {
-                Rh[i * n + j].re = 0.5L * ((long double)Rhh[i * n + j].re + Rhh[j * n + i].re);
-                Rh[i * n + j].im = 0.5L * ((long double)Rhh[i * n + j].im - Rhh[j * n + i].im);
-            }
-        host_hermitian_eig(Rh.data(), n, lam.data(), V.data());
-        long double lmax = 0.0L, lmin = 0.0L;
-        for (int j = 0; j < n; j++) { lmax = std::max(lmax, lam[j]); lmin = std::min(lmin, lam[j]); }
-        if (lmin < -1e-12L * lmax || (lmax == 0.0L && lmin < 0.0L)) return WCE_EINVAL;
-        // C = F Rhh F^H = U U^H, U = F V_r sqrt(Lambda_r), eigen-directions in
-        // descending order; the eigenvalues of C are 53 lambda (F^H F = 53 I)
-        std::vector<int> ord(n);
-        for (int j = 0; j < n; j++) ord[j] = j;
-        std::sort(ord.begin(), ord.end(), [&](int x, int y) { return lam[x] > lam[y]; });
-        int r = 0;
-        while (r < n && lam[ord[r]] > kCovRankTol * lmax && lmax > 0.0L) r++;
+    {
+        CovFactor cf;
+        if (cov_factor(Fl, Rhh, cf) != WCE_OK) return WCE_EINVAL;
+        const int r = cf.r;
         std::memset(st->U, 0, sizeof(st->U));
         std::memset(st->UT, 0, sizeof(st->UT));
         std::memset(st->Pk, 0, sizeof(st->Pk));
-        std::vector<cld> Ul((size_t)n * LRL_RMAX);   // U[k][j], j < LRL_RMAX, in 80 bits
-        for (int j = 0; j < r; j++) {
-            const long double sl = sqrtl(lam[ord[j]]);
+        for (int j = 0; j < r; j++)
             for (int k = 0; k < n; k++) {
-                cld u = mk(0, 0);
-                for (int t = 0; t < n; t++) u = u + F[k * n + t] * from(V[t * n + ord[j]]);
-                u = u * mk(sl, 0.0L);
+                const cld u = cf.U[(size_t)k * r + j];
                 st->U[2 * (k * CLD + j)] = st->UT[2 * (j * CLD + k)] = (double)__real__ u;
                 st->U[2 * (k * CLD + j) + 1] = st->UT[2 * (j * CLD + k) + 1] = (double)__imag__ u;
-                if (j < LRL_RMAX) Ul[(size_t)k * LRL_RMAX + j] = u;
             }
-        }
         if (r <= LRL_RMAX)   // P_k[i][j] = conj(U[k][i]) U[k][j], i >= j (mmse_lr_lane_kernel)
             for (int k = 0; k < n; k++)
                 for (int i = 0; i < r; i++)
                     for (int j = 0; j <= i; j++) {
-                        cld ui = Ul[(size_t)k * LRL_RMAX + i];
+                        cld ui = cf.U[(size_t)k * r + i];
                         __imag__ ui = -__imag__ ui;
-                        const cld v = ui * Ul[(size_t)k * LRL_RMAX + j];
+                        const cld v = ui * cf.U[(size_t)k * r + j];
                         const int e = (k * LRL_NP + i * (i + 1) / 2 + j) * 2;
                         st->Pk[e] = (double)__real__ v;
                         st->Pk[e + 1] = i == j ? 0.0 : (double)__imag__ v;
                     }
-        // a diagonal Rhh (every off-diagonal entry exactly zero): the tap-domain
-        // tables (State::cov_taps).  The Jacobi sweep took no rotation, so column
-        // j of U is the DFT column of tap ord[j]; the kernels evaluate it from
-        // the exact DFT E[m] = exp(-2 pi i m / 53), rounded once from 80 bits.
-        bool diag = true;
-        for (int i = 0; i < n && diag; i++)
-            for (int j = 0; j < n; j++)
-                if (i != j && (Rhh[i * n + j].re != 0.0 || Rhh[i * n + j].im != 0.0)) { diag = false; break; }
+        // a diagonal Rhh: the tap-domain tables (State::cov_taps)
         st->cov_taps = 0;
+        st->taps_contig = 0;
         std::memset(st->tap_of, 0, sizeof(st->tap_of));
         std::memset(st->col_s, 0, sizeof(st->col_s));
         std::memset(st->tap_s, 0, sizeof(st->tap_s));
         std::memset(st->dft, 0, sizeof(st->dft));
         for (int t = 0; t < NPAD; t++) st->col_of[t] = -1;
-        if (diag) {
-            const long double pi = acosl(-1.0L);
+        if (cf.diag) {
             for (int m = 0; m < n; m++) {
-                const long double ang = -2.0L * pi * (long double)m / (long double)n;
-                st->dft[2 * m] = (double)cosl(ang);
-                st->dft[2 * m + 1] = (double)sinl(ang);
+                st->dft[2 * m] = (double)__real__ cf.E[m];
+                st->dft[2 * m + 1] = (double)__imag__ cf.E[m];
             }
             for (int j = 0; j < r; j++) {
-                const int t = ord[j];
-                const double sl = (double)sqrtl(lam[t]);
+                const int t = cf.tap[j];
+                const double sl = (double)sqrtl(cf.lam[j]);
                 st->tap_of[j] = t;
                 st->col_of[t] = j;
                 st->col_s[j] = sl;
                 st->tap_s[t] = sl;
             }
             st->cov_taps = 1;
+            st->taps_contig = cf.contig ? 1 : 0;
         }
         st->cov_rank = r;
-        st->cov_lmax = (double)(n * lmax);
-        st->cov_lmin = r ? (double)(n * lam[ord[r - 1]]) : 0.0;
-        const bool dense = r == n && lam[ord[0]] <= kCovDenseKappa * lam[ord[r - 1]];
+        st->cov_lmax = (double)(n * cf.lmax);
+        st->cov_lmin = r ? (double)(n * cf.lmin_kept) : 0.0;
+        const bool dense = r == n && cf.lmax <= kCovDenseKappa * cf.lmin_kept;
         st->cov_k0 = dense ? -1 : std::min((n - r) / 8, COV_K0_MAX);
     }
     for (int r = 0; r < n; r++)
@@ -523,34 +584,13 @@ int host_build_cm(State *st, const ldc *Fl, const wce_complex *Rhh, const wce_co
         // the kernel's |x|^2, bit for bit: fma(re, re, im * im)
         p[k] = ((st->xmask >> k) & 1ull) ? std::fma(x_ref[k].re, x_ref[k].re, x_ref[k].im * x_ref[k].im) : 0.0;
     }
-    // U (80 bits) from the Hermitian part of Rhh, exactly as host_apply_cov keeps it
-    std::vector<ldc> Rh(n * n), V(n * n);
-    std::vector<long double> lam(n);
-    for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) {
-            Rh[i * n + j].re = 0.5L * ((long double)Rhh[i * n + j].re + Rhh[j * n + i].re);
-            Rh[i * n + j].im = 0.5L * ((long double)Rhh[i * n + j].im - Rhh[j * n + i].im);
-        }
-    host_hermitian_eig(Rh.data(), n, lam.data(), V.data());
-    long double lmax = 0.0L;
-    for (int j = 0; j < n; j++) lmax = std::max(lmax, lam[j]);
-    std::vector<int> ord(n);
-    for (int j = 0; j < n; j++) ord[j] = j;
-    std::sort(ord.begin(), ord.end(), [&](int x, int y) { return lam[x] > lam[y]; });
-    int r = 0;
-    while (r < n && lam[ord[r]] > kCovRankTol * lmax && lmax > 0.0L) r++;
+    // U (80 bits), exactly as host_apply_cov keeps it
+    CovFactor cf;
+    if (cov_factor(Fl, Rhh, cf) != WCE_OK) return WCE_EINVAL;
+    const int r = cf.r;
     if (r != st->cov_rank) return WCE_EINVAL;   // not the Rhh this state was built from
     if (r == 0) { st->cm_on = 1; std::memcpy(st->pcm, p, sizeof(p)); return WCE_OK; }   // C = 0: K = 0
-    std::vector<cld> F(n * n), U((size_t)n * r);
-    for (int i = 0; i < n * n; i++) F[i] = from(Fl[i]);
-    for (int j = 0; j < r; j++) {
-        const long double sl = sqrtl(lam[ord[j]]);
-        for (int k = 0; k < n; k++) {
-            cld u = mk(0, 0);
-            for (int t = 0; t < n; t++) u = u + F[k * n + t] * from(V[t * n + ord[j]]);
-            U[(size_t)k * r + j] = u * mk(sl, 0.0L);
-        }
-    }
+    const std::vector<cld> &U = cf.U;
     // G = a U^H P U + b I
     std::vector<ldc> G((size_t)r * r), Q((size_t)r * r);
     std::vector<long double> d(r);

@@ -1059,11 +1059,10 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
                 leg.update({"wave_kernel": c.lr_kernel(B), "wave_kernel_ms_per_step": tw})
             finally:
                 assert lib.wce_debug_set_variant(3, 0) == 0
-        if lr and r > 16:
-            # the wave kernel's tap-domain Gram (diagonal Rhh, round 4) against the
-            # product Gram on the same ctx (variant 5); FP64-VALU bound, priced at
-            # the tap form's algorithmic flops: r x r Cholesky +
-            # triangular solves + the Q / D / read-out DFTs (20 N^2)
+        if lr:
+            # the tap-domain forms (a diagonal Rhh, round 4: the Toeplitz Gram of the
+            # lane / quad kernels, the DFT Gram of the wave kernel) against the
+            # product Gram on the same ctx (variant 5)
             assert lib.wce_debug_set_variant(3, 5) == 0
             try:
                 for _ in range(2):
@@ -1073,6 +1072,9 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
                             "taps_speedup": tp / t})
             finally:
                 assert lib.wce_debug_set_variant(3, 0) == 0
+        if lr and r > 16:
+            # FP64-VALU bound, priced at the tap form's algorithmic flops (DESIGN.md
+            # s2): r x r Cholesky + triangular solves + the Q / D / read-out DFTs (20 N^2)
             fl = flop_lr_taps(r)
             ach = fl * B / (t * 1e-3) / 1e12
             kw, wsrc = pmc_leg("lowrank%d" % L, B, N * 16.0 * B, waves=B)

@@ -48,9 +48,9 @@ def _run(wce, ctx, fr, mask, f32=False):
     ("TEXTBOOK", "LT_LS|PS_LINEAR", False, "C"),     # ls_elem_kernel
     ("TEXTBOOK", "ALL", True, "C"),                  # fused solve + LS family + equalization, fp32 outputs
     ("COV", "PS_MMSE", False, "C"),                  # dense solve + MFMA apply
-    ("COV8", "PS_MMSE", False, "C"),                 # 8-tap PDP: one frame per lane, mmse_lr_lane_staged_kernel<8>
+    ("COV8", "PS_MMSE", False, "C"),                 # 8-tap PDP: one frame per lane, mmse_lr_lane_staged_kernel<8, 1, true>
     ("COV8", "PS_MMSE", False, "MATLAB"),            # the same, split per-block solves + block mean
-    ("COV12", "PS_MMSE", False, "C"),                # 12 taps: 16 lanes per frame, mmse_lr_quad_kernel<12>
+    ("COV12", "PS_MMSE", False, "C"),                # 12 taps: 16 lanes per frame, mmse_lr_quad_kernel<12, true>
     ("COV24", "PS_MMSE", False, "C"),                # 24 taps: one frame per wave, mmse_lr_kernel<3, true>
     ("COV24", "PS_MMSE", False, "MATLAB"),           # the same, split per-block solves
     ("REF", "ALL", True, "C"),                       # ref_ls_elem_kernel, fp32 LS / eq
@@ -72,7 +72,7 @@ def test_64bit_frame_indexing(layouts, mode, mask, f32, sem):
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4)
         assert ctx.cov_info()[:2] == (L, True)
         units = B * (4 if sem == "MATLAB" else 1)
-        assert ctx.lr_kernel(units) == {8: "mmse_lr_lane_staged_kernel<8>", 12: "mmse_lr_quad_kernel<12>",
+        assert ctx.lr_kernel(units) == {8: "mmse_lr_lane_staged_kernel<8, 1, true>", 12: "mmse_lr_quad_kernel<12, true>",
                                         24: "mmse_lr_kernel<3, true>"}[L]
     else:
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], getattr(wce, "MMSE_" + mode))

@@ -84,7 +84,7 @@ def c_ld(oracle, R):
 
 # (taps, decay, per-frame kernel): quad (rank 16), Gram wave kernel (24, K0 = 3;
 # a full-rank spectrum wider than 1e5, K0 = 0), dense solve + H = C W
-PROFILES = [(16, 0.5, "mmse_lr_quad_kernel<16>"), (24, 0.3, "mmse_lr_kernel<3, true>"), (53, 0.5, "mmse_lr_kernel<0, true>"),
+PROFILES = [(16, 0.5, "mmse_lr_quad_kernel<16, true>"), (24, 0.3, "mmse_lr_kernel<3, true>"), (53, 0.5, "mmse_lr_kernel<0, true>"),
             (53, 0.12, "")]
 
 

@@ -323,3 +323,25 @@ def test_taps_algebra_vs_long_double(wce, oracle, inp, L, decay):
         exp = oracle.mmse_unified(C, np.ones(N, np.uint8), 1.0, ow2, tx, rx)
         worst = max(worst, float(normrel(got, exp)))
     assert worst < 1e-11, worst
+
+
+def test_taps_contig_orders_columns_by_tap(wce, inp):
+    """A PDP whose kept taps are exactly 0..L-1 (any powers, not necessarily
+    decreasing) orders U's columns by tap index (State::taps_contig: the lane and
+    quad kernels' Toeplitz Gram reads Q(i - j)); scattered taps keep the
+    descending-power order and taps_contig = 0."""
+    L = 6
+    p = np.array([0.5, 1.0, 0.25, 0.8, 0.1, 0.3]) * 1e-5
+    R = np.zeros((N, N), np.complex128)
+    R[np.arange(L), np.arange(L)] = p
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    on, tap_of, col_of, col_s, tap_s, dft = taps_tables(blob)
+    contig = int(blob[len(blob) - TAPS_TAIL + 4:len(blob) - TAPS_TAIL + 8].view(np.int32)[0])
+    assert on == 1 and contig == 1
+    assert np.array_equal(tap_of[:L], np.arange(L)) and np.allclose(col_s[:L], np.sqrt(p), rtol=1e-15, atol=0)
+    R2 = np.zeros((N, N), np.complex128)
+    R2[[0, 2, 5], [0, 2, 5]] = [1e-5, 3e-5, 2e-5]
+    blob2 = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R2)
+    on2, tap2, _, s2, _, _ = taps_tables(blob2)
+    contig2 = int(blob2[len(blob2) - TAPS_TAIL + 4:len(blob2) - TAPS_TAIL + 8].view(np.int32)[0])
+    assert on2 == 1 and contig2 == 0 and list(tap2[:3]) == [2, 5, 0]

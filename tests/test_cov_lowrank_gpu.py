@@ -225,29 +225,33 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
     QPSK frames against the long double solve, and against the wave-per-frame
     Gram kernel (variant WCE_VARIANT_LR = 1) on the same frames, C and MATLAB
     semantics, 515 frames (a partial last wave of lanes).  The product at this
-    size is the staged one-workgroup-per-CU build (variant 3 forces it: bit
-    for bit); the two-workgroups build (variant 4; ranks 7, 8) computes the
-    same sums (bit for bit); the direct form (variant 2: per-lane loads, no
-    LDS staging) is the independent check of the staging (to rounding)."""
+    size is the staged one-workgroup-per-CU build in the Toeplitz form (a PDP
+    with taps 0..L-1: Gamma = S Q S, round 4; variant 3 forces the same build:
+    bit for bit); the two-workgroups build (variant 4; ranks 7, 8) computes the
+    same sums (bit for bit); variant 5 runs the product Gram (sum_k |x_k|^2 P_k)
+    in the same staged build, and the direct form (variant 2: per-lane loads,
+    no LDS staging, product Gram) is the independent check of the staging (to
+    rounding)."""
     inp = golden["inputs"]
     lib = gpu_wce.load()
     R = pdp_rhh(L, 0.4)
     ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
     assert ctx.cov_info()[:2] == (L, True)
     B = 515
-    assert ctx.lr_kernel(B) == f"mmse_lr_lane_staged_kernel<{L}>"
+    assert ctx.lr_kernel(B) == f"mmse_lr_lane_staged_kernel<{L}, 1, true>"
     tx, rx = synth(ctx, gpu_wce, B, seed=0x1A0 + L)
     rng = np.random.default_rng(L)
     txq = constellation(rng, "qpsk", tx.shape)
     txq[:, :, 26] = 0
     rxq = channel_frames(rng, txq, inp["ow2"])
     C = c_ld(oracle, R)
-    names = {2: f"mmse_lr_lane_kernel<{L}>", 3: f"mmse_lr_lane_staged_kernel<{L}>",
-             4: f"mmse_lr_lane_staged_kernel<{L}, 2>" if L >= 7 else f"mmse_lr_lane_staged_kernel<{L}>"}
+    names = {2: f"mmse_lr_lane_kernel<{L}>", 3: f"mmse_lr_lane_staged_kernel<{L}, 1, true>",
+             4: f"mmse_lr_lane_staged_kernel<{L}, 2, true>" if L >= 7 else f"mmse_lr_lane_staged_kernel<{L}, 1, true>",
+             5: f"mmse_lr_lane_staged_kernel<{L}>"}
     try:
         for t, r in ((tx, rx), (txq, rxq)):
             got = {}
-            for v in (0, 1, 2, 3, 4):
+            for v in (0, 1, 2, 3, 4, 5):
                 assert lib.wce_debug_set_variant(3, v) == 0
                 if v in names:
                     assert ctx.lr_kernel(B) == names[v]
@@ -255,10 +259,13 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
                 got[v, "m"] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE, semantics=gpu_wce.SEM_MATLAB)["ps_mmse"]
             for v in (3, 4):
                 assert np.array_equal(got[v], got[0]) and np.array_equal(got[v, "m"], got[0, "m"]), v
-            # direct vs LDS-staged form: same sums in the same order (the compiler may
-            # contract a product into an FMA differently in the two instantiations)
-            dd = max(normrel(got[0], got[2]).max(), normrel(got[0, "m"], got[2, "m"]).max())
+            # direct vs LDS-staged form of the product Gram: same sums in the same order (the
+            # compiler may contract a product into an FMA differently in the two instantiations)
+            dd = max(normrel(got[5], got[2]).max(), normrel(got[5, "m"], got[2, "m"]).max())
             assert dd < 1e-12, dd
+            # Toeplitz vs product Gram: the same Gamma summed two ways
+            dt = max(normrel(got[0], got[5]).max(), normrel(got[0, "m"], got[5, "m"]).max())
+            assert dt < 1e-11, dt
             sel = np.r_[0:30, B - 10:B]
             err = normrel(got[0][sel], solve_ld(oracle, C, t[sel, 0], r[sel, 0], inp["ow2"]))
             assert err.max() < TOL, err.max()
@@ -269,7 +276,7 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
             # carries the most rounding, ~1e-11 from the long double solve, r03 probe)
             d = max(normrel(got[0], got[1]).max(), normrel(got[0, "m"], got[1, "m"]).max())
             print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, lane vs wave kernel {d:.2e}, "
-                  f"direct vs staged {dd:.2e}")
+                  f"direct vs staged {dd:.2e}, Toeplitz vs product {dt:.2e}")
             assert d < TOL
     finally:
         assert lib.wce_debug_set_variant(3, 0) == 0
@@ -280,7 +287,8 @@ def test_lane_kernel_every_small_rank(gpu_wce, golden, oracle, L):
 def test_lane_two_workgroup_build_at_size(gpu_wce, golden, oracle, L, matlab):
     """Ranks 7 and 8 past one 64-unit wave per SIMD (> 65,536 (frame, block)
     units on 256 CUs) run the two-workgroups-per-CU build
-    mmse_lr_lane_staged_kernel<R, 2> (launch_mmse_lr; rank 8 spills there):
+    mmse_lr_lane_staged_kernel<R, 2, true> (launch_mmse_lr; the product
+    Gram's build, variant 5, spills at rank 8):
     70,001 frames in C semantics, 17,001 frames = 68,004 units in MATLAB split
     mode.  The first half of the batch is BPSK, the second QPSK (the
     correction pass).  Non-finite scan clean; the first, the last and 30
@@ -311,13 +319,17 @@ def test_lane_two_workgroup_build_at_size(gpu_wce, golden, oracle, L, matlab):
         return H
 
     try:
-        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}, 2>"
+        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}, 2, true>"
         H = run(0)
         assert ctx.nonfinite_scan(H, B)[1] == 0
         got = H.numpy()
         assert lib.wce_debug_set_variant(3, 3) == 0
-        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}>"
+        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}, 1, true>"
         assert np.array_equal(run(3).numpy(), got)
+        assert lib.wce_debug_set_variant(3, 5) == 0              # the product Gram's MW = 2 build
+        assert ctx.lr_kernel(units) == f"mmse_lr_lane_staged_kernel<{L}, 2>"
+        prod = run(5).numpy()
+        assert normrel(prod, got).max() < 1e-11
     finally:
         assert lib.wce_debug_set_variant(3, 0) == 0
     C = c_ld(oracle, R)
@@ -334,10 +346,12 @@ def test_lane_two_workgroup_build_at_size(gpu_wce, golden, oracle, L, matlab):
 
 @pytest.mark.parametrize("L", [9, 10, 12, 13, 16])
 def test_quad_kernel_mid_ranks(gpu_wce, golden, oracle, L):
-    """Ranks 9..16 run 16 lanes per frame (mmse_lr_quad_kernel): BPSK and QPSK
-    frames against the long double solve and against the wave-per-frame Gram
-    kernel (variant WCE_VARIANT_LR = 1), C and MATLAB semantics, 515 frames
-    (a partial last row group of the last wave)."""
+    """Ranks 9..16 run 16 lanes per frame (mmse_lr_quad_kernel; a PDP with taps
+    0..L-1 in the Toeplitz form, round 4): BPSK and 16-QAM frames against the
+    long double solve, against the wave-per-frame Gram kernel (variant
+    WCE_VARIANT_LR = 1) and against the quad kernel's product Gram (variant
+    5), C and MATLAB semantics, 515 frames (a partial last row group of the
+    last wave)."""
     inp = golden["inputs"]
     lib = gpu_wce.load()
     R = pdp_rhh(L, 0.3)
@@ -353,16 +367,21 @@ def test_quad_kernel_mid_ranks(gpu_wce, golden, oracle, L):
     try:
         for t, r in ((tx, rx), (txq, rxq)):
             got = {}
-            for v in (0, 1):
+            for v in (0, 1, 5):
                 assert lib.wce_debug_set_variant(3, v) == 0
+                if v != 1:
+                    assert ctx.lr_kernel(B) == f"mmse_lr_quad_kernel<{L}{', true' if v == 0 else ''}>"
                 got[v] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE)["ps_mmse"]
                 got[v, "m"] = ctx.estimate_host(t, r, mask=gpu_wce.PS_MMSE, semantics=gpu_wce.SEM_MATLAB)["ps_mmse"]
+            dp = max(normrel(got[0], got[5]).max(), normrel(got[0, "m"], got[5, "m"]).max())
+            assert dp < 1e-11, dp
             sel = np.r_[0:30, B - 10:B]
             err = normrel(got[0][sel], solve_ld(oracle, C, t[sel, 0], r[sel, 0], inp["ow2"]))
             per = [solve_ld(oracle, C, t[sel, b], r[sel, b], inp["ow2"]) for b in range(4)]
             errm = normrel(got[0, "m"][sel], (((per[0] + per[1]) + per[2]) + per[3]) / 4)
             d = max(normrel(got[0], got[1]).max(), normrel(got[0, "m"], got[1, "m"]).max())
-            print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, quad vs wave kernel {d:.2e}")
+            print(f"\nrank {L}: vs long double {max(err.max(), errm.max()):.2e}, quad vs wave kernel {d:.2e}, "
+                  f"Toeplitz vs product {dp:.2e}")
             assert err.max() < TOL and errm.max() < TOL and d < TOL
     finally:
         assert lib.wce_debug_set_variant(3, 0) == 0

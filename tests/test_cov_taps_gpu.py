@@ -117,3 +117,26 @@ def test_non_diagonal_rhh_keeps_product_gram(gpu_wce, golden):
     R[2, 5] = R[5, 2] = 1e-9
     ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
     assert ctx.lr_kernel(4096) == "mmse_lr_kernel<3>"
+
+
+@pytest.mark.parametrize("L", [8, 12])
+def test_scattered_taps_keep_product_lane_and_quad(gpu_wce, golden, oracle, L):
+    """A PDP whose kept taps are not 0..L-1 has no Toeplitz Gram at i - j: the
+    lane / quad kernels run their product Gram (State::taps_contig = 0), within
+    1e-10 of the long double solve; the contiguous profile of the same powers
+    runs the Toeplitz form."""
+    wce = gpu_wce
+    inp = golden["inputs"]
+    perm = np.random.default_rng(40 + L).permutation(N)
+    R = pdp_rhh(L, 0.5, perm)
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    prod = "mmse_lr_lane_staged_kernel<8>" if L == 8 else "mmse_lr_quad_kernel<12>"
+    assert ctx.lr_kernel(4096) == prod
+    B = 300
+    tx, rx = synth(ctx, wce, B, seed=0x5C + L)
+    out = ctx.estimate_host(tx, rx, mask=wce.PS_MMSE)["ps_mmse"]
+    exp = solve_ld(oracle, c_ld(oracle, R), tx[:, 0], rx[:, 0], inp["ow2"])
+    err = normrel(out, exp)
+    assert err.max() < TOL, err.max()
+    ctc = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh(L, 0.5))
+    assert ctc.lr_kernel(4096) == ("mmse_lr_lane_staged_kernel<8, 1, true>" if L == 8 else "mmse_lr_quad_kernel<12, true>")
