@@ -34,6 +34,25 @@ rows = [
      f"{100 * cov['solve_frac_fp64_peak']:.0f}% of FP64 peak; MFMA `C·W` {ap['achieved_tflops']:.1f} TF algorithmic, "
      f"{ap.get('executed_tflops', 0):.1f} TF executed, pipe busy {100 * ap.get('mfma_busy_frac_pmc', 0):.0f}% by PMC of "
      f"same-size launches)"),
+]
+lr = d.get("cov_lowrank", {})
+if lr:
+    rows.append(("PS_MMSE, model covariance = a 4 / 8 / 16 / 24 / 53-tap power-delay profile (COV low-rank paths: "
+                 "Toeplitz / tap-domain Gram)",
+                 " / ".join(f"{lr[L]['frames_per_s']:.3g}" for L in ("L4", "L8", "L16", "L24", "L53") if L in lr)
+                 + " frames/s, ≤2.3e-13 from the long double solve (≤1.5e-11 at rank 1)"))
+    cm = lr.get("L53", {}).get("constant_modulus")
+    if cm:
+        rows.append(("the same, 53 taps, BPSK frames on the shared operator (`wce_ctx_set_modulus`)",
+                     f"{cm['frames_per_s']:.3g} frames/s ({cm['speedup_vs_per_frame']:.1f}× the per-frame solve)"))
+c5r = d.get("config5_ref", {})
+if c5r:
+    rows.append(("configs[4] in `main.c` semantics (REF + LS family + eq), 1,048,576 frames",
+                 f"{c5r['fp64']['frames_per_s']:.3g} frames/s fp64 ({c5r['fp64']['roofline']['achieved'] / 1000:.2f} TB/s); "
+                 f"{c5r['mixed_fp64_solve_fp32_ls']['frames_per_s']:.3g} with fp32 LS outputs; with each frame's PS_MMSE "
+                 f"on its own LT_LS (FRAME_COV, as main.c:37-53) {c5r['frame_cov_fp64']['frames_per_s']:.3g}"
+                 if "frame_cov_fp64" in c5r else ""))
+rows += [
     ("LT_LS + PS_Linear (config 2)",
      f"{l65['frames_per_s']:.2g} frames/s at 65,536 frames ({l65['achieved_GBs'] / 1000:.1f} TB/s algorithmic); "
      f"{ls['frames_per_s']:.2g} at 1,048,576 ({ls['achieved_GBs'] / 1000:.1f} TB/s algorithmic"
