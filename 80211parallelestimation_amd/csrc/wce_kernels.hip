@@ -1603,30 +1603,47 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, Solve
     }
 #endif
     wave_lds_sync();   // every lane's reads of u[1] / the pair tables are done
-    s.blk[lane] = Qd;
+    // The system is factorised in the scaled form M = S^-1 (a Gamma + b I) S^-1
+    // = a T + b S^-2 (T_ij = Q(t_i - t_j)), bordered by S^-1 beta = conj(D(t_j)):
+    // its solution is w = S t = the tap vector c of the read-out itself.  A
+    // diagonal scaling leaves Cholesky's backward error unchanged (van der
+    // Sluis; the dense path's scaled form, s5), and every element is a plain
+    // gather of a Q (pre-scaled by a) instead of a product of three factors.
+    // Padding columns j in [r, RMAX): pivot b, zero border -> w_j = 0.
+    s.blk[lane] = cscale(Qd, ac);
     s.z[lane] = Dd;
-    s.u[1][lane] = make_double2(st->col_s[lane], (double)st->tap_of[lane]);   // column j: {s_j, t_j}
+    int *tapl = reinterpret_cast<int *>(s.u[1]);   // column j -> its tap (256 B of u[1]) ...
+    double *bl = reinterpret_cast<double *>(tapl + 64);   // ... and M's diagonal term b / lambda_j (b past r)
+    const int r = st->cov_rank;
+    {
+        tapl[lane] = st->tap_of[lane];
+        const double sl = st->col_s[lane];
+        bl[lane] = lane < r ? bc / (sl * sl) : bc;
+    }
     wave_lds_sync();
 #pragma unroll
     for (int m = 0; m < NB; ++m) {
         const int j1 = p + 8 * m;
-        const double2 c1 = s.u[1][j1];
-        const int t1 = (int)c1.y;
+        const bool v1 = j1 < r;
+        const int t1 = tapl[j1];
+        const double d1 = bl[j1];
 #pragma unroll
         for (int n = 0; n <= m; ++n) {
             const int j2 = q + 8 * n;
-            const double2 c2 = s.u[1][j2];
-            const int t2 = (int)c2.y;
+            const bool v2 = j2 < r;
+            const int t2 = tapl[j2];
             int dd = t1 - t2;
             dd += dd < 0 ? NSC : 0;
             double2 e;
             if (j1 < RMAX && j2 < RMAX) {
-                e = cscale(s.blk[dd], ac * c1.x * c2.x);
-                e.x += j1 == j2 ? bc : 0.0;
+                e = s.blk[dd];
+                e = make_double2(v1 && v2 ? e.x : 0.0, v1 && v2 ? e.y : 0.0);
+                e.x += j1 == j2 ? d1 : 0.0;
             } else if (j1 == RMAX && j2 < RMAX) {
-                e = cscale(s.z[t2], c2.x);
+                e = s.z[t2];
+                e = make_double2(v2 ? e.x : 0.0, v2 ? e.y : 0.0);
             } else if (j2 == RMAX && j1 < RMAX) {
-                e = cscale(cconj(s.z[t1]), ac * c1.x);
+                e = cscale(cconj(s.z[t1]), v1 ? ac : 0.0);
             } else {
                 e = make_double2(0.0, 0.0);
             }
@@ -1670,12 +1687,12 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     for (int bb = 0; bb < RB; ++bb) P[bb] = brow ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
     back_blocks_from<RB - 1, K0>(A, P, rq, s, p, q, lane);
     wave_lds_sync();
-    // c_t = s_t t_col(t) on lane t (t_j = z[8 K0 + j]); E back into u[0]
+    // c_t = s_t t_col(t) = w_col(t) on lane t (w_j = z[8 K0 + j], the scaled system's solution); E back into u[0]
     const int col = act ? st->col_of[lane] : -1;
     const double ts = st->tap_s[lane];
     {
-        const double2 tj = s.z[8 * K0 + (col < 0 ? 0 : col)];
-        s.u[1][lane] = col < 0 ? make_double2(0.0, 0.0) : cscale(tj, ts);
+        const double2 wj = s.z[8 * K0 + (col < 0 ? 0 : col)];
+        s.u[1][lane] = col < 0 ? make_double2(0.0, 0.0) : wj;
         s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
     }
     wave_lds_sync();
