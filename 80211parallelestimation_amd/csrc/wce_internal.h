@@ -14,7 +14,7 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
-constexpr int32_t STATE_LAYOUT = 6;   // State layout version: bump with every change to struct State
+constexpr int32_t STATE_LAYOUT = 7;   // State layout version: bump with every change to struct State
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
@@ -71,7 +71,9 @@ struct State {
     double pcm[NPAD];
     int32_t cm_on;
     int32_t cm_reserved[3];
-    // WCE_MMSE_COV with a diagonal Rhh -- a power-delay profile (round 4): C's
+    // WCE_MMSE_COV with a diagonal Rhh -- a power-delay profile (round 4): C
+    // itself is then the exact-DFT circulant C_ij = sum_t p_t E[(i - j) t] (the
+    // model every COV path of such a state evaluates: State::C, U, K).  C's
     // eigen-directions are DFT columns, U[:, j] = s_j F[:, t_j], and the Gram
     // matrix U^H P U (P = diag |x|^2) is s_i s_j Q(t_i - t_j) with Q the DFT of
     // |x|^2: the tap-domain form of the Gram path (mmse_lr_kernel<K0, true>)

@@ -549,8 +549,17 @@ int host_apply_cov(State *st, const ldc *Fl, const wce_complex *Rhh)
             __imag__ v = -__imag__ v;
             FH[r * n + c] = v;   // F' (conjugate transpose)
         }
-    mat_mul(R.data(), n, n, FH.data(), n, t1.data());
-    mat_mul(F.data(), n, n, t1.data(), n, C.data());
+    if (st->cov_taps) {   // diagonal Rhh: C = F_exact diag(p) F_exact^H, the circulant the tap-domain U factors
+        CovFactor cf;
+        if (cov_factor(Fl, Rhh, cf) != WCE_OK) return WCE_EINVAL;
+        std::vector<cld> c(n, mk(0, 0));
+        for (int d = 0; d < n; d++)
+            for (int t = 0; t < n; t++) c[d] = c[d] + cf.E[(d * t) % n] * mk((long double)Rhh[t * n + t].re, 0.0L);
+        for (int i = 0; i < n * n; i++) C[i] = c[((i / n) - (i % n) + n) % n];
+    } else {
+        mat_mul(R.data(), n, n, FH.data(), n, t1.data());
+        mat_mul(F.data(), n, n, t1.data(), n, C.data());
+    }
     for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) {
             st->C[2 * (i * CLD + j)] = (double)__real__ C[i * n + j];

@@ -116,7 +116,7 @@ def test_no_device_fails_loudly(wce):
 
 
 CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16     # State's constant-modulus operator Kcm, pattern pcm, cm_on (+ 12 B)
-TAPS_TAIL = 16 + 2 * 64 * 4 + 2 * 64 * 8 + 64 * 16   # cov_taps (+ 12 B), tap_of, col_of, col_s, tap_s, dft
+TAPS_TAIL = 16 + 2 * 64 * 4 + 2 * 64 * 8 + 64 * 16   # cov_taps, taps_contig (+ 8 B), tap_of, col_of, col_s, tap_s, dft
 
 
 def _pdp_cov(L=53, decay=0.12):

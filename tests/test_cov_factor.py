@@ -9,7 +9,7 @@ from oracle_py import N, normrel
 
 
 CM_TAIL = 64 * 64 * 16 + 64 * 8 + 16               # State: Kcm, pcm, cm_on (+ 12 B)
-TAPS_TAIL = 16 + 2 * 64 * 4 + 2 * 64 * 8 + 64 * 16   # State: cov_taps (+ 12 B), tap_of, col_of, col_s, tap_s, dft
+TAPS_TAIL = 16 + 2 * 64 * 4 + 2 * 64 * 8 + 64 * 16   # State: cov_taps, taps_contig (+ 8 B), tap_of, col_of, col_s, tap_s, dft
 
 
 def taps_tables(blob):
@@ -20,7 +20,7 @@ def taps_tables(blob):
     col_of = t[272:528].view(np.int32)
     col_s = t[528:1040].view(np.float64)
     tap_s = t[1040:1552].view(np.float64)
-    dft = t[1552:].view(np.complex128)
+    dft = t[1552:2576].view(np.complex128)
     return on, tap_of, col_of, col_s, tap_s, dft
 
 
@@ -345,3 +345,21 @@ def test_taps_contig_orders_columns_by_tap(wce, inp):
     on2, tap2, _, s2, _, _ = taps_tables(blob2)
     contig2 = int(blob2[len(blob2) - TAPS_TAIL + 4:len(blob2) - TAPS_TAIL + 8].view(np.int32)[0])
     assert on2 == 1 and contig2 == 0 and list(tap2[:3]) == [2, 5, 0]
+
+
+@pytest.mark.parametrize("L,decay", [(53, 0.12), (53, 0.5), (6, 0.5)])
+def test_circulant_C_for_diagonal_rhh(wce, oracle, inp, L, decay):
+    """A diagonal Rhh's State::C is the exact-DFT circulant C_ij = c((i - j) mod 53)
+    -- the model U (and the constant-modulus K) of the same state factor: within
+    the reference F's own phase error of F Rhh F^H in long double, equal to U U^H."""
+    R = pdp_rhh(L, decay)
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    C = blob[:64 * 64 * 16].view(np.complex128).reshape(64, 64)[:N, :N]
+    k = np.arange(N)
+    assert np.array_equal(C, C[(k[:, None] - k[None, :]) % N, 0])
+    F = oracle.fmatrix()
+    Cref = np.asarray(F @ oracle._ld(R) @ F.conj().T, np.complex128)
+    assert np.max(np.abs(C - Cref)) < 2e-13 * np.max(np.abs(Cref))
+    U, r, _, _, _ = wce.cov_factor(blob)
+    if r == N or L < N:
+        assert np.max(np.abs(U @ U.conj().T - C)) < 4e-15 * np.max(np.abs(C))
