@@ -538,7 +538,12 @@ constexpr int KSTEPS = 14;   // 4-deep MFMA k-steps over 56 >= 53 subcarriers
 
 constexpr int CVS = 9;    // row stride (complex) of the panel transpose buffer
 
-struct SolveLds {
+// R0 > 0 (the Gram path at K0 >= 2, rows 8 K0 .. 55 only): the panel transpose
+// buffer holds rows R0 .. 55, so the wave needs less LDS and more waves fit a CU.
+template <int R0>
+struct SolveLdsT {
+    static constexpr int ROW0 = R0;
+    __device__ int ci(int row, int c) const { return (row - R0) * CVS + c; }   // conv element (row, c)
     double2 u[2][64];     // pivot column k (unscaled A[:, k]) ping-pong
     double2 x[64];        // masked tx of the frame (diagonal of X), 0 past 53
     double2 rx[64];
@@ -548,7 +553,7 @@ struct SolveLds {
             double2 z[64];    // solution
             double rd[64];    // r_k = 1 / d_k, 0 past 52
         };
-        double2 conv[56 * CVS];   // row-per-lane panels: block column -> rows (to_rows)
+        double2 conv[(56 - R0) * CVS];   // row-per-lane panels: block column -> rows (to_rows)
         struct {                  // the tap-domain Gram's DFT pair tables (lr_dft53p), past blk / z / rd
             double2 pad_bzr[160];
             double2 pa[32], pb[32];   // c_k + c_{53-k}, c_k - c_{53-k}, k = 1..26 (complex vectors)
@@ -556,12 +561,12 @@ struct SolveLds {
         } tp;
     };
 };
+using SolveLds = SolveLdsT<0>;
 static_assert(sizeof(SolveLds::tp.pad_bzr) == 2 * sizeof(SolveLds::blk) + sizeof(SolveLds::rd),
               "the tap pair tables start past blk / z / rd");
-// conv element (row, c) at row * 9 + c: the odd row stride keeps both the
-// block-cyclic stores and the row reads bank-conflict free (an XOR swizzle of
-// an unpadded buffer measured 1% slower: address VALU).
-__device__ __forceinline__ int conv_idx(int row, int c) { return row * CVS + c; }
+// conv element (row, c) at (row - R0) * 9 + c (SolveLdsT::ci): the odd row
+// stride keeps both the block-cyclic stores and the row reads bank-conflict
+// free (an XOR swizzle of an unpadded buffer measured 1% slower: address VALU).
 
 
 // 1/sqrt(d) from v_rsq_f64 (relative error ~2^-24).  One third-order
@@ -681,16 +686,17 @@ __device__ __forceinline__ double rsq_uniform(double d)
 // last step block column KB+1 is updated, written once to LDS by all lanes and
 // read back transposed (6 - KB stores + 8 reads per panel).
 // ---------------------------------------------------------------------
-template <int KB>
-__device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)[8], SolveLds &s, int p, int q,
+template <int KB, typename L = SolveLds>
+__device__ __forceinline__ void to_rows(const double2 (&A)[RB][RB], double2 (&P)[8], L &s, int p, int q,
                                         int lane)
 {
 #pragma unroll
-    for (int aa = KB; aa < RB; ++aa) s.conv[conv_idx(p + 8 * aa, q)] = A[aa][KB];
+    for (int aa = KB; aa < RB; ++aa) s.conv[s.ci(p + 8 * aa, q)] = A[aa][KB];
     wave_lds_sync();
-    const int l = lane < 56 ? lane : 55;   // lanes 56..63 carry a copy of row 55 (never read)
+    int l = lane < 56 ? lane : 55;   // lanes 56..63 carry a copy of row 55 (never read)
+    l = l < L::ROW0 ? L::ROW0 : l;   // (R0 > 0: rows above the system read row R0; never read either)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) P[c] = s.conv[conv_idx(l, c)];
+    for (int c = 0; c < 8; ++c) P[c] = s.conv[s.ci(l, c)];
 }
 
 // Back-substitution L' z = w (unit diagonal), rows 8*BLK .. 8*BLK+7.  The
@@ -722,9 +728,9 @@ __device__ __forceinline__ double2 bcast_row_lane(double2 w, int t)
     }
 }
 
-template <int BLK>
+template <int BLK, typename L = SolveLds>
 __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
-                                           SolveLds &s, int p, int q, int lane)
+                                           L &s, int p, int q, int lane)
 {
     constexpr int NROW = (BLK == RB - 1) ? (NSC - 8 * (RB - 1)) : 8;
     // w_j = r_j * (conj(u_53,j) - sum_{i solved} conj(u_ij) z_i),  j = 8*BLK + q
@@ -901,23 +907,24 @@ constexpr uint64_t lanes_q(int qq) { return 0x0101010101010101ull << qq; }   // 
 // Column c of a finished panel goes to conv as soon as it is final (after its
 // own step's in-panel updates, stash_col), so the panel's registers free up
 // column by column; to_blocks then only reads the block column back.
-__device__ __forceinline__ void stash_col(SolveLds &s, int lane, int c, double2 v)
+template <typename L = SolveLds>
+__device__ __forceinline__ void stash_col(L &s, int lane, int c, double2 v)
 {
-    if (lane < 56) s.conv[conv_idx(lane, c)] = v;
+    if (lane < 56 && lane >= L::ROW0) s.conv[s.ci(lane, c)] = v;
 }
-template <int KB>
-__device__ __forceinline__ void to_blocks(double2 (&A)[RB][RB], const double2 (&P)[8], SolveLds &s, int p, int q,
+template <int KB, typename L = SolveLds>
+__device__ __forceinline__ void to_blocks(double2 (&A)[RB][RB], const double2 (&P)[8], L &s, int p, int q,
                                           int lane)
 {
     stash_col(s, lane, 7, P[7]);
     wave_lds_sync();
 #pragma unroll
-    for (int aa = KB; aa < RB; ++aa) A[aa][KB] = s.conv[conv_idx(p + 8 * aa, q)];
+    for (int aa = KB; aa < RB; ++aa) A[aa][KB] = s.conv[s.ci(p + 8 * aa, q)];
     wave_lds_sync();   // to_rows<KB + 1> reuses conv
 }
 
-template <int KB, int K0 = 0, bool KEEP = false>
-__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s, int p,
+template <int KB, int K0 = 0, bool KEEP = false, typename L = SolveLds>
+__device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, L &s, int p,
                                            int q, int lane, double &rsel)
 {
 #pragma unroll
@@ -973,7 +980,8 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
 // Pivots 48..52 on register block (6, 6) and the read-out.  Eliminated
 // columns take unmasked updates (never read again); (54, 53) receives every
 // step, the last (pivot 52) straight from the published c_52.
-__device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, int p, int q)
+template <typename L = SolveLds>
+__device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], L &s, int p, int q)
 {
     constexpr int B6 = 8 * (RB - 1);
 #pragma unroll
@@ -996,7 +1004,8 @@ __device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], SolveLds &s, 
 // Pivots 49..52 on register block (6, 6) keeping L (the dense-C path):
 // each finished column is scaled in place (lanes q == kq), rsel collects
 // 1/sqrt(d).  Entering: column 48 scaled in place and published.
-__device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane, double &rsel)
+template <typename L = SolveLds>
+__device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], L &s, int p, int q, int lane, double &rsel)
 {
     constexpr int B6 = 8 * (RB - 1);
 #pragma unroll
@@ -1014,8 +1023,8 @@ __device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], SolveLds &s
     }
 }
 
-template <int KB>
-__device__ __forceinline__ void chol_panels_keep(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, SolveLds &s,
+template <int KB, typename L = SolveLds>
+__device__ __forceinline__ void chol_panels_keep(double2 (&A)[RB][RB], double2 (&P)[8], double2 &R, L &s,
                                                  int p, int q, int lane, double &rsel)
 {
     if constexpr (KB < RB - 1) {
@@ -1030,8 +1039,8 @@ __device__ __forceinline__ void chol_panels_keep(double2 (&A)[RB][RB], double2 (
 // Entering: A built (block rows/columns K0..6, row 53 = the conj right-hand
 // side).  K0 > 0 (the low-rank path, mmse_lr_kernel): the system occupies
 // rows 8 K0 .. 52 only and the panels before it are skipped.
-template <int K0 = 0>
-__device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], SolveLds &s, int p, int q, int lane)
+template <int K0 = 0, typename L = SolveLds>
+__device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], L &s, int p, int q, int lane)
 {
     double rsel = 0.0;
     if constexpr (K0 < RB - 1) {
@@ -1094,7 +1103,8 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
     return v;
 }
 
-__device__ __forceinline__ void exact_first_step(const SolveArgs &a, SolveLds &s, int64_t f, double ac, double bc)
+template <typename L = SolveLds>
+__device__ __forceinline__ void exact_first_step(const SolveArgs &a, L &s, int64_t f, double ac, double bc)
 {
     const int lane = threadIdx.x;
     const bool act = lane < NSC;
@@ -1139,7 +1149,8 @@ __device__ __forceinline__ void exact_first_step(const SolveArgs &a, SolveLds &s
 // by conj(rx) (row 53) and (w o x)^T (row 54), factorised with row-per-lane
 // Cholesky panels 0..5 (chol_panel) and the block-cyclic last panel
 // (chol_last); returns s = -S(54, 53) = w^T X Ryy^-1 rx.
-__device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
+template <typename L = SolveLds>
+__device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, const SolveArgs &a, L &s,
                                               int64_t f, double ac, double bc)
 {
     const int lane = threadIdx.x;
@@ -1198,8 +1209,8 @@ __device__ __forceinline__ double2 dot_factor(const State *__restrict__ st, cons
     return chol_last(A, s, p, q);
 }
 
-template <bool FC, bool DOT = false>
-__device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
+template <bool FC, bool DOT = false, typename L = SolveLds>
+__device__ __forceinline__ double2 solve_block(const State *__restrict__ st, const SolveArgs &a, L &s,
                                                int64_t base, int64_t f)
 {
     const int lane = threadIdx.x;
@@ -1357,8 +1368,8 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
 #endif
 // Gram column j of G~ at subcarrier k: x_k U[k][j] (U is zero past column
 // r - 1), rx_k at the border column j = 53 - 8 K0, 0 past it.
-template <int K0>
-__device__ __forceinline__ double2 lr_gcol(const State *__restrict__ st, const SolveLds &s, int k, int j)
+template <int K0, typename L = SolveLds>
+__device__ __forceinline__ double2 lr_gcol(const State *__restrict__ st, const L &s, int k, int j)
 {
     constexpr int RMAX = NSC - 8 * K0;
     const double2 g = cmul(s.x[k], ld2(st->U, k * CLD + j));   // k, j < 64 (U zero-padded)
@@ -1374,13 +1385,13 @@ __device__ __forceinline__ double2 lr_gcol(const State *__restrict__ st, const S
 // triangles, 4 real MFMAs per complex product).  Operand reads: lanes that
 // share p (or q) read one address, so each ds_read_b128 touches <= 8 slots.
 constexpr int LR_KC = 8;   // subcarriers per staged chunk
-template <int K0>
-__device__ __forceinline__ void lr_gram_valu(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB],
+template <int K0, typename L = SolveLds>
+__device__ __forceinline__ void lr_gram_valu(const State *__restrict__ st, L &s, double2 (&A)[RB][RB],
                                              int lane, int p, int q, double ac, double bc)
 {
     constexpr int NC = 8 * (RB - K0);   // staged Gram columns (block rows K0..6)
     constexpr int NB = RB - K0;
-    static_assert(LR_KC * NC <= 56 * CVS, "chunk fits the conv buffer");
+    static_assert(LR_KC * NC <= (56 - L::ROW0) * CVS, "chunk fits the conv buffer");
     double2 *T = s.conv;
 #pragma unroll
     for (int aa = K0; aa < RB; ++aa)
@@ -1425,9 +1436,9 @@ __device__ __forceinline__ void lr_gram_valu(const State *__restrict__ st, Solve
     }
 }
 
-template <int BLK, int K0>
+template <int BLK, int K0, typename L = SolveLds>
 __device__ __forceinline__ void back_blocks_from(const double2 (&A)[RB][RB], double2 (&P)[RB], const double (&rq)[RB],
-                                                 SolveLds &s, int p, int q, int lane)
+                                                 L &s, int p, int q, int lane)
 {
     if constexpr (BLK >= K0) {
         back_block<BLK>(A, P, rq, s, p, q, lane);
@@ -1436,8 +1447,8 @@ __device__ __forceinline__ void back_blocks_from(const double2 (&A)[RB][RB], dou
 }
 
 // One (frame, block): returns H_k on lane k (k < 53).
-template <int K0>
-__device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const SolveArgs &a, SolveLds &s, int64_t base)
+template <int K0, typename L = SolveLds>
+__device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const SolveArgs &a, L &s, int64_t base)
 {
     constexpr int RMAX = NSC - 8 * K0;
     const int lane = threadIdx.x;
@@ -1561,8 +1572,8 @@ __device__ __forceinline__ double2 lr_dft53p(const double2 *e, const double2 *pa
     return y;
 }
 
-template <int K0>
-__device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, SolveLds &s, double2 (&A)[RB][RB],
+template <int K0, typename L = SolveLds>
+__device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s, double2 (&A)[RB][RB],
                                              int lane, int p, int q, double ac, double bc)
 {
     constexpr int RMAX = NSC - 8 * K0;   // Gram column of the border (row 53)
@@ -1655,8 +1666,8 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, Solve
 }
 
 // lr_solve with the tap-domain Gram and read-out (State::cov_taps)
-template <int K0>
-__device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, const SolveArgs &a, SolveLds &s,
+template <int K0, typename L = SolveLds>
+__device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, const SolveArgs &a, L &s,
                                                  int64_t base)
 {
     const int lane = threadIdx.x;
@@ -1729,15 +1740,22 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
 #ifndef WCE_TAPS_WAVES_K0   // the tap form at K0 = 0 (168 VGPRs, 13 spilled at 3 waves/SIMD)
 #define WCE_TAPS_WAVES_K0 WCE_DENSE_WAVES_PER_SIMD
 #endif
+// K0 >= 2: the LDS holds only rows 8 K0 .. 55 of the panel transposes
+// (SolveLdsT<8 K0>: 9.9 KB per wave at K0 = 2 instead of 12.2), so 4 waves per
+// SIMD fit a CU's 160 KB where 3.25 did.
+constexpr int lr_row0(int k0) { return k0 >= 2 ? 8 * k0 : 0; }
+#ifndef WCE_LR_TAPS_WAVES   // the tap form at K0 >= 2 (<= 118 VGPRs)
+#define WCE_LR_TAPS_WAVES 4
+#endif
 constexpr int lr_waves(int k0, bool taps)
 {
-    return taps ? (k0 == 0 ? WCE_TAPS_WAVES_K0 : WCE_DENSE_WAVES_PER_SIMD)
+    return taps ? (k0 == 0 ? WCE_TAPS_WAVES_K0 : (k0 == 1 ? WCE_DENSE_WAVES_PER_SIMD : WCE_LR_TAPS_WAVES))
                 : (k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD));
 }
 template <int K0, bool TAPS = false>
 __global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
 {
-    __shared__ SolveLds s;
+    __shared__ SolveLdsT<lr_row0(K0)> s;
     const int64_t g = blockIdx.x;
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;

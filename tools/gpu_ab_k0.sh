@@ -1,0 +1,5 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_cov_taps_gpu.py tests/test_cov_lowrank_gpu.py -m gpu > gpurun_out/taps_tests.log 2>&1
+for T in 24 33 40; do timeout -k 10 200 python -u tools/ab_libs.py build_variants/prev build_variants/ldsr --leg lowrank --taps $T --frames 65536 >> gpurun_out/ab_k0.txt 2>&1 || exit 1; done
