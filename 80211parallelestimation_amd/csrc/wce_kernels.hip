@@ -2162,8 +2162,12 @@ __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v)
 {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    // every lane of the 16-lane row reads a valid source lane for the controls
+    // used here (row_newbcast, quad_perm, mirrors), so no "old" value is needed:
+    // mov_dpp is one v_mov_b32_dpp per half, where update_dpp(0, ...) also
+    // materialised the zero (a v_mov_b32 per half)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 template <int N>
