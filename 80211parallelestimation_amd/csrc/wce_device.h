@@ -97,8 +97,8 @@ __device__ __forceinline__ void st2_nt(double *p, int64_t idx, double2 v)
 // pairs and order as the __shfl_xor butterfly, so results are bit-identical.
 __device__ __forceinline__ double dpp_ror8(double v)
 {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x128, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x128, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x128, 0xf, 0xf, true);   // every lane has a source:
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x128, 0xf, 0xf, true);   // no materialised old value
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double sum_xor16(double v)

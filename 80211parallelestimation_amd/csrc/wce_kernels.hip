@@ -371,8 +371,8 @@ __global__ __launch_bounds__(256) void ls_elem_kernel(const State *__restrict__ 
 template <int CTRL>
 __device__ __forceinline__ double dpp_quad(double v)
 {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);   // quad_perm: every lane has a
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);   // source, no old value needed
     return __hiloint2double(hi, lo);
 }
 // sum over the 4 lanes of each quad, ((t0 + t1) + (t2 + t3)) in every lane

@@ -35,7 +35,17 @@ def test_checker_flags_dpp_after_a_label():
     """A DPP instruction at a branch target / loop header has predecessors the
     straight-line scan cannot see: flagged unless 2 wait states follow the label."""
     import isa_check
-    bad = "v_mov_b32 v1, v2\n.LBB0_3:\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
+    asm = "v_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1"
+    bad = f"v_mov_b32 v1, v2\n.LBB0_3:\n\t;;#ASMSTART\n{asm}\n\t;;#ASMEND\n"
     assert [p for _, p in isa_check.dpp_hazards(bad)] == [isa_check.LABEL]
-    ok = ".LBB0_3:\ns_nop 1\nv_fmac_f64_dpp v[78:79], -v[122:123], v[90:91] row_newbcast:1\n"
+    ok = f".LBB0_3:\n\t;;#ASMSTART\ns_nop 1\n{asm}\n\t;;#ASMEND\n"
     assert isa_check.dpp_hazards(ok) == []
+
+
+def test_compiler_dpp_after_a_label_is_the_compilers():
+    """A compiler-emitted DPP (no ;;#ASMSTART) at a label: the compiler's hazard
+    recognizer sees its predecessors, so only the straight-line rule applies."""
+    import isa_check
+    dpp = "v_mov_b32_dpp v30, v24 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+    assert isa_check.dpp_hazards(f"s_or_b64 exec, exec, s[0:1]\n.LBB0_3:\n{dpp}\n") == []
+    assert len(isa_check.dpp_hazards(f"v_mov_b32 v24, v2\n{dpp}\n")) == 1

@@ -5,7 +5,11 @@ wce_kernels.hip cmsub_bc).  The hardware needs 2 wait states between a VALU
 write of a VGPR and a DPP instruction reading it through the DPP crossbar;
 the compiler cannot see into inline asm, so this checks the emitted code:
 no VALU instruction in the 2 wait states before a DPP instruction writes
-that instruction's DPP source (src0).
+that instruction's DPP source (src0).  A DPP instruction at a branch target
+whose predecessors the straight-line scan cannot see is flagged only when it
+comes from inline asm (;;#ASMSTART .. ;;#ASMEND): the compiler's own hazard
+recognizer covers every predecessor of the DPP instructions it emits
+(__builtin_amdgcn_mov_dpp, the quad kernel's row broadcasts).
 usage: python tools/isa_check.py [file.s]   (default: compile wce_kernels.hip)"""
 import os
 import re
@@ -30,26 +34,39 @@ def regs(tok: str):
 LABEL = "<label>"
 
 
-def instructions(text: str, labels=False):
-    """Instruction lines; with labels=True also the basic-block labels (as LABEL)."""
+def _lines(text: str):
+    """(instruction or LABEL, inside inline asm) for every instruction and label."""
+    in_asm = False
     for line in text.splitlines():
+        c = line.strip()
+        if c.startswith(";;#ASMSTART"):
+            in_asm = True
+        elif c.startswith(";;#ASMEND"):
+            in_asm = False
         t = line.split(";")[0].strip()
         if t.endswith(":"):   # labels (".LBB0_3:", "kernel:") before directives (".p2align")
-            if labels:
-                yield LABEL
+            yield LABEL, in_asm
             continue
         if not t or t.startswith("."):
             continue
-        yield t
+        yield t, in_asm
+
+
+def instructions(text: str, labels=False):
+    """Instruction lines; with labels=True also the basic-block labels (as LABEL)."""
+    for t, _ in _lines(text):
+        if t != LABEL or labels:
+            yield t
 
 
 def dpp_hazards(text: str):
     """List of (dpp instruction, offending earlier instruction).  A label is a
     branch target or loop header whose predecessors this straight-line scan
     cannot see: a DPP instruction fewer than 2 wait states after one is
-    reported (offender LABEL) unless those wait states come after the label."""
+    reported (offender LABEL) unless those wait states come after the label --
+    for inline-asm DPP only (module docstring)."""
     out, prev = [], []   # prev: (wait states the instruction provides, text)
-    for ins in instructions(text, labels=True):
+    for ins, in_asm in _lines(text):
         if ins == LABEL:
             prev.append((0, LABEL))
             prev = prev[-8:]
@@ -63,7 +80,8 @@ def dpp_hazards(text: str):
                 if ws >= 2:
                     break
                 if p == LABEL:
-                    out.append((ins, LABEL))
+                    if in_asm:
+                        out.append((ins, LABEL))
                     break
                 pop = p.split()[0]
                 if pop.startswith("v_") and not pop.startswith(("v_readlane", "v_readfirstlane", "v_cmp")):
