@@ -1798,7 +1798,10 @@ __global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const S
 //    each chunk's loads issued one chunk ahead into registers; every lane then
 //    reads its own frame's 4 values from LDS (row stride 5 complex:
 //    conflict-free), and H goes out the same way in reverse.  0.110 ms at
-//    131,072 frames, 0.95 ms at 1,048,576, but 0.061 ms at 65,536.
+//    131,072 frames, 0.95 ms at 1,048,576, but 0.061 ms at 65,536.  H leaves
+//    in chunks of 8 subcarriers (8 frames x 128 B per store, 7 stores per
+//    frame instead of 14 of 64 B): rank 8 0.055 -> 0.046 ms at 65,536 frames,
+//    2.7-4% at 1,048,576, bit-identical (profiles/r04_ab_lowrank_store8.txt).
 #ifndef WCE_LR_LANE_UNROLL   // direct form without the look-ahead: subcarriers per step up to rank 4
 #define WCE_LR_LANE_UNROLL 4
 #endif
@@ -2050,25 +2053,34 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
         }
         return y;
     };
-    if constexpr (STAGED) {   // each lane its frame's 4 subcarriers of a chunk into LDS, then 16 frames x 64 B per store
-        int64_t ob[4];
+    if constexpr (STAGED) {   // each lane its frame's 8 subcarriers of a chunk into LDS (x and r as one
+                              // area), then 8 frames x 128 B per store: a frame's H in 7 stores, not 14
+        constexpr int SC = 8, SS = 9;   // subcarriers per store chunk, LDS row stride (complex) per frame
+        static_assert(sizeof(LrLaneLds) >= 64 * SS * sizeof(double2), "store staging fits the chunk buffers");
+        double2 *so = sp->x;
+        int64_t ob[8];
+        uint32_t live8 = 0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) ob[m] = (g0 + (lane >> 2) + 16 * m) * a.ws;
+        for (int m = 0; m < 8; ++m) {
+            const int64_t u = g0 + (lane >> 3) + 8 * m;
+            ob[m] = u * a.ws;
+            live8 |= (u < units ? 1u : 0u) << m;
+        }
 #pragma unroll 1
-        for (int c = 0; c < LRL_NCH; ++c) {
+        for (int c = 0; c < (NSC + SC - 1) / SC; ++c) {
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int kk = 0; kk < LRL_KC; ++kk) {
-                const int k = LRL_KC * c + kk;
+            for (int kk = 0; kk < SC; ++kk) {
+                const int k = SC * c + kk;
                 if (kk > 0 && k >= NSC) break;
-                sp->x[lane * LRL_LS + kk] = hk(k);
+                so[lane * SS + kk] = hk(k);
             }
             asm volatile("" ::: "memory");
-            const int k = LRL_KC * c + (lane & 3);
+            const int k = SC * c + (lane & 7);
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const double2 y = sp->x[((lane >> 2) + 16 * m) * LRL_LS + (lane & 3)];
-                if (((live >> m) & 1u) && k < NSC) st2(a.w, ob[m] + k, y);
+            for (int m = 0; m < 8; ++m) {
+                const double2 y = so[((lane >> 3) + 8 * m) * SS + (lane & 7)];
+                if (((live8 >> m) & 1u) && k < NSC) st2(a.w, ob[m] + k, y);
             }
         }
     } else {
