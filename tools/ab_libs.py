@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
-ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank"], default="config5")
+ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm"], default="config5")
 ap.add_argument("--taps", type=int, default=8, help="lowrank: L-tap PDP covariance (rank L; 53 = decay 0.5)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--frames", type=int, default=262144)
@@ -34,7 +34,7 @@ for d in args.dirs:
     if args.leg in ("dense", "apply"):
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rhh())
-    elif args.leg == "lowrank":
+    elif args.leg in ("lowrank", "cm"):   # cm: the same ctx on the constant-modulus operator (wce_ctx_set_modulus)
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rank(args.taps))
     else:
@@ -51,7 +51,9 @@ for d in args.dirs:
         f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.ALL, st.handle))(ctx, fr, o, st, m)
         keep += outs + [eq]
         check = outs[4]
-    elif args.leg in ("headline", "lowrank"):
+    elif args.leg in ("headline", "lowrank", "cm"):
+        if args.leg == "cm":
+            ctx.set_modulus(tx.rows(0)[0, 0])
         H = m.DeviceArray((n, N))
         fr = ctx.frames(tx, rx, n)
         o = m.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
