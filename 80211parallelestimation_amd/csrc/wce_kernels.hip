@@ -1531,6 +1531,9 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
 #ifndef WCE_TAPS_UNROLL
 #define WCE_TAPS_UNROLL 2
 #endif
+#ifndef WCE_TAPS_SPLIT   // the Q / D DFTs over half the pairs per half-wave, outputs d and 53 - d together
+#define WCE_TAPS_SPLIT 1
+#endif
 // Every DFT here runs over pairs (k, 53 - k): E[(53 - k) m] = conj(E[k m]), so
 //     c_k E[km] + c_{53-k} conj(E[km]) = (c_k + c_{53-k}) Re E[km] + i (c_k - c_{53-k}) Im E[km]
 // -- one gather and half the FMAs and index steps of the plain sum.
@@ -1572,6 +1575,54 @@ __device__ __forceinline__ double2 lr_dft53p(const double2 *e, const double2 *pa
     return y;
 }
 
+// The same sum as lr_dft53p, outputs m and 53 - m together (E[k (53 - m)] =
+// conj(E[k m]): A = sum pa_k Re E, B = i sum pb_k Im E (CONJ: -Im), y(m) = c_0 + A
+// + B, y(53 - m) = c_0 + A - B), half-wave h over the pairs k = 1 + 13 h ..
+// 13 + 13 h; the halves meet in xs (>= 59 entries of free LDS), which ends up
+// holding y, returned on lane m (lanes past 52: y(0)).
+#ifndef WCE_TAPS_SPLIT_OUT
+#define WCE_TAPS_SPLIT_OUT 1
+#endif
+template <bool CONJ>
+__device__ __forceinline__ double2 lr_dft53_split(const double2 *e, const double2 *pa, const double2 *pb, double2 c0,
+                                                  int lane, double2 *xs)
+{
+    const int h = lane >> 5, d = lane & 31;
+    const bool dv = d <= NSC / 2;
+    const int dd = dv ? d : 0;
+    const int k0 = 1 + (NSC / 4) * h;
+    const uint32_t st = 16u * (uint32_t)dd, sw = st - 16u * NSC;
+    uint32_t o = 16u * (uint32_t)((k0 * dd) % NSC);
+    double2 A = make_double2(0.0, 0.0), B = A;
+#pragma unroll WCE_TAPS_UNROLL
+    for (int j = 0; j < NSC / 4; ++j) {
+        const int k = k0 + j;
+        const double2 w = ld_e(e, o), va = pa[k], vb = pb[k];
+        const double wy = CONJ ? -w.y : w.y;
+        A.x = fma(va.x, w.x, A.x);
+        A.y = fma(va.y, w.x, A.y);
+        B.x = fma(-vb.y, wy, B.x);
+        B.y = fma(vb.x, wy, B.y);
+        o = dft_step(o, st, sw);
+    }
+    if (h == 1 && dv) {
+        xs[d] = A;
+        xs[32 + d] = B;
+    }
+    wave_lds_sync();
+    if (h == 0 && dv) {
+        A = cadd(A, xs[d]);
+        B = cadd(B, xs[32 + d]);
+    }
+    wave_lds_sync();
+    if (h == 0 && dv) {
+        xs[d] = cadd(c0, cadd(A, B));
+        if (d > 0) xs[NSC - d] = cadd(c0, csub(A, B));
+    }
+    wave_lds_sync();
+    return xs[lane < NSC ? lane : 0];
+}
+
 template <int K0, typename L = SolveLds>
 __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s, double2 (&A)[RB][RB],
                                              int lane, int p, int q, double ac, double bc)
@@ -1597,6 +1648,57 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
 #ifdef WCE_ABLATE_TAPS_DFT   // timing-only: no Q / D DFTs
     Qd = make_double2(s.rd[lane], 0.0);
     Dd = s.u[1][lane];
+#elif WCE_TAPS_SPLIT
+    // Outputs d and 53 - d share every gather: E[k (53 - d)] = conj(E[k d]), so
+    // with A = sum pa_k Re E[k d] and B = i sum pb_k Im E[k d] (over the pairs),
+    // D(d) = v_0 + A + B and D(53 - d) = v_0 + A - B; Q(53 - d) = conj(Q(d)).
+    // Lane (h, d) = (lane >> 5, lane & 31), d <= 26, sums the pairs k = 1 + 13 h
+    // .. 13 + 13 h: 13 steps instead of 26; the halves meet in LDS (blk / z,
+    // free until the element build).
+    {
+        const int h = lane >> 5, d = lane & 31;
+        const bool dv = d <= NSC / 2;
+        const int dd = dv ? d : 0;
+        const int k0 = 1 + (NSC / 4) * h;   // 1 or 14
+        const uint32_t st = 16u * (uint32_t)dd, sw = st - 16u * NSC;
+        uint32_t o = 16u * (uint32_t)((k0 * dd) % NSC);
+        double2 q = make_double2(0.0, 0.0), A = q, B = q;
+#pragma unroll WCE_TAPS_UNROLL
+        for (int j = 0; j < NSC / 4; ++j) {
+            const int k = k0 + j;
+            const double2 w = ld_e(s.u[0], o), va = s.tp.pa[k], vb = s.tp.pb[k];
+            const double2 pp = s.tp.rp[k];   // {p_k + p_{53-k}, p_k - p_{53-k}}
+            q.x = fma(pp.x, w.x, q.x);
+            q.y = fma(-pp.y, w.y, q.y);
+            A.x = fma(va.x, w.x, A.x);
+            A.y = fma(va.y, w.x, A.y);
+            B.x = fma(-vb.y, w.y, B.x);
+            B.y = fma(vb.x, w.y, B.y);
+            o = dft_step(o, st, sw);
+        }
+        if (h == 1 && dv) {
+            s.blk[d] = q;
+            s.z[d] = A;
+            s.z[32 + d] = B;
+        }
+        wave_lds_sync();
+        if (h == 0 && dv) {
+            q = cadd(q, s.blk[d]);
+            A = cadd(A, s.z[d]);
+            B = cadd(B, s.z[32 + d]);
+        }
+        wave_lds_sync();
+        if (h == 0 && dv) {
+            const double2 v0 = s.u[1][0];
+            const double2 Qp = make_double2(s.rd[0] + q.x, q.y);
+            s.blk[d] = cscale(Qp, ac);
+            s.z[d] = cadd(v0, cadd(A, B));
+            if (d > 0) {
+                s.blk[NSC - d] = cscale(cconj(Qp), ac);
+                s.z[NSC - d] = cadd(v0, csub(A, B));
+            }
+        }
+    }
 #else
     {
         const uint32_t st = 16u * (uint32_t)(act ? lane : 0), sw = st - 16u * NSC;
@@ -1621,8 +1723,10 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
     // Sluis; the dense path's scaled form, s5), and every element is a plain
     // gather of a Q (pre-scaled by a) instead of a product of three factors.
     // Padding columns j in [r, RMAX): pivot b, zero border -> w_j = 0.
+#if !WCE_TAPS_SPLIT || defined(WCE_ABLATE_TAPS_DFT)
     s.blk[lane] = cscale(Qd, ac);
     s.z[lane] = Dd;
+#endif
     int *tapl = reinterpret_cast<int *>(s.u[1]);   // column j -> its tap (256 B of u[1]) ...
     double *bl = reinterpret_cast<double *>(tapl + 64);   // ... and M's diagonal term b / lambda_j (b past r)
     const int r = st->cov_rank;
@@ -1714,7 +1818,11 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
 #ifdef WCE_ABLATE_TAPS_OUT   // timing-only: no read-out DFT
     double2 y = s.u[1][kk];
 #else
+#if WCE_TAPS_SPLIT_OUT
+    double2 y = lr_dft53_split<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z);   // y_k = sum_t c_t E[k t]
+#else
     double2 y = lr_dft53p<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], kk);   // y_k = sum_t c_t E[k t]
+#endif
 #endif
     if (__ballot(act && xl.y != 0.0) != 0) {   // complex symbols: y += U U^H [(x - conj x) o rho] / b
         const double2 rho = csub(s.rx[lane], cscale(cmul(xl, y), ac));   // b Ryy^-1 rx
@@ -1722,12 +1830,20 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
         wave_lds_sync();   // (also: every lane's read-out reads of the pair tables are done)
         dft_pairs(s.blk, s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
+#if WCE_TAPS_SPLIT_OUT
+        const double2 w = lr_dft53_split<true>(s.u[0], s.tp.pa, s.tp.pb, s.blk[0], lane, s.z);   // w_t = sum_k conj(E[k t]) v_k
+#else
         const double2 w = lr_dft53p<true>(s.u[0], s.tp.pa, s.tp.pb, s.blk[0], kk);   // w_t = sum_k conj(E[k t]) v_k
+#endif
         s.u[1][lane] = act ? cscale(w, ts * ts / bc) : make_double2(0.0, 0.0);
         wave_lds_sync();
         dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
+#if WCE_TAPS_SPLIT_OUT
+        y = cadd(y, lr_dft53_split<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z));
+#else
         y = cadd(y, lr_dft53p<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], kk));
+#endif
     }
     return y;
 }
