@@ -197,6 +197,12 @@ int wce_ctx_mark_ready(wce_ctx *c)
     HIPCHECK(hipMemcpy(h.get(), c->d_state, sizeof(State), hipMemcpyDeviceToHost), "read state");
     if (!wce::state_ok(h.get()))
         return fail(WCE_ESTATE, "state buffer does not hold a valid state of this build (magic, layout, size, mode, rank)");
+    // the host copy (wce_ctx_set_modulus rebuilds from it) stays only if the
+    // device now holds exactly it; another state drops it
+    if (c->has_host && std::memcmp(h.get(), &c->host, sizeof(State)) != 0) {
+        c->has_host = false;
+        c->rhh.clear();
+    }
     c->mode = h->mode;
     c->cov_rank = h->cov_rank;
     c->cov_k0 = h->cov_k0;
@@ -214,6 +220,10 @@ int wce_ctx_load_state(wce_ctx *c, const void *host_state, size_t bytes)
         return fail(WCE_ESTATE, "state blob is not a valid state of this build (magic, layout, size, mode, rank)");
     DeviceGuard g(c->device);
     HIPCHECK(hipMemcpy(c->d_state, host_state, sizeof(State), hipMemcpyHostToDevice), "upload state");
+    if (c->has_host && std::memcmp(st, &c->host, sizeof(State)) != 0) {   // see wce_ctx_mark_ready
+        c->has_host = false;
+        c->rhh.clear();
+    }
     c->mode = st->mode;
     c->cov_k0 = st->cov_k0;
     c->cov_rank = st->cov_rank;
@@ -522,8 +532,12 @@ static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
     double *hw = ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
     const State *st = c->d_state;
     *done = false;
+    // without `hout` the factor launch writes w only at the 4 pilot rows, which
+    // is all ref_ls_elem_kernel reads; the wave-per-frame REF_LS variant reads
+    // all 53 rows of w, so it takes the full-row path below
     if (c->mode == WCE_MMSE_REF && sa.ref_pilots && in->semantics == WCE_SEM_C &&
-        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0) {
+        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0 &&
+        (hout || wce::variant_value(wce::WCE_VARIANT_REF_LS) == 0)) {
         rc = wce::launch_ref_fc(st, sa, reinterpret_cast<const double *>(in->rx_pre), in->pre_stride,
                                 reinterpret_cast<const double *>(in->tx_pre), uw, ww, WS_LD, hout, stream);
         if (rc) return fail(rc, "ref_fc launch (frame covariance)");

@@ -113,7 +113,9 @@ inline bool state_ok(const State *st)
     if (st->mode != WCE_MMSE_REF && st->mode != WCE_MMSE_TEXTBOOK && st->mode != WCE_MMSE_COV) return false;
     if (st->mode == WCE_MMSE_COV)
         return st->cov_rank >= 0 && st->cov_rank <= NSC && st->cov_k0 >= -1 && st->cov_k0 <= COV_K0_MAX &&
-               (st->cov_k0 >= 0 || st->cov_rank == NSC) && taps_ok(st);
+               (st->cov_k0 >= 0 || st->cov_rank == NSC) &&
+               // the Gram kernels' row bound: RMAX = 53 - 8 K0 (lr_solve_taps reads z[8 K0 + col], col < rank)
+               (st->cov_k0 < 0 || st->cov_rank <= NSC - 8 * st->cov_k0) && taps_ok(st);
     return st->cov_k0 == -1;
 }
 

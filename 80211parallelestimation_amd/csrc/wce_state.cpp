@@ -598,6 +598,20 @@ int host_build_cm(State *st, const ldc *Fl, const wce_complex *Rhh, const wce_co
     if (cov_factor(Fl, Rhh, cf) != WCE_OK) return WCE_EINVAL;
     const int r = cf.r;
     if (r != st->cov_rank) return WCE_EINVAL;   // not the Rhh this state was built from
+    // same rank is not enough: U (rounded to fp64 as host_apply_cov stores it)
+    // and, for a diagonal Rhh, the tap tables must be this state's bit for bit,
+    // or K would belong to another C than the one the per-frame path and the
+    // non-real correction use
+    for (int j = 0; j < r; j++)
+        for (int k = 0; k < n; k++) {
+            const cld u = cf.U[(size_t)k * r + j];
+            if (st->U[2 * (k * CLD + j)] != (double)__real__ u || st->U[2 * (k * CLD + j) + 1] != (double)__imag__ u)
+                return WCE_EINVAL;
+        }
+    if ((st->cov_taps != 0) != cf.diag) return WCE_EINVAL;
+    if (cf.diag)
+        for (int j = 0; j < r; j++)
+            if (st->tap_of[j] != cf.tap[j] || st->col_s[j] != (double)sqrtl(cf.lam[j])) return WCE_EINVAL;
     if (r == 0) { st->cm_on = 1; std::memcpy(st->pcm, p, sizeof(p)); return WCE_OK; }   // C = 0: K = 0
     const std::vector<cld> &U = cf.U;
     // G = a U^H P U + b I

@@ -180,6 +180,30 @@ def test_state_validation_rejects_foreign_blobs(wce, golden):
         wce.state_mode(blob[:-16].copy())                          # short blob
 
 
+def test_state_validation_rank_within_gram_rows(wce, golden):
+    """cov_rank <= 53 - 8 cov_k0 (the Gram kernels' RMAX): a blob
+    whose k0 is in range but leaves fewer Gram rows than its rank is refused
+    before any kernel indexes LDS with it."""
+    inp = golden["inputs"]
+    R = np.zeros((N, N), np.complex128)
+    R[:8, :8] = _pdp_cov(8, 0.5)                                  # rank 8, k0 = 5: 13 rows
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    o = _state_field_offset(blob)
+    assert wce.state_mode(blob) == wce.MMSE_COV
+    b2 = blob.copy()
+    b2[o + 4:o + 8] = np.array([6], np.int32).view(np.uint8)     # k0 = 6 <= COV_K0_MAX, but 53 - 48 = 5 < 8
+    with pytest.raises(wce.WceError):
+        wce.state_mode(b2)
+    R16 = np.zeros((N, N), np.complex128)
+    R16[:16, :16] = _pdp_cov(16, 0.5)
+    b3 = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R16)
+    k0 = b3[o + 4:o + 8].view(np.int32)[0]
+    assert 16 <= 53 - 8 * k0                                      # the builder keeps the invariant
+    b3[o + 4:o + 8] = np.array([k0 + 1], np.int32).view(np.uint8)
+    with pytest.raises(wce.WceError):
+        wce.state_mode(b3)
+
+
 @pytest.mark.gpu
 def test_c_host_cli_runs():
     """tools/wce_cli.c, a C host using only include/wce.h, runs every

@@ -21,7 +21,44 @@ def _latest(pattern):
 
 @pytest.fixture(scope="module")
 def line():
+    """The driver-facing line: bench.py prints it LAST, compact (round 5+)."""
     return json.load(open(_latest("r*_bench.json")))
+
+
+@pytest.fixture(scope="module")
+def full(line):
+    """The full per-leg record (bench.py --extras-out, committed as
+    profiles/<round>_bench_extras.json); rounds <= 4 printed it as the line."""
+    path = _latest("r*_bench.json").replace("_bench.json", "_bench_extras.json")
+    return json.load(open(path)) if os.path.exists(path) else line
+
+
+def test_line_fits_driver_tail():
+    """The driver keeps the last 8 KB of stdout and parses the final line:
+    the committed line must fit whole (BENCH_r04.json parsed null at 20 KB)."""
+    path = _latest("r*_bench.json")
+    if os.path.basename(path) < "r05":
+        pytest.skip("round <= 4 line predates the compact form")
+    text = open(path).read().strip()
+    assert "\n" not in text and len(text.encode()) <= 8192, len(text)
+
+
+def test_compact_line_bounded_and_faithful():
+    """bench.compact() of any full record (the largest committed one) stays
+    under the limit and carries the headline numbers unchanged."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    fulls = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_bench_extras.json"))) or \
+        [f for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_bench.json")))]
+    src = json.load(open(max(fulls, key=os.path.getsize)))
+    c = bench.compact(src, "x.json")
+    text = json.dumps(c, separators=(",", ":"))
+    assert len(text) <= bench.COMPACT_LIMIT
+    for k in ("metric", "value", "ms_per_step", "n_gpus", "dtype"):
+        assert c[k] == src[k]
+    assert c["roofline"]["frac"] == src["roofline"]["frac"]
+    assert c["cpu_baseline"]["value"] == src["cpu_baseline"]["value"]
 
 
 def test_contract_keys(line):
@@ -62,9 +99,10 @@ def test_cpu_baseline_fields(line):
         assert c["max_normrel_err_vs_gpu"] < 1e-10
 
 
-def test_leg_rooflines(line):
+def test_leg_rooflines(full):
     """Legs that carry a roofline keep its arithmetic; counters come from
     same-size launches (pmc_source names the legs file, not a refusal)."""
+    line = full
     ref = line.get("ref_mode", {}).get("b1048576")
     if ref:
         r = ref["roofline"]
@@ -93,15 +131,15 @@ def test_rocprof_headline_average_agrees(line):
     assert abs(avg_ms - line["roofline"]["avg_launch_ms"]) / avg_ms < 0.10, (avg_ms, line["roofline"]["avg_launch_ms"])
 
 
-def test_extra_legs_consistent(line):
+def test_extra_legs_consistent(line, full):
     """The extra legs that carry their own arithmetic agree with it: configs[3]
     (strong scaling over 1,048,576 frames), the PCIe-inclusive host pipeline,
     and the non-finite check of the headline output."""
-    c4 = line.get("config4")
+    c4 = full.get("config4")
     if c4:
         assert c4["global_frames"] == 1 << 20 and c4["scaling"] == "strong"
         assert abs(c4["frames_per_s"] - c4["global_frames"] / (c4["ms_per_step"] * 1e-3)) / c4["frames_per_s"] < 1e-6
-    hp = line.get("host_pipeline")
+    hp = full.get("host_pipeline")
     if hp:
         assert hp["bit_identical_to_device_path"] is True
         assert hp["frames_per_s"] < line["value"]          # PCIe-bound, never the headline
@@ -109,8 +147,8 @@ def test_extra_legs_consistent(line):
         assert line["nonfinite_frames"] == 0
 
 
-def test_config5_sharded_consistent(line):
-    c5 = line.get("config5_sharded")
+def test_config5_sharded_consistent(full):
+    c5 = full.get("config5_sharded")
     if c5:
         if "nonfinite_outputs" in c5:
             assert c5["nonfinite_outputs"] == 0

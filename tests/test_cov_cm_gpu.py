@@ -173,3 +173,29 @@ def test_constant_modulus_off_and_rank8(gpu_wce, golden):
     plain = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
     with pytest.raises(wce.WceError):
         plain.set_modulus(tx[0, 0])
+
+
+def test_set_modulus_after_load_state(gpu_wce, golden):
+    """create_cov -> load_state(another COV blob) -> set_modulus must not
+    re-upload the ORIGINAL state over the loaded one: the ctx
+    drops its host copy, set_modulus refuses, and estimates keep running the
+    loaded state.  Loading the ctx's own state back keeps set_modulus usable."""
+    wce = gpu_wce
+    inp = golden["inputs"]
+    rng = np.random.default_rng(9)
+    B = 257
+    tx = mixed_frames(rng, B, np.full(B, "bpsk"))
+    rx = channel_rx(rng, tx, inp["ow2"])
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh(16, 0.5))
+    own = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh(16, 0.5))
+    other_blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh(24, 0.3))
+    other = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh(24, 0.3))
+    want = run(other, wce, tx, rx, True)
+    ctx.load_state(other_blob)
+    with pytest.raises(wce.WceError):
+        ctx.set_modulus(tx[0, 0])
+    assert np.array_equal(run(ctx, wce, tx, rx, True), want)     # still the loaded state
+    ctx2 = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=pdp_rhh(16, 0.5))
+    ctx2.load_state(own)                                          # its own state, byte for byte
+    ctx2.set_modulus(tx[0, 0])
+    ctx2.set_modulus(None)

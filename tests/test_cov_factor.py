@@ -232,6 +232,36 @@ def test_constant_modulus_rejects_mismatch(wce, inp):
     assert rc != 0
 
 
+@pytest.mark.parametrize("case", ["scaled", "permuted_taps", "dense_offdiag"])
+def test_constant_modulus_rejects_same_rank_mismatch(wce, inp, case):
+    """A different Rhh of the SAME rank must not pass: K would be
+    built for another C than the state's C / U that the per-frame path and the
+    non-real correction use.  Same power profile scaled, the same taps in
+    another order of power, and a non-diagonal Rhh of equal rank."""
+    import ctypes
+    lib = wce.load()
+    R = pdp_rhh(16, 0.5)
+    blob = wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    if case == "scaled":
+        R2 = R * 1.5
+    elif case == "permuted_taps":
+        d = np.diag(R).copy()
+        R2 = np.diag(np.r_[d[:16][::-1], np.zeros(N - 16)]).astype(np.complex128)   # taps 0..15, powers reversed
+    else:
+        R2 = R.copy()
+        R2[1, 2] = R2[2, 1] = 0.1 * R[2, 2]
+    assert wce.cov_factor(wce.state_blob(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R2))[1] == 16
+    x = np.full(N, 8.8753 + 0j)
+    x[26] = 0
+    before = blob.copy()
+    rc = lib.wce_state_set_modulus(blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes,
+                                   R2.ctypes.data_as(ctypes.c_void_p), x.ctypes.data_as(ctypes.c_void_p))
+    assert rc != 0
+    rc = lib.wce_state_set_modulus(before.ctypes.data_as(ctypes.c_void_p), before.nbytes,
+                                   R.ctypes.data_as(ctypes.c_void_p), x.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0                                    # the state's own Rhh still passes
+
+
 @pytest.mark.parametrize("L,decay,spread", [(53, 0.5, False), (24, 0.3, False), (20, 0.2, True)])
 def test_tap_tables(wce, oracle, inp, L, decay, spread):
     """A diagonal Rhh sets State's tap-domain tables (mmse_lr_kernel<K0, true>):

@@ -64,3 +64,36 @@ def test_ref_variants_identical(gpu_wce, golden, lib, frame_cov):
         got.append(H.numpy())
     assert np.isfinite(got[0]).all()
     assert np.array_equal(got[1], got[0])
+
+
+def test_ref_frame_cov_ls_variant_full_w_rows(gpu_wce, golden, lib):
+    """REF + FRAME_COV + the LS family on the wave-per-frame REF_LS variant
+    (1) reads all 53 rows of w: the factor launch must write them, not only
+    the 4 pilot rows.  The workspace is first filled with NaN
+    by a call on NaN preambles; the next call must be finite and agree with
+    the default one-element-per-thread form (0)."""
+    inp = golden["inputs"]
+    ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
+    B = 4099
+    tx, rx, pre = gpu_wce.DeviceArray((B, NBLK, N)), gpu_wce.DeviceArray((B, NBLK, N)), gpu_wce.DeviceArray((B, N))
+    ctx.synth(tx, rx, pre, B, seed=0x3C)
+    ctx.reserve(B)
+    nanpre = gpu_wce.DeviceArray.from_numpy(np.full((B, N), np.nan + 1j * np.nan))
+    mask = gpu_wce.ALL | gpu_wce.FRAME_COV
+    got = []
+    try:
+        for v in (0, 1):
+            assert lib.wce_debug_set_variant(2, v) == 0
+            outs = [gpu_wce.DeviceArray((B, N), zero=True) for _ in range(5)]
+            eq = gpu_wce.DeviceArray((B, NBLK, N), zero=True)
+            o = gpu_wce.Outputs(*(x.addr for x in outs), eq.addr, N, NBLK * N, N, 0, 0)
+            ctx.estimate(ctx.frames(tx, rx, B, rx_pre=nanpre), o, mask)      # poisons the workspace
+            ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre), o, mask)
+            gpu_wce.synchronize()
+            got.append([x.numpy() for x in outs] + [eq.numpy()])
+    finally:
+        assert lib.wce_debug_set_variant(2, 0) == 0
+    for a, b in zip(got[0], got[1]):
+        assert np.isfinite(b).all()
+        scale = np.abs(a).max(axis=-1, keepdims=True)
+        assert (np.abs(a - b) <= 1e-12 * scale).all()
