@@ -518,34 +518,27 @@ int wce_ctx_reserve(wce_ctx *c, int64_t n)
     return wce_ctx_reserve_stream(c, n, nullptr);
 }
 
-// WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvecs), into
-// the solve arguments.  lt_ready: the caller's LT_LS output already holds H_LT.
-// REF in C semantics takes one launch (ref_fc_kernel): with `hout` it also
-// writes H = u s and sets *done; otherwise u and w (pilot rows) go to the
-// workspace for ref_ls_elem_kernel.
-static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready, bool hout,
+// WCE_MMSE_FRAME_COV: H_LT_f -> factors u_f, w_f of C_f (MFMA matvec, and for
+// REF the folded pilot-row map), into the solve arguments.  lt_ready: the
+// caller's LT_LS output already holds H_LT.  REF in C semantics takes one
+// launch (ref_fc_kernel) that writes H = u s itself and sets *done.
+static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready,
                           wce::SolveArgs &sa, double *ws, bool *done, void *stream)
 {
     const int64_t n = in->n_frames;
     if (!in->rx_pre) return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
     int rc = WCE_OK;
-    double *hw = ws, *gw = hw + n * WS_LD * 2, *uw = gw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
+    double *hw = ws, *uw = hw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
     const State *st = c->d_state;
     *done = false;
-    // without `hout` the factor launch writes w only at the 4 pilot rows, which
-    // is all ref_ls_elem_kernel reads; the wave-per-frame REF_LS variant reads
-    // all 53 rows of w, so it takes the full-row path below
+    // the fused LS epilogue after it must be ref_ls_elem_kernel (the default
+    // REF_LS form); the wave-per-frame form takes the path below
     if (c->mode == WCE_MMSE_REF && sa.ref_pilots && in->semantics == WCE_SEM_C &&
-        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0 &&
-        (hout || wce::variant_value(wce::WCE_VARIANT_REF_LS) == 0)) {
+        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0 && wce::variant_value(wce::WCE_VARIANT_REF_LS) == 0) {
         rc = wce::launch_ref_fc(st, sa, reinterpret_cast<const double *>(in->rx_pre), in->pre_stride,
-                                reinterpret_cast<const double *>(in->tx_pre), uw, ww, WS_LD, hout, stream);
+                                reinterpret_cast<const double *>(in->tx_pre), stream);
         if (rc) return fail(rc, "ref_fc launch (frame covariance)");
-        *done = hout;
-        sa.cu = uw;
-        sa.cw = ww;
-        sa.cs = WS_LD;
-        sa.hout = 1;
+        *done = true;
         return WCE_OK;
     }
     const double *h = hw;
@@ -567,12 +560,8 @@ static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
         rc = wce::launch_ls(c->d_state, a, stream);
         if (rc) return fail(rc, "ls launch (H_LT for frame covariance)");
     }
-    if (c->mode == WCE_MMSE_REF) {
-        rc = wce::launch_matvec(st->Mg, st->Mu, h, hs, gw, uw, WS_LD, n, false, stream);     // g, u
-        if (!rc) rc = wce::launch_matvec(st->Mw, nullptr, gw, WS_LD, ww, nullptr, WS_LD, n, true, stream);
-    } else {
-        rc = wce::launch_matvec(st->Mu, nullptr, h, hs, uw, nullptr, WS_LD, n, false, stream);
-    }
+    rc = wce::launch_matvec(st->Mu, nullptr, h, hs, uw, nullptr, WS_LD, n, false, stream);   // u
+    if (!rc && c->mode == WCE_MMSE_REF) rc = wce::launch_ref_w(st, h, hs, ww, WS_LD, n, stream);   // w, pilot rows
     if (rc) return fail(rc, "matvec launch (frame covariance)");
     sa.cu = uw;
     sa.cw = c->mode == WCE_MMSE_REF ? ww : nullptr;
@@ -658,9 +647,14 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     if (fc) {
         const bool lt_ready = !fuse && (mask & WCE_EST_LT_LS) && !(out->flags & WCE_OUT_LS_F32);
         bool done = false;   // REF, C semantics: H written by the factor launch itself
-        rc = prep_frame_cov(c, in, out, lt_ready, !fuse, sa, ws, &done, stream);
+        rc = prep_frame_cov(c, in, out, lt_ready, sa, ws, &done, stream);
         if (rc) return rc;
-        if (done) return WCE_OK;
+        if (done && !fuse) return WCE_OK;
+        if (done) {   // the LS family + equalization still ride the one-element-per-thread pass
+            sa.mmse_done = 1;
+            rc = wce::launch_mmse_solve_ls(c->d_state, sa, la, stream);
+            return rc ? fail(rc, "ls epilogue launch") : WCE_OK;
+        }
     }
     double *aux = ws ? ws + (WS_ARRAYS - 1) * n * WS_LD * 2 : nullptr;
     if (split) {

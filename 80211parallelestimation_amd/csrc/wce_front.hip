@@ -52,9 +52,6 @@ __constant__ double2 kW64[64] = {
     {0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2}, {0x1.e9f4156c62ddap-1, 0x1.294062ed59f06p-2},
     {0x1.f6297cff75cb0p-1, 0x1.8f8b83c69a60bp-3}, {0x1.fd88da3d12526p-1, 0x1.917a6bc29b42cp-4}};
 
-#ifndef WCE_FE_NT_LOAD
-#define WCE_FE_NT_LOAD 0
-#endif
 // Memory policy per variant, chosen by interleaved A/B on the box
 // (tools/ab_front.py, profiles/r01_ab_front.txt): the block kernel stages its
 // bins through LDS and stores them as one run per wave, with nontemporal loads

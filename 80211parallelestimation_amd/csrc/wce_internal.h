@@ -14,7 +14,7 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
-constexpr int32_t STATE_LAYOUT = 7;   // State layout version: bump with every change to struct State
+constexpr int32_t STATE_LAYOUT = 8;   // State layout version: bump with every change to struct State
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
@@ -34,6 +34,11 @@ struct State {
     double Mg[CLD * CLD * 2];
     double Mu[CLD * CLD * 2];
     double Mw[CLD * CLD * 2];
+    // REF: w at the 4 pilot rows folded into one real map of h (round 5):
+    // w_p = sum_k Ar[p][k] re h_k + Ai[p][k] im h_k with Ar = Mw_P (re Mg - im Mg),
+    // Ai = -Mw_P (re Mg + im Mg), products in 80 bits (Mw_P = rows P of Mw);
+    // stored {Ar, Ai} pairs, Wp[2 (p NPAD + k)], zero past k = 52.
+    double Wp[4 * NPAD * 2];
     double cvec[NPAD * 2];     // rank-1 factors of the shared C = u w^T: u = cvec and
     double cwvec[NPAD * 2];    // w = conj(cvec) (TEXTBOOK: c = F ifft(H_LT)) or w = cwvec
                                // (REF: u = F g, w = FH^T q, main.c:186-203)
@@ -170,7 +175,7 @@ struct SolveArgs {
                               // writes W_b to w[g*ws] (or, with hout, cw . W_b to dots[g])
     double *dots;
     int32_t ref_pilots;       // REF (main.c): a = 0 and X = the 4 pilots -> mmse_ref_flat_kernel
-    int32_t pad;
+    int32_t mmse_done;        // H already written (REF frame covariance): the fused launch runs the LS family only
     const uint8_t *skip;      // per unit: nonzero = H already written (constant-modulus path); null = none
 };
 struct SynthArgs {
@@ -218,10 +223,12 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream);
 int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs &a, void *stream);
 // the kernel launch_mmse_lr runs for `units` (frame, block) units (wce_debug_lr_kernel)
 const char *lr_kernel_name(int k0, int rank, int taps, int64_t units);
-// REF + WCE_MMSE_FRAME_COV (C semantics) in one launch: LT_LS of rx_pre, u = Mu h,
-// w = Mw q(Mg h) at the pilot rows; hout: H = u s to a.w, else u / w rows to uw / ww
+// REF + WCE_MMSE_FRAME_COV (C semantics) in one launch: LT_LS of rx_pre, w at the
+// pilots from State::Wp, s, u = Mu h and H = u s to a.w
 int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
-                  double *uw, double *ww, int64_t wld, bool hout, void *stream);
+                  void *stream);
+// the same w as full rows W[f] (zero off the pilots) from h rows X[f] (the variant path)
+int launch_ref_w(const State *st, const double *X, int64_t xs, double *W, int64_t ws, int64_t n, void *stream);
 // H[f] = mean of X rows 4f .. 4f+3 (MATLAB block average, left to right)
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk

@@ -40,10 +40,7 @@ namespace wce {
 // LS family + equalization: one wave per frame, lane k = subcarrier k.
 // =====================================================================
 constexpr int LS_WAVES = 4;   // waves per 256-thread workgroup
-#ifndef WCE_LS_FRAMES
-#define WCE_LS_FRAMES 4
-#endif
-constexpr int LS_FRAMES = WCE_LS_FRAMES;  // frames per wave iteration: all loads issued up front
+constexpr int LS_FRAMES = 4;  // frames per wave iteration: all loads issued up front
 
 // Per-lane (subcarrier k) constants of the LS family, shared by ls_kernel and
 // the fused MMSE epilogue.
@@ -122,9 +119,6 @@ __device__ __forceinline__ void st_out(double *p, int64_t idx, double2 v, bool f
 
 // store the requested LS-family outputs of frame f, subcarrier k, and run
 // WiFi_Equalization.m:1-9 over the frame's 15 blocks rv (already loaded)
-#ifndef WCE_EQ_F32_MATH   // fp32 outputs: the equalizer's divisions in fp32 (0: fp64, rounded on the store)
-#define WCE_EQ_F32_MATH 1
-#endif
 template <bool EQ>
 __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, uint32_t mask, double2 hlt, double2 hlin,
                                             double2 hcub, double2 hsnc, const double2 (&rv)[NBLK])
@@ -138,7 +132,7 @@ __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, u
     if constexpr (EQ) {
         const double2 hps = a.eq_src == WCE_EST_PS_CUBIC ? hcub : (a.eq_src == WCE_EST_PS_SINC ? hsnc : hlin);
         const int64_t eb = f * a.eqfs + k;
-        if (f32 && WCE_EQ_F32_MATH) {
+        if (f32) {   // fp32 outputs: the equalizer's divisions in fp32
             // WCE_OUT_LS_F32 (BASELINE configs[4]'s fp32 interpolation stage): the
             // 15 divisions in fp32.  H_UTIL_b = hlt + ((b+1)/15)(hps - hlt) stays
             // fp64 (one fma per component: the blend cancels where the channel
@@ -172,12 +166,7 @@ __device__ __forceinline__ void ls_store_rv(const LsArgs &a, int64_t f, int k, u
         for (int b = 0; b < NBLK; b++) {
             const double wlt = (double)(NBLK - (b + 1)) / NBLK, wps = (double)(b + 1) / NBLK;
             const double2 hu = cadd(cscale(hlt, wlt), cscale(hps, wps));
-#ifdef WCE_ABLATE_EQ_VALU   // timing-only: store rx instead of rx / H (same traffic, no blend/division)
-            const double2 e = k == WCE_DC ? make_double2(0, 0) : rv[b];
-            (void)hu;
-#else
             const double2 e = k == WCE_DC ? make_double2(0, 0) : cdiv(rv[b], hu);
-#endif
             st_out(a.eq, eb + b * a.eqbs, e, f32);
         }
     }
@@ -202,17 +191,12 @@ __device__ __forceinline__ void ls_store(const LsArgs &a, int64_t f, int k, uint
 // LIGHT: the request is a subset of LT_LS | PS_Linear (BASELINE configs[1]);
 // the Cubic/Sinc constants and paths compile out, which keeps the kernel under
 // 128 VGPRs (4 waves/SIMD: twice the loads in flight of the generic kernel).
-#ifndef WCE_LS_PIPE   // LIGHT: loads of the next frame group issued before this group's math
-#define WCE_LS_PIPE 1
-#endif
-#ifndef WCE_LS_PIPE_FRAMES
-#define WCE_LS_PIPE_FRAMES 4
-#endif
+constexpr int LS_PIPE_FRAMES = 4;   // LIGHT: frames per group, the next group's loads issued before this group's math
 template <bool EQ, bool ML, bool LIGHT = false>
 __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, LsArgs a)
 {
-    constexpr bool PIPE = LIGHT && WCE_LS_PIPE;
-    constexpr int F = PIPE ? WCE_LS_PIPE_FRAMES : LS_FRAMES;   // frames per wave iteration
+    constexpr bool PIPE = LIGHT;
+    constexpr int F = PIPE ? LS_PIPE_FRAMES : LS_FRAMES;   // frames per wave iteration
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * LS_WAVES;
     const bool act = lane < NSC;
@@ -284,10 +268,7 @@ __global__ __launch_bounds__(256) void ls_kernel(const State *__restrict__ st, L
 // (mmse_ref_flat_kernel) and the non-finite scan.  (Round 1's ls_flat_kernel,
 // 512-element chunks per wave, was retired in round 4: profiles/r02_ab_ls.txt.)
 // =====================================================================
-#ifndef WCE_FLAT_U
-#define WCE_FLAT_U 8
-#endif
-constexpr int FLAT_U = WCE_FLAT_U;                      // elements per lane per chunk
+constexpr int FLAT_U = 8;                               // elements per lane per chunk
 constexpr int FLAT_CHUNK = 64 * FLAT_U;                 // 512
 constexpr int FLAT_FR = (FLAT_CHUNK - 1) / NSC + 2;     // frames one chunk can touch: 11
 static_assert(4 * FLAT_FR <= 64, "one pilot per lane");
@@ -485,15 +466,16 @@ __global__ __launch_bounds__(256) void ref_ls_elem_kernel(const State *__restric
     const bool shared = a.cs == 0;
     // ---- every load first
     const int64_t po = f * a.fs + (int64_t)a.blk * a.bs;
-    double2 xt[4], xr[4], wp[4];
+    const bool mm = !a.mmse_done;   // REF frame covariance: ref_fc_kernel wrote H already
+    double2 xt[4], xr[4], wp[4] = {};
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         xt[p] = ld2(a.tx, po + PILOT[p]);
         xr[p] = ld2(a.rx, po + PILOT[p]);
         const int64_t wo = shared ? PILOT[p] : f * a.cs + PILOT[p];
-        wp[p] = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
+        if (mm) wp[p] = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
     }
-    const double2 uk = ld2(a.cu, shared ? k : f * a.cs + k);
+    const double2 uk = mm ? ld2(a.cu, shared ? k : f * a.cs + k) : make_double2(0, 0);
     const double2 rp = l.rx_pre ? ld2_nt(l.rx_pre, f * l.ps + k) : make_double2(0, 0);
     double2 rv[NBLK];
     if constexpr (EQ) {
@@ -502,10 +484,12 @@ __global__ __launch_bounds__(256) void ref_ls_elem_kernel(const State *__restric
     }
     const LsLane c = ls_lane(st, l.tx_pre, k);
     // ---- PS_MMSE (REF): H = u s, s = w^T X rx / b over the 4 pilots
-    double2 tp[4];
+    if (mm) {
+        double2 tp[4];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) tp[p] = ref_term(wp[p], xt[p], xr[p]);
-    st2(a.w, f * a.ws + k, ref_out(uk, ref_sum4(tp[0], tp[1], tp[2], tp[3], 1.0 / st->bcoef)));
+        for (int p = 0; p < 4; ++p) tp[p] = ref_term(wp[p], xt[p], xr[p]);
+        st2(a.w, f * a.ws + k, ref_out(uk, ref_sum4(tp[0], tp[1], tp[2], tp[3], 1.0 / st->bcoef)));
+    }
     // ---- LS family + equalization
     double2 h[4];
 #pragma unroll
@@ -761,18 +745,7 @@ __device__ __forceinline__ void back_block(const double2 (&A)[RB][RB], double2 (
     for (int bb = 0; bb < BLK; ++bb) cmsub_conj(P[bb], zp, A[BLK][bb]);
 }
 
-#ifndef WCE_ABLATE_KEEP  // timing-only build: dense Cholesky without keeping L (with WCE_ABLATE_BACKSOLVE)
-#define WCE_ABLATE_KEEP 0
-#endif
-#ifndef WCE_ABLATE_RYY   // timing-only build: Ryy = b I (no C loads, no build)
-#define WCE_ABLATE_RYY 0
-#endif
-#ifndef WCE_SOLVE_WAVES_PER_SIMD
-#define WCE_SOLVE_WAVES_PER_SIMD 3
-#endif
-#ifndef WCE_DENSE_WAVES_PER_SIMD
-#define WCE_DENSE_WAVES_PER_SIMD WCE_SOLVE_WAVES_PER_SIMD
-#endif
+constexpr int SOLVE_WAVES_PER_SIMD = 3;   // the per-frame solve kernels (rank-1 and dense C)
 // Dense C, scaled form.  Ryy = a X C X^H + b I = a X M X^H with
 // M = C + diag(b / (a |x_i|^2)), so Ryy^-1 rx = X^-H M^-1 y / a, y = X^-1 rx,
 // and W = X z = (x / (a conj x)) o (M^-1 y).  M is C itself off the diagonal:
@@ -1028,7 +1001,7 @@ __device__ __forceinline__ void chol_panels_keep(double2 (&A)[RB][RB], double2 (
                                                  int p, int q, int lane, double &rsel)
 {
     if constexpr (KB < RB - 1) {
-        chol_panel<KB, 0, !WCE_ABLATE_KEEP>(A, P, R, s, p, q, lane, rsel);
+        chol_panel<KB, 0, true>(A, P, R, s, p, q, lane, rsel);
         chol_panels_keep<KB + 1>(A, P, R, s, p, q, lane, rsel);
     }
 }
@@ -1217,7 +1190,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     const int p = lane >> 3, q = lane & 7;
     const double ac = st->acoef, bc = st->bcoef;
     double2 A[RB][RB];
-    const bool cbuild = !FC && ac != 0.0 && !WCE_ABLATE_RYY;
+    const bool cbuild = !FC && ac != 0.0;
     {
         const bool act = lane < NSC;
         const double2 t = !act ? make_double2(0, 0) : ld2(a.tx, base + lane);
@@ -1297,13 +1270,6 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     const bool brow = (p == NSC - 8 * (RB - 1));
 #pragma unroll
     for (int bb = 0; bb < RB; ++bb) P[bb] = brow ? cconj(A[RB - 1][bb]) : make_double2(0, 0);
-#ifdef WCE_ABLATE_BACKSOLVE   // timing-only build: skip the back-substitution
-#pragma unroll
-    for (int aa = 0; aa < RB; ++aa)
-#pragma unroll
-        for (int bb = 0; bb <= aa; ++bb) asm volatile("" ::"v"(A[aa][bb].x), "v"(A[aa][bb].y));
-    if (lane < NSC) s.z[lane] = P[lane & 7];
-#else
     back_block<6>(A, P, rq, s, p, q, lane);
     back_block<5>(A, P, rq, s, p, q, lane);
     back_block<4>(A, P, rq, s, p, q, lane);
@@ -1311,7 +1277,6 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     back_block<2>(A, P, rq, s, p, q, lane);
     back_block<1>(A, P, rq, s, p, q, lane);
     back_block<0>(A, P, rq, s, p, q, lane);
-#endif
     wave_lds_sync();
     const double2 xl = s.x[lane];
     if (cbuild) {   // W = (x / (a conj x)) o (M^-1 y)
@@ -1326,7 +1291,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 // instead of the dense State::C (COV mode, or a = 0).
 // split (MATLAB averaging): one wave per (frame, block), W_b to row g of a.w.
 template <bool R1>
-__global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
+__global__ __launch_bounds__(64, SOLVE_WAVES_PER_SIMD) void mmse_solve_kernel(const State *__restrict__ st, SolveArgs a)
 {
     __shared__ SolveLds s;
     const int64_t g = blockIdx.x;
@@ -1363,9 +1328,7 @@ __global__ __launch_bounds__(64, WCE_DENSE_WAVES_PER_SIMD) void mmse_solve_kerne
 // Gram tiles, 1.25-1.33x slower, were retired in round 4:
 // profiles/r03_ab_lowrank_dense.txt.)
 // =====================================================================
-#ifndef WCE_LR_WAVES_PER_SIMD   // K0 >= 2 (<= 122 VGPRs); 12 KB of LDS per wave caps a CU at 13 waves anyway
-#define WCE_LR_WAVES_PER_SIMD 4
-#endif
+constexpr int LR_WAVES_PER_SIMD = 4;   // K0 >= 2 (<= 122 VGPRs); 12 KB of LDS per wave caps a CU at 13 waves anyway
 // Gram column j of G~ at subcarrier k: x_k U[k][j] (U is zero past column
 // r - 1), rx_k at the border column j = 53 - 8 K0, 0 past it.
 template <int K0, typename L = SolveLds>
@@ -1528,12 +1491,6 @@ __device__ __forceinline__ double2 lr_solve(const State *__restrict__ st, const 
 // lambda_t, then a fourth.  E[k d mod 53] is gathered from LDS by the exact
 // index recurrence (no phase accumulation).
 // ---------------------------------------------------------------------
-#ifndef WCE_TAPS_UNROLL
-#define WCE_TAPS_UNROLL 2
-#endif
-#ifndef WCE_TAPS_SPLIT   // the Q / D DFTs over half the pairs per half-wave, outputs d and 53 - d together
-#define WCE_TAPS_SPLIT 1
-#endif
 // Every DFT here runs over pairs (k, 53 - k): E[(53 - k) m] = conj(E[k m]), so
 //     c_k E[km] + c_{53-k} conj(E[km]) = (c_k + c_{53-k}) Re E[km] + i (c_k - c_{53-k}) Im E[km]
 // -- one gather and half the FMAs and index steps of the plain sum.
@@ -1558,31 +1515,11 @@ __device__ __forceinline__ double2 ld_e(const double2 *e, uint32_t o)
 {
     return *reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(e) + o);
 }
-template <bool CONJ>
-__device__ __forceinline__ double2 lr_dft53p(const double2 *e, const double2 *pa, const double2 *pb, double2 c0, int m)
-{
-    double2 y = c0;
-    const uint32_t st = 16u * (uint32_t)m, sw = st - 16u * NSC;
-    uint32_t o = st;   // 16 (k m mod 53) at k = 1 (m < 53)
-#pragma unroll WCE_TAPS_UNROLL
-    for (int k = 1; k <= NSC / 2; ++k) {
-        const double2 w = ld_e(e, o), A = pa[k], B = pb[k];
-        const double wy = CONJ ? -w.y : w.y;
-        y.x = fma(A.x, w.x, fma(-B.y, wy, y.x));
-        y.y = fma(A.y, w.x, fma(B.x, wy, y.y));
-        o = dft_step(o, st, sw);
-    }
-    return y;
-}
-
-// The same sum as lr_dft53p, outputs m and 53 - m together (E[k (53 - m)] =
+// y(m) = c_0 + sum_k (pa_k Re E[k m] + i pb_k Im E[k m]) over the pairs (k, 53 - k), outputs m and 53 - m together (E[k (53 - m)] =
 // conj(E[k m]): A = sum pa_k Re E, B = i sum pb_k Im E (CONJ: -Im), y(m) = c_0 + A
 // + B, y(53 - m) = c_0 + A - B), half-wave h over the pairs k = 1 + 13 h ..
 // 13 + 13 h; the halves meet in xs (>= 59 entries of free LDS), which ends up
 // holding y, returned on lane m (lanes past 52: y(0)).
-#ifndef WCE_TAPS_SPLIT_OUT
-#define WCE_TAPS_SPLIT_OUT 1
-#endif
 template <bool CONJ>
 __device__ __forceinline__ double2 lr_dft53_split(const double2 *e, const double2 *pa, const double2 *pb, double2 c0,
                                                   int lane, double2 *xs)
@@ -1594,7 +1531,7 @@ __device__ __forceinline__ double2 lr_dft53_split(const double2 *e, const double
     const uint32_t st = 16u * (uint32_t)dd, sw = st - 16u * NSC;
     uint32_t o = 16u * (uint32_t)((k0 * dd) % NSC);
     double2 A = make_double2(0.0, 0.0), B = A;
-#pragma unroll WCE_TAPS_UNROLL
+#pragma unroll 2
     for (int j = 0; j < NSC / 4; ++j) {
         const int k = k0 + j;
         const double2 w = ld_e(e, o), va = pa[k], vb = pb[k];
@@ -1644,11 +1581,6 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
     }
     wave_lds_sync();
     // Q(d) = sum_k p_k conj(E[k d]), D(d) = sum_k v_k E[k d] on lane d
-    double2 Qd = make_double2(s.rd[0], 0.0), Dd = s.u[1][0];
-#ifdef WCE_ABLATE_TAPS_DFT   // timing-only: no Q / D DFTs
-    Qd = make_double2(s.rd[lane], 0.0);
-    Dd = s.u[1][lane];
-#elif WCE_TAPS_SPLIT
     // Outputs d and 53 - d share every gather: E[k (53 - d)] = conj(E[k d]), so
     // with A = sum pa_k Re E[k d] and B = i sum pb_k Im E[k d] (over the pairs),
     // D(d) = v_0 + A + B and D(53 - d) = v_0 + A - B; Q(53 - d) = conj(Q(d)).
@@ -1663,7 +1595,7 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
         const uint32_t st = 16u * (uint32_t)dd, sw = st - 16u * NSC;
         uint32_t o = 16u * (uint32_t)((k0 * dd) % NSC);
         double2 q = make_double2(0.0, 0.0), A = q, B = q;
-#pragma unroll WCE_TAPS_UNROLL
+#pragma unroll 2
         for (int j = 0; j < NSC / 4; ++j) {
             const int k = k0 + j;
             const double2 w = ld_e(s.u[0], o), va = s.tp.pa[k], vb = s.tp.pb[k];
@@ -1699,22 +1631,6 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
             }
         }
     }
-#else
-    {
-        const uint32_t st = 16u * (uint32_t)(act ? lane : 0), sw = st - 16u * NSC;
-        uint32_t o = st;
-#pragma unroll WCE_TAPS_UNROLL
-        for (int k = 1; k <= NSC / 2; ++k) {
-            const double2 w = ld_e(s.u[0], o), va = s.tp.pa[k], vb = s.tp.pb[k];
-            const double2 pp = s.tp.rp[k];   // {p_k + p_{53-k}, p_k - p_{53-k}}
-            Qd.x = fma(pp.x, w.x, Qd.x);
-            Qd.y = fma(-pp.y, w.y, Qd.y);
-            Dd.x = fma(va.x, w.x, fma(-vb.y, w.y, Dd.x));
-            Dd.y = fma(va.y, w.x, fma(vb.x, w.y, Dd.y));
-            o = dft_step(o, st, sw);
-        }
-    }
-#endif
     wave_lds_sync();   // every lane's reads of u[1] / the pair tables are done
     // The system is factorised in the scaled form M = S^-1 (a Gamma + b I) S^-1
     // = a T + b S^-2 (T_ij = Q(t_i - t_j)), bordered by S^-1 beta = conj(D(t_j)):
@@ -1723,10 +1639,6 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
     // Sluis; the dense path's scaled form, s5), and every element is a plain
     // gather of a Q (pre-scaled by a) instead of a product of three factors.
     // Padding columns j in [r, RMAX): pivot b, zero border -> w_j = 0.
-#if !WCE_TAPS_SPLIT || defined(WCE_ABLATE_TAPS_DFT)
-    s.blk[lane] = cscale(Qd, ac);
-    s.z[lane] = Dd;
-#endif
     int *tapl = reinterpret_cast<int *>(s.u[1]);   // column j -> its tap (256 B of u[1]) ...
     double *bl = reinterpret_cast<double *>(tapl + 64);   // ... and M's diagonal term b / lambda_j (b past r)
     const int r = st->cov_rank;
@@ -1813,37 +1725,20 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     wave_lds_sync();
     dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
     wave_lds_sync();
-    const int kk = act ? lane : 0;
     const double2 xl = s.x[lane];   // re-read: nothing of the frame stays live across the factorisation
-#ifdef WCE_ABLATE_TAPS_OUT   // timing-only: no read-out DFT
-    double2 y = s.u[1][kk];
-#else
-#if WCE_TAPS_SPLIT_OUT
     double2 y = lr_dft53_split<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z);   // y_k = sum_t c_t E[k t]
-#else
-    double2 y = lr_dft53p<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], kk);   // y_k = sum_t c_t E[k t]
-#endif
-#endif
     if (__ballot(act && xl.y != 0.0) != 0) {   // complex symbols: y += U U^H [(x - conj x) o rho] / b
         const double2 rho = csub(s.rx[lane], cscale(cmul(xl, y), ac));   // b Ryy^-1 rx
         s.blk[lane] = act ? make_double2(-2.0 * xl.y * rho.y, 2.0 * xl.y * rho.x) : make_double2(0, 0);
         wave_lds_sync();   // (also: every lane's read-out reads of the pair tables are done)
         dft_pairs(s.blk, s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
-#if WCE_TAPS_SPLIT_OUT
         const double2 w = lr_dft53_split<true>(s.u[0], s.tp.pa, s.tp.pb, s.blk[0], lane, s.z);   // w_t = sum_k conj(E[k t]) v_k
-#else
-        const double2 w = lr_dft53p<true>(s.u[0], s.tp.pa, s.tp.pb, s.blk[0], kk);   // w_t = sum_k conj(E[k t]) v_k
-#endif
         s.u[1][lane] = act ? cscale(w, ts * ts / bc) : make_double2(0.0, 0.0);
         wave_lds_sync();
         dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
-#if WCE_TAPS_SPLIT_OUT
         y = cadd(y, lr_dft53_split<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z));
-#else
-        y = cadd(y, lr_dft53p<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], kk));
-#endif
     }
     return y;
 }
@@ -1853,20 +1748,16 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
 // K0 = 0 (r > 45: a Gram system as large as Ryy itself) holds all 28
 // register blocks through the product build: 2 waves/SIMD; K0 = 1: 156.
 // TAPS: the tap-domain Gram (State::cov_taps), registers as the dense solve's.
-#ifndef WCE_TAPS_WAVES_K0   // the tap form at K0 = 0 (168 VGPRs, 13 spilled at 3 waves/SIMD)
-#define WCE_TAPS_WAVES_K0 WCE_DENSE_WAVES_PER_SIMD
-#endif
+constexpr int TAPS_WAVES_K0 = SOLVE_WAVES_PER_SIMD;   // the tap form at K0 = 0 (168 VGPRs, 13 spilled at 3 waves/SIMD)
 // K0 >= 2: the LDS holds only rows 8 K0 .. 55 of the panel transposes
 // (SolveLdsT<8 K0>: 9.9 KB per wave at K0 = 2 instead of 12.2), so 4 waves per
 // SIMD fit a CU's 160 KB where 3.25 did.
 constexpr int lr_row0(int k0) { return k0 >= 2 ? 8 * k0 : 0; }
-#ifndef WCE_LR_TAPS_WAVES   // the tap form at K0 >= 2 (<= 118 VGPRs)
-#define WCE_LR_TAPS_WAVES 4
-#endif
+constexpr int LR_TAPS_WAVES = 4;   // the tap form at K0 >= 2 (<= 118 VGPRs)
 constexpr int lr_waves(int k0, bool taps)
 {
-    return taps ? (k0 == 0 ? WCE_TAPS_WAVES_K0 : (k0 == 1 ? WCE_DENSE_WAVES_PER_SIMD : WCE_LR_TAPS_WAVES))
-                : (k0 == 0 ? 2 : (k0 <= 2 ? 3 : WCE_LR_WAVES_PER_SIMD));
+    return taps ? (k0 == 0 ? TAPS_WAVES_K0 : (k0 == 1 ? SOLVE_WAVES_PER_SIMD : LR_TAPS_WAVES))
+                : (k0 == 0 ? 2 : (k0 <= 2 ? 3 : LR_WAVES_PER_SIMD));
 }
 template <int K0, bool TAPS = false>
 __global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
@@ -1918,12 +1809,9 @@ __global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const S
 //    in chunks of 8 subcarriers (8 frames x 128 B per store, 7 stores per
 //    frame instead of 14 of 64 B): rank 8 0.055 -> 0.046 ms at 65,536 frames,
 //    2.7-4% at 1,048,576, bit-identical (profiles/r04_ab_lowrank_store8.txt).
-#ifndef WCE_LR_LANE_UNROLL   // direct form without the look-ahead: subcarriers per step up to rank 4
-#define WCE_LR_LANE_UNROLL 4
-#endif
-#ifndef WCE_LR_LDS_P   // direct form: P_k and U staged in LDS per workgroup instead of scalar loads, for the ranks whose bit is set
-#define WCE_LR_LDS_P 0x110   // ranks 4 and 8 (measured per rank, profiles/r03_ab_lowrank_ldsp.txt)
-#endif
+constexpr int LR_LANE_UNROLL = 4;   // direct form without the look-ahead: subcarriers per step up to rank 4
+constexpr int LR_LDS_P = 0x110;     // direct form: P_k and U staged in LDS per workgroup instead of scalar loads, for the
+                                    // ranks whose bit is set: 4 and 8 (measured per rank, profiles/r03_ab_lowrank_ldsp.txt)
 constexpr int LRL_KC = 4;                         // subcarriers per chunk
 constexpr int LRL_NCH = (NSC + LRL_KC - 1) / LRL_KC;   // 14 chunks (k = 52..55: only 52 is live)
 constexpr int LRL_LS = 5;                         // LDS row stride (complex) per frame
@@ -1981,18 +1869,12 @@ __device__ __forceinline__ void lrl_sweep(LrLaneLds *sp, const SolveArgs &a, con
             }
         }
     } else {
-#ifdef WCE_LR_ABLATE_LOADS   // timing-only build: one sector of the frame, reused for every k
-        const double2 x0 = ld2(a.tx, base), r0 = ld2(a.rx, base);
-#pragma unroll UN
-        for (int k = 0; k < NSC; ++k) fn(k, x0, r0);
-#else
 #pragma unroll UN
         for (int k = 0; k < NSC; ++k)
             fn(k, own ? ld2(a.tx, base + k) : make_double2(0.0, 0.0), own ? ld2(a.rx, base + k) : make_double2(0.0, 0.0));
-#endif
     }
 }
-// Pl / Ul (WCE_LR_LDS_P, direct form): the workgroup's LDS copies of P_k
+// Pl / Ul (LR_LDS_P, direct form): the workgroup's LDS copies of P_k
 // (R (R + 1) / 2 entries per k) and U (R per k); else State::Pk / State::U
 // TQ (State::taps_contig, staged form with LDS tables): Pl holds E[k s mod 53]
 // (R per k) instead of P_k, and pass 1 accumulates the Toeplitz Gram's R
@@ -2043,7 +1925,7 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
 #pragma unroll
     for (int e = 0; e < NO; ++e) go[e] = make_double2(0.0, 0.0);
     bool cplx = false;
-    constexpr int UN = R <= 4 ? WCE_LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
+    constexpr int UN = R <= 4 ? LR_LANE_UNROLL : 1;   // ranks 5..8: the Gram registers leave no room
     if constexpr (TQ) {
         double q0 = 0.0;                      // Q(0) (real)
         double2 qs[R > 1 ? R - 1 : 1];        // Q(1..R-1)
@@ -2201,19 +2083,14 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
         }
     } else {
         double *W = a.w + 2 * g * a.ws;
-#ifdef WCE_LR_ABLATE_STORES   // timing-only build: H_0 alone
-        st2(W, 0, hk(0));
-#else
 #pragma unroll 4
         for (int k = 0; k < NSC; ++k) st2(W, k, hk(k));
-#endif
     }
 }
 template <int R>
 __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restrict__ st, SolveArgs a, int fpw)
 {
-#if WCE_LR_LDS_P
-    if constexpr (((WCE_LR_LDS_P >> R) & 1) != 0) {
+    if constexpr (((LR_LDS_P >> R) & 1) != 0) {
     // P_k and U through LDS: their scalar loads each wait a round trip per k
     // (18 s_load_dwordx16 per k at rank 8, and rank 8's 30 KB of P_k does not
     // stay in the scalar cache), fully exposed at one wave per SIMD.  Per rank
@@ -2232,18 +2109,16 @@ __global__ __launch_bounds__(256) void mmse_lr_lane_kernel(const State *__restri
     } else {
         lr_lane_body<R, false>(st, a, nullptr, fpw);
     }
-#else
-    lr_lane_body<R, false>(st, a, nullptr, fpw);   // (no LDS)
-#endif
 }
-#ifndef WCE_LR_STAGED_LDS_P   // staged form: 4-wave workgroups sharing one LDS copy of P_k and U, for the ranks whose bit is set
-#define WCE_LR_STAGED_LDS_P 0x1fe   // every rank: 1,048,576 frames, rank 8 1476 -> 951 us, 7 1343 -> 875, 6 1189 -> 845,
-                                    // 5 894 -> 840, 2 952 -> 934, 4 equal (profiles/r03_ab_lowrank_ldsp.txt)
-#endif
-#ifndef WCE_LR_STAGED_MINWG   // 4-wave workgroups per CU asked of the register allocator, ranks >= 7, batches past one wave per SIMD
-#define WCE_LR_STAGED_MINWG 2   // 1,048,576 frames: rank 7 898 -> 858 us, rank 8 955 -> 896 (2 waves/SIMD instead of 1; rank 8
-#endif                          // spills 52 B); at 65,536 frames (one wave per SIMD anyway) rank 8 63.3 -> 67.5, so MW = 1 there
-constexpr int lr_staged_threads(int r) { return ((WCE_LR_STAGED_LDS_P >> r) & 1) ? 256 : 64; }
+// staged form: 4-wave workgroups sharing one LDS copy of P_k and U, for the ranks whose bit is set: every rank
+// (1,048,576 frames, rank 8 1476 -> 951 us, 7 1343 -> 875, 6 1189 -> 845, 5 894 -> 840, 2 952 -> 934, 4 equal;
+// profiles/r03_ab_lowrank_ldsp.txt)
+constexpr int LR_STAGED_LDS_P = 0x1fe;
+// 4-wave workgroups per CU asked of the register allocator, ranks >= 7, batches past one wave per SIMD.
+// 1,048,576 frames: rank 7 898 -> 858 us, rank 8 955 -> 896 (2 waves/SIMD instead of 1; rank 8 spills 52 B);
+// at 65,536 frames (one wave per SIMD anyway) rank 8 63.3 -> 67.5, so MW = 1 there
+constexpr int LR_STAGED_MINWG = 2;
+constexpr int lr_staged_threads(int r) { return ((LR_STAGED_LDS_P >> r) & 1) ? 256 : 64; }
 template <int R, int MW = 1, bool TQ = false>
 __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_kernel(const State *__restrict__ st, SolveArgs a)
 {
@@ -2579,7 +2454,7 @@ __global__ __launch_bounds__(256) void avg_blocks_kernel(const double *__restric
 // LS path overlaps the VALU-bound solve instead of running as its own pass.
 // C semantics, one block.  FC: per-frame covariance (H written directly).
 template <bool R1, bool HOUT, bool EQ>
-__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_kernel(const State *__restrict__ st,
+__global__ __launch_bounds__(64, SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_kernel(const State *__restrict__ st,
                                                                                     SolveArgs a, LsArgs l)
 {
     __shared__ SolveLds s;
@@ -2616,7 +2491,7 @@ __global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_ls_ke
 // bordered row (solve_block<., DOT>) -- no back-substitution, no C W GEMM.
 // split (MATLAB): one wave per (frame, block) writes its s_b to dots[g];
 // fc_finish averages.
-__global__ __launch_bounds__(64, WCE_SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_kernel(const State *__restrict__ st,
+__global__ __launch_bounds__(64, SOLVE_WAVES_PER_SIMD) void mmse_solve_fc_kernel(const State *__restrict__ st,
                                                                                     SolveArgs a)
 {
     __shared__ SolveLds s;
@@ -2746,142 +2621,6 @@ __global__ __launch_bounds__(256) void matvec_kernel(const double *__restrict__ 
                 }
             }
         }
-    }
-}
-
-// =====================================================================
-// REF per-frame covariance in one launch (WCE_MMSE_FRAME_COV with
-// WCE_MMSE_REF, C semantics; round 4).  main.c's PS_MMSE consumes the
-// frame's own H_EST_LT_LS (main.c:37-53, 148): g = invF h, Rhh = g q(g)^T,
-// C = F Rhh FH = u w^T with u = F invF h = Mu h and w = Mw q(g), and with
-// Ryy = 2 ow2 I and X the 4 pilots, H = u s, s = sum_p w_p x_p rx_p / b
-// (main.c:186-205).  Only w at the pilot rows P = {5, 19, 33, 47} is ever
-// read.  Per 16-frame tile (one wave):
-//   h = LT_LS(tx_pre, rx_pre_f)            ls_elem_kernel's formula, in the
-//                                          MFMA A layout (frame l&15, j = 4s + (l>>4))
-//   g = Mg h, u = Mu h                     matvec_kernel's 3M chains, same order
-//   q(g) = re g - im g                     through LDS into the A layout
-//   w_P = Mw[P, :] q(g)                    matvec_kernel<QIN>'s chain, output
-//                                          blocks 0..2 only (rows 5, 19, 33, 47)
-//   HOUT: s and H = u s                    ref_term / ref_sum4 / ref_out (the REF kernels' order)
-//   else: u and w_P to the workspace       for ref_ls_elem_kernel (the LS outputs)
-// Every value is rounded exactly as the four launches it replaces (LT_LS pass,
-// the g/u matvec, the w matvec, the REF read-out) round it, so H is
-// bit-identical to them; g never goes to HBM and w is formed for 4 rows of 53.
-// =====================================================================
-struct RefFcLds {
-    double q[16][64 + 1];   // q(g) of the tile's 16 frames (row stride 65: the transposing reads spread over banks)
-    double2 w[16][4];       // w at the 4 pilots, per frame
-    double2 s[16];          // s per frame
-};
-template <bool HOUT>
-__global__ __launch_bounds__(256) void ref_fc_kernel(const State *__restrict__ st, SolveArgs a,
-                                                     const double *__restrict__ rx_pre, int64_t ps,
-                                                     const double *__restrict__ tx_pre, double *uw, double *ww,
-                                                     int64_t wld)
-{
-    __shared__ RefFcLds lds[APPLY_WAVES];
-    const int lane = threadIdx.x & 63;
-    RefFcLds &L = lds[threadIdx.x >> 6];
-    const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
-    if (f0 >= a.n) return;
-    const int ml = lane & 15, kl = lane >> 4;
-    const int64_t fa = f0 + ml;
-    const double *txp = tx_pre ? tx_pre : st->tx_pre;
-    // ---- h = LT_LS of the frame's own preamble (main.c:66-75), A layout
-    double ar[KSTEPS], ai[KSTEPS];
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-        const int j = 4 * s + kl;
-        double2 h = make_double2(0, 0);
-        if (fa < a.n && j < NSC) {
-            const double2 rp = ld2_nt(rx_pre, fa * ps + j);
-            const double2 t = ld2(txp, j);
-            const double cq = t.x - t.y;
-            h = cdiv(make_double2(cq * rp.x, cq * rp.y), make_double2(cq * t.x, cq * t.y));
-            if (j == WCE_DC) h = make_double2(0, 0);
-        }
-        ar[s] = h.x;
-        ai[s] = h.y;
-    }
-    // one 16-row output block of M h for the tile: matvec_kernel's 3M chains and order
-    auto mh = [&](const double *M, int nt, v4d &accr, v4d &acci) {
-        const int i = 16 * nt + ml;
-        v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
-#pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) {
-            const double2 c = ld2(M, i * CLD + 4 * s + kl);   // zero-padded 64 x 64
-            p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], c.x, p1, 0, 0, 0);
-            p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s], c.y, p2, 0, 0, 0);
-            p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s] + ai[s], c.x + c.y, p3, 0, 0, 0);
-        }
-        accr = p1 - p2;
-        acci = (p3 - p1) - p2;
-    };
-    // ---- g = Mg h, straight to q(g) = re - im in LDS (transposed)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int i = 16 * nt + ml;
-        v4d gr, gi;
-        mh(st->Mg, nt, gr, gi);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) L.q[kl + 4 * r][i] = i < NSC ? gr[r] - gi[r] : 0.0;   // matvec reads rows < 53 only
-        __builtin_amdgcn_sched_barrier(0);   // one block's C loads in flight at a time (no 4-block hoist)
-    }
-    wave_lds_sync();
-    // ---- w = Mw q(g) at the pilot rows: matvec_kernel<QIN>'s accr chain, blocks 0..2
-    {
-        double qa[KSTEPS];
-#pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) qa[s] = L.q[ml][4 * s + kl];
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt) {
-            const int i = 16 * nt + ml;
-            v4d accr = {0, 0, 0, 0};
-#pragma unroll
-            for (int s = 0; s < KSTEPS; ++s)
-                accr = __builtin_amdgcn_mfma_f64_16x16x4f64(qa[s], st->Mw[2 * (i * CLD + 4 * s + kl)], accr, 0, 0, 0);
-            const int p = i == WCE_P0 ? 0 : i == WCE_P1 ? 1 : i == WCE_P2 ? 2 : i == WCE_P3 ? 3 : -1;
-            if (p >= 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) L.w[kl + 4 * r][p] = make_double2(accr[r], 0.0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    wave_lds_sync();
-    const int pil = kl == 0 ? WCE_P0 : kl == 1 ? WCE_P1 : kl == 2 ? WCE_P2 : WCE_P3;
-    if constexpr (HOUT) {
-        // ---- s = w^T X rx / b over the 4 pilots of the frame's block (lane: frame ml, pilot kl)
-        double2 t = make_double2(0, 0);
-        if (fa < a.n) {
-            const int64_t o = fa * a.fs + (int64_t)a.blk * a.bs + pil;
-            t = ref_term(L.w[ml][kl], ld2(a.tx, o), ld2(a.rx, o));
-        }
-        L.w[ml][kl] = t;   // (each lane rewrites only its own slot)
-        wave_lds_sync();
-        if (kl == 0) L.s[ml] = ref_sum4(L.w[ml][0], L.w[ml][1], L.w[ml][2], L.w[ml][3], 1.0 / st->bcoef);
-        wave_lds_sync();
-    } else if (fa < a.n) {
-        st2(ww, fa * wld + pil, L.w[ml][kl]);   // w at the pilot rows, for ref_ls_elem_kernel
-    }
-    // ---- u = Mu h, block by block: H = u s (HOUT), or u to the workspace
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int i = 16 * nt + ml;
-        v4d ur, ui;
-        mh(st->Mu, nt, ur, ui);
-        if (i < NSC) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t fr = f0 + kl + 4 * r;
-                if (fr >= a.n) continue;
-                const double2 uv = make_double2(ur[r], ui[r]);
-                if constexpr (HOUT) st2(a.w, fr * a.ws + i, ref_out(uv, L.s[kl + 4 * r]));
-                else st2(uw, fr * wld + i, uv);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -3136,17 +2875,13 @@ static int hip_status(hipError_t e) { return e == hipSuccess ? WCE_OK : WCE_EHIP
 
 // A/B kernel variants, process-wide (wce_debug_set_variant): lets one process
 // time two kernels on the same buffers, interleaved.  Defaults = the product.
-#ifndef WCE_LR_FPW   // mmse_lr_lane_kernel (direct): units per wave at or below WCE_LR_FPW_BELOW units
-#define WCE_LR_FPW 64
-#endif
-#ifndef WCE_LR_FPW_BELOW
-#define WCE_LR_FPW_BELOW 131072
-#endif
-#ifndef WCE_LR_STAGE_FROM   // mmse_lr_lane_kernel: the LDS-staged form past this many (frame, block) units
-#define WCE_LR_STAGE_FROM 0   // round 3, with P_k / U shared in LDS (WCE_LR_STAGED_LDS_P) the staged form wins at every size:
-                             // 65,536 frames rank 4 52.1 -> 37.2 us, 5 63.1 -> 40.8, 6 65.8 -> 46.8, 7 75.4 -> 53.0, 8 68.1 -> 64.4
-                             // (before the LDS sharing: rank 4 direct 51.6 vs staged ~60 at 65,536, so 98,304 then)
-#endif
+constexpr int LR_FPW = 64;             // mmse_lr_lane_kernel (direct): units per wave at or below LR_FPW_BELOW units
+constexpr int64_t LR_FPW_BELOW = 131072;
+// mmse_lr_lane_kernel: the LDS-staged form past this many (frame, block) units.  Round 3, with P_k / U shared
+// in LDS (LR_STAGED_LDS_P) the staged form wins at every size: 65,536 frames rank 4 52.1 -> 37.2 us,
+// 5 63.1 -> 40.8, 6 65.8 -> 46.8, 7 75.4 -> 53.0, 8 68.1 -> 64.4 (before the LDS sharing: rank 4 direct 51.6 vs
+// staged ~60 at 65,536, so 98,304 then)
+constexpr int64_t LR_STAGE_FROM = 0;
 static int g_variant[WCE_VARIANT_COUNT] = {0, 2, 0, 0, 0};
 int set_variant(int which, int value)
 {
@@ -3251,17 +2986,17 @@ static LrForm lr_form(int rank, int64_t units)
     int lv = variant(WCE_VARIANT_LR);
     if (lv == 5) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), not the kernel form
     if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
-        // the LDS-staged form at every size by default (WCE_LR_STAGE_FROM = 0);
+        // the LDS-staged form at every size by default (LR_STAGE_FROM = 0);
         // the direct form runs only as variant 2, the gate's independent check
         // of the staging (tests/test_cov_lowrank_gpu.py)
-        const bool staged = lv >= 3 || (lv == 0 && units > (int64_t)WCE_LR_STAGE_FROM);
+        const bool staged = lv >= 3 || (lv == 0 && units > LR_STAGE_FROM);
         if (!staged) return LrForm::Direct;
         if (lr_staged_threads(rank) != 256) return LrForm::Staged64;
-        // ranks 7, 8: the two-workgroups-per-CU build (MW = WCE_LR_STAGED_MINWG)
+        // ranks 7, 8: the two-workgroups-per-CU build (MW = LR_STAGED_MINWG)
         // past one 64-unit wave per SIMD; variant 3 forces the MW = 1 build and
         // variant 4 the MW = 2 build at any size, so the gate checks both
         const bool many = lv == 4 || (lv == 0 && units > 64 * 4 * (int64_t)cu_count());
-        return rank >= 7 && WCE_LR_STAGED_MINWG > 1 && many ? LrForm::StagedMW : LrForm::Staged;
+        return rank >= 7 && LR_STAGED_MINWG > 1 && many ? LrForm::StagedMW : LrForm::Staged;
     }
     if (rank > LRL_RMAX && rank <= 16 && lv == 0) return LrForm::Quad;
     return LrForm::Wave;
@@ -3299,7 +3034,7 @@ const char *lr_kernel_name(int k0, int rank, int taps, int64_t units)
         "mmse_lr_lane_staged_kernel<3, 1, true>", "mmse_lr_lane_staged_kernel<4, 1, true>",
         "mmse_lr_lane_staged_kernel<5, 1, true>", "mmse_lr_lane_staged_kernel<6, 1, true>",
         "mmse_lr_lane_staged_kernel<7, 1, true>", "mmse_lr_lane_staged_kernel<8, 1, true>"};
-    static_assert(WCE_LR_STAGED_MINWG == 2 || WCE_LR_STAGED_MINWG <= 1, "lr_kernel_name spells MW = 2");
+    static_assert(LR_STAGED_MINWG == 2 || LR_STAGED_MINWG <= 1, "lr_kernel_name spells MW = 2");
     const int r = rank < 1 ? 1 : (rank > LRL_RMAX ? LRL_RMAX : rank);
     switch (lr_form(rank, units)) {
     case LrForm::Direct: return lane[0][r];
@@ -3321,17 +3056,17 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
     const LrForm form = lr_form(rank, waves);
     if (form == LrForm::Direct || form == LrForm::Staged64 || form == LrForm::Staged || form == LrForm::StagedMW) {
         // direct form: fewer units per wave on a small batch (latency-bound at one wave per SIMD)
-        const int fpw = waves <= (int64_t)WCE_LR_FPW_BELOW ? WCE_LR_FPW : 64;
+        const int fpw = waves <= LR_FPW_BELOW ? LR_FPW : 64;
         const int64_t dw = (waves + fpw - 1) / fpw;
         const dim3 gs((unsigned)((waves + 63) / 64)), bs(64), gd((unsigned)((dw + 3) / 4)), bd(256);
-        const dim3 gs4((unsigned)((waves + 255) / 256)), bs4(256);   // staged, 4-wave workgroups (WCE_LR_STAGED_LDS_P)
+        const dim3 gs4((unsigned)((waves + 255) / 256)), bs4(256);   // staged, 4-wave workgroups (LR_STAGED_LDS_P)
         const bool tq = lr_contig(taps);
 #define WCE_LRL(RR)                                                                                         \
     case RR:                                                                                                \
-        if constexpr (RR >= 7 && lr_staged_threads(RR) == 256 && WCE_LR_STAGED_MINWG > 1) {                \
+        if constexpr (RR >= 7 && lr_staged_threads(RR) == 256 && LR_STAGED_MINWG > 1) {                \
             if (form == LrForm::StagedMW) {                                                                 \
-                if (tq) hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG, true>), gs4, bs4, 0, s, st, a); \
-                else hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, WCE_LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
+                if (tq) hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, LR_STAGED_MINWG, true>), gs4, bs4, 0, s, st, a); \
+                else hipLaunchKernelGGL((mmse_lr_lane_staged_kernel<RR, LR_STAGED_MINWG>), gs4, bs4, 0, s, st, a); \
                 break;                                                                                      \
             }                                                                                               \
         }                                                                                                   \
@@ -3402,6 +3137,7 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 {
     if (a.n <= 0) return WCE_OK;
     if (a.hout && !a.cu) return WCE_EINVAL;
+    if (a.mmse_done && !(a.ref_pilots && a.hout && !a.split && variant(WCE_VARIANT_REF_LS) == 0)) return WCE_EINVAL;
     const dim3 g((unsigned)a.n), b(64);
     hipStream_t s = (hipStream_t)stream;
     const bool eq = (l.mask & WCE_EQUALIZE) && l.eq;
@@ -3436,9 +3172,7 @@ int launch_mmse_solve_ls(const State *st, const SolveArgs &a, const LsArgs &l, v
 // matvec_kernel for rows 0..47; rows 48..52 on v_mfma_f64_4x4x4_4b
 // (apply_tile3: 508 -> 465 us per 1,048,576 frames), whose results matched
 // the 16x16x4 form bit for bit on every A/B run (tools/ab_libs.py --leg apply).
-#ifndef WCE_APPLY_WG_PER_CU
-#define WCE_APPLY_WG_PER_CU 2
-#endif
+constexpr int APPLY_WG_PER_CU = 2;
 // Row stride (complex) of the staged C.  A read sc[i * ACS + 4 s + kl] (i =
 // 16 nt + (lane & 15), kl = lane >> 4) is a ds_read_b128, banked in four
 // 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... on 16-B slots
@@ -3474,10 +3208,13 @@ __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t 
 // (48..51, 52..55), three independent chains each.  The Gauss form's imaginary
 // part carries ~eps (|Re w| + |Im w|)(|Re c| + |Im c|) per term, the same order
 // as the 4-product form's ~eps (|Re w Im c| + |Im w Re c|).
+// SCS: Re c + Im c staged beside c (apply_kernel); else added per k-step (one
+// VALU add, the same bits).  Outputs through the Store: row16(r, i, v) for
+// frame kl + 4 r, row4(i, v) for frame ml.
 constexpr int APPLY_PF = 2;
+template <bool SCS, class Store>
 __device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs, const double (&ar)[KSTEPS],
-                                            const double (&ai)[KSTEPS], int ml, int kl, double *Y, int64_t ys,
-                                            int64_t f0, int64_t n, const uint8_t *__restrict__ skip)
+                                            const double (&ai)[KSTEPS], int ml, int kl, const Store &out)
 {
     constexpr int NS = APPLY_NT * KSTEPS;
     constexpr int PF = APPLY_PF;
@@ -3487,18 +3224,18 @@ __device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs
     for (int t = 0; t < PF; ++t) {
         const int e = (16 * (t / KSTEPS) + ml) * ACS + 4 * (t % KSTEPS) + kl;
         cb[t] = sc[e];
-        cbs[t] = scs[e];
+        if constexpr (SCS) cbs[t] = scs[e];
     }
     v4d p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
         const int nt = t / KSTEPS, s = t % KSTEPS;
         const double2 c = cb[t % PF];
-        const double cs = cbs[t % PF];
+        const double cs = SCS ? cbs[t % PF] : c.x + c.y;
         if (t + PF < NS) {
             const int e = (16 * ((t + PF) / KSTEPS) + ml) * ACS + 4 * ((t + PF) % KSTEPS) + kl;
             cb[t % PF] = sc[e];
-            cbs[t % PF] = scs[e];
+            if constexpr (SCS) cbs[t % PF] = scs[e];
         }
         const double as = ar[s] + ai[s];
         __builtin_amdgcn_sched_barrier(0);
@@ -3513,10 +3250,7 @@ __device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs
             const int i = 16 * nt + ml;
             if (i < NSC) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t fr = f0 + kl + 4 * r;
-                    if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, make_double2(hr[r], hi[r]));
-                }
+                for (int r = 0; r < 4; ++r) out.row16(r, i, make_double2(hr[r], hi[r]));
             }
             p1 = p2 = p3 = v4d{0, 0, 0, 0};
         }
@@ -3524,17 +3258,23 @@ __device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs
     const int m4 = ml & 3;
     double a0 = 0.0, b0 = 0.0, g0 = 0.0, a1 = 0.0, b1 = 0.0, g1 = 0.0;
     double2 n0 = sc[(48 + m4) * ACS + kl], n1 = sc[(52 + m4) * ACS + kl];
-    double ns0 = scs[(48 + m4) * ACS + kl], ns1 = scs[(52 + m4) * ACS + kl];
+    double ns0 = 0.0, ns1 = 0.0;
+    if constexpr (SCS) {
+        ns0 = scs[(48 + m4) * ACS + kl];
+        ns1 = scs[(52 + m4) * ACS + kl];
+    }
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
         const double2 c0 = n0, c1 = n1;
-        const double cs0 = ns0, cs1 = ns1;
+        const double cs0 = SCS ? ns0 : c0.x + c0.y, cs1 = SCS ? ns1 : c1.x + c1.y;
         asm volatile("" ::: "memory");
         if (s + 1 < KSTEPS) {
             n0 = sc[(48 + m4) * ACS + 4 * (s + 1) + kl];
             n1 = sc[(52 + m4) * ACS + 4 * (s + 1) + kl];
-            ns0 = scs[(48 + m4) * ACS + 4 * (s + 1) + kl];
-            ns1 = scs[(52 + m4) * ACS + 4 * (s + 1) + kl];
+            if constexpr (SCS) {
+                ns0 = scs[(48 + m4) * ACS + 4 * (s + 1) + kl];
+                ns1 = scs[(52 + m4) * ACS + 4 * (s + 1) + kl];
+            }
         }
         const double as = ar[s] + ai[s];
         a0 = __builtin_amdgcn_mfma_f64_4x4x4f64(c0.x, ar[s], a0, 0, 0, 0);
@@ -3544,14 +3284,28 @@ __device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs
         g0 = __builtin_amdgcn_mfma_f64_4x4x4f64(cs0, as, g0, 0, 0, 0);
         g1 = __builtin_amdgcn_mfma_f64_4x4x4f64(cs1, as, g1, 0, 0, 0);
     }
-    const int64_t fr = f0 + ml;
-    if (fr < n && !(skip && skip[fr])) {
-        st2(Y, fr * ys + 48 + kl, make_double2(a0 - b0, (g0 - a0) - b0));
-        if (kl == 0) st2(Y, fr * ys + 52, make_double2(a1 - b1, (g1 - a1) - b1));   // rows 53..55: padding, never stored
-    }
+    out.row4(48 + kl, make_double2(a0 - b0, (g0 - a0) - b0));
+    if (kl == 0) out.row4(52, make_double2(a1 - b1, (g1 - a1) - b1));   // rows 53..55: padding, never stored
 }
 
-__global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const double *__restrict__ M, const double *X,
+// apply_kernel's stores: H = C W rows of the live, not-skipped frames
+struct ApplyStore {
+    double *Y;
+    int64_t ys, f0, n;
+    const uint8_t *skip;
+    __device__ void row16(int r, int i, double2 v) const
+    {
+        const int64_t fr = f0 + (threadIdx.x & 63) / 16 + 4 * r;
+        if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, v);
+    }
+    __device__ void row4(int i, double2 v) const
+    {
+        const int64_t fr = f0 + (threadIdx.x & 15);
+        if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, v);
+    }
+};
+
+__global__ __launch_bounds__(256, APPLY_WG_PER_CU) void apply_kernel(const double *__restrict__ M, const double *X,
                                                                         int64_t xs, double *Y, int64_t ys, int64_t n,
                                                                         const uint8_t *__restrict__ skip)
 {
@@ -3583,7 +3337,245 @@ __global__ __launch_bounds__(256, WCE_APPLY_WG_PER_CU) void apply_kernel(const d
             apply_load(X, xs, n, g + stride, ml, kl, wn, tile_done(skip, 16 * (g + stride), n, lane));
         const int64_t f0 = 16 * g;
         if (tile_done(skip, f0, n, lane)) continue;
-        apply_tile3(sc, scs, ar, ai, ml, kl, Y, ys, f0, n, skip);
+        apply_tile3<true>(sc, scs, ar, ai, ml, kl, ApplyStore{Y, ys, f0, n, skip});
+    }
+}
+
+// =====================================================================
+// REF per-frame covariance (WCE_MMSE_FRAME_COV with WCE_MMSE_REF, C
+// semantics).  main.c's PS_MMSE consumes the frame's own H_EST_LT_LS
+// (main.c:37-53, 148): g = invF h, Rhh = g q(g)^T, C = F Rhh FH = u w^T with
+// u = F invF h = Mu h and w = Mw q(g), and with Ryy = 2 ow2 I and X the 4
+// pilots, H = u s, s = sum_p w_p x_p rx_p / b (main.c:186-205).  Only w at
+// the pilot rows P = {5, 19, 33, 47} is ever read, and q(g) = re g - im g is
+// real-linear in (re h, im h), so w_P = Ar re h + Ai im h with the 4 x 53
+// real maps Ar, Ai formed once in 80 bits (State::Wp, round 5): g is never
+// formed, and the per-frame MFMA work is the one product u = Mu h.
+//
+// Lane layout throughout = the MFMA A layout: lane l holds frame l & 15 of
+// the 16-frame tile at subcarriers j = 4 s + (l >> 4), s < 14.
+//   h    = LT_LS(tx_pre, rx_pre_f)        ls_elem_kernel's formula (main.c:66-75)
+//   w_p  = sum over the lane's j, then over the 4 lanes of the frame
+//          (ref_w4: 2 x 14 FMA per pilot, permlane16/32 sums)
+//   s    = ref_sum4(ref_term(w_p, x_p, rx_p)) / b    the REF kernels' rounding
+//   H    = u s, u = Mu h on f64 MFMA           apply_tile3's chains (3M form)
+// The variant path (WCE_VARIANT_REF_FC = 1, and MATLAB semantics) forms the
+// same values in separate launches (LT_LS pass, matvec of Mu, ref_w_kernel,
+// the REF read-out) and is bit-identical to it.
+// =====================================================================
+__device__ __forceinline__ void ref_w4(const double2 *__restrict__ wp, const double (&ar)[KSTEPS],
+                                       const double (&ai)[KSTEPS], int kl, double (&w)[4])
+{
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        double acc = 0.0;
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const double2 c = wp[p * APPLY_ROWS + 4 * s + kl];   // {Ar, Ai}[p][j], zero past j = 52
+            acc = fma(c.x, ar[s], acc);
+            acc = fma(c.y, ai[s], acc);
+        }
+        w[p] = sum_xor32(sum_xor16(acc));   // the frame's 4 lanes, same bits in each
+    }
+}
+
+// h of frame fa at the lane's subcarriers: LT_LS of its preamble (ls_elem_kernel's
+// cdiv, the same bits), zero at DC and past 52
+__device__ __forceinline__ void ref_h(const double2 (&rp)[KSTEPS], const double2 *tp, int kl, bool live,
+                                      double (&ar)[KSTEPS], double (&ai)[KSTEPS])
+{
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        double2 h = make_double2(0, 0);
+        if (live && j < NSC && j != WCE_DC) {
+            const double2 t = tp[j];   // tx_pre (LDS: re-read per tile, not held in registers)
+            const double cq = t.x - t.y;
+            h = cdiv(make_double2(cq * rp[s].x, cq * rp[s].y), make_double2(cq * t.x, cq * t.y));
+        }
+        ar[s] = h.x;
+        ai[s] = h.y;
+    }
+}
+
+// s of frame ml of the tile from the lane's own pilot kl (x, rx of block blk):
+// the 4 pilot terms meet in every lane of the frame through 3 lane swaps and
+// are summed in pilot order (ref_sum4), so each lane holds the same bits
+__device__ __forceinline__ double2 ref_s(const double (&w)[4], double2 xt, double2 xr, int kl, double rb)
+{
+    const double wk = kl == 0 ? w[0] : kl == 1 ? w[1] : kl == 2 ? w[2] : w[3];
+    const double2 t0 = ref_term(make_double2(wk, 0.0), xt, xr);
+    const double2 t1 = shfl_xor_c(t0, 16), t2 = shfl_xor_c(t0, 32), t3 = shfl_xor_c(t0, 48);
+    auto pick = [&](int p) {   // pilot p's term sits in lane (p ^ kl) swaps away
+        const int d = p ^ kl;
+        return d == 0 ? t0 : d == 1 ? t1 : d == 2 ? t2 : t3;
+    };
+    return ref_sum4(pick(0), pick(1), pick(2), pick(3), rb);
+}
+// the same from all 4 pilots loaded by every lane of the frame
+__device__ __forceinline__ double2 ref_s4(const double (&w)[4], const SolveArgs &a, int64_t fa, double rb)
+{
+    if (fa >= a.n) return make_double2(0, 0);
+    const int64_t o = fa * a.fs + (int64_t)a.blk * a.bs;
+    double2 t[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) t[p] = ref_term(make_double2(w[p], 0.0), ld2(a.tx, o + PILOT[p]), ld2(a.rx, o + PILOT[p]));
+    return ref_sum4(t[0], t[1], t[2], t[3], rb);
+}
+
+#ifndef WCE_FC_PILOT_PF
+#define WCE_FC_PILOT_PF 1
+#endif
+#ifndef WCE_FC_TP_LDS
+#define WCE_FC_TP_LDS 1
+#endif
+#ifndef WCE_FC_LATE_LOAD
+#define WCE_FC_LATE_LOAD 0
+#endif
+#ifndef WCE_FC_EARLY_FIRST
+#define WCE_FC_EARLY_FIRST 1
+#endif
+constexpr int FC_WG_PER_CU = 2;
+struct RefFcShared {
+    double2 sc[APPLY_ROWS * ACS];        // Mu rows 0..55 (apply_kernel's staging, no Re + Im copy)
+    double2 wp[4 * APPLY_ROWS];          // {Ar, Ai} at the 4 pilots, j < 56
+    double2 tp[NPAD];                    // tx_pre
+    double2 s[APPLY_WAVES][16];          // s of each wave's current tile
+};
+static_assert(FC_WG_PER_CU * sizeof(RefFcShared) <= 160 * 1024, "two workgroups per CU");
+
+// H = u s of the tile's frames: rows 0..47 frame kl + 4 r, rows 48..52 frame ml
+struct RefFcStore {
+    double *H;
+    int64_t hs, f0, n;
+    double2 sv[4], sm;
+    __device__ void row16(int r, int i, double2 u) const
+    {
+        const int64_t fr = f0 + (threadIdx.x & 63) / 16 + 4 * r;
+        if (fr < n) st2(H, fr * hs + i, ref_out(u, sv[r]));
+    }
+    __device__ void row4(int i, double2 u) const
+    {
+        const int64_t fr = f0 + (threadIdx.x & 15);
+        if (fr < n) st2(H, fr * hs + i, ref_out(u, sm));
+    }
+};
+
+// Persistent: each wave walks 16-frame tiles g, g + stride, ... with the next
+// tile's preamble in flight under this tile's work; Mu and Wp staged once per
+// workgroup.
+__global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *__restrict__ st, SolveArgs a,
+                                                                   const double *__restrict__ rx_pre, int64_t ps,
+                                                                   const double *__restrict__ tx_pre)
+{
+    __shared__ RefFcShared sh;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int pil = kl == 0 ? WCE_P0 : kl == 1 ? WCE_P1 : kl == 2 ? WCE_P2 : WCE_P3;
+    const int64_t ng = (a.n + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * APPLY_WAVES;
+    int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + wv;
+    // the next tile's inputs: the preamble at the lane's subcarriers, pilot kl of block blk
+    double2 rpn[KSTEPS], xtn, xrn;
+    auto load = [&](int64_t gt) {
+        const int64_t fa = 16 * gt + ml;
+        const bool live = fa < a.n;
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl;
+            rpn[s] = (live && j < NSC) ? ld2_nt(rx_pre, fa * ps + j) : make_double2(0, 0);
+        }
+#if WCE_FC_PILOT_PF
+        const int64_t o = fa * a.fs + (int64_t)a.blk * a.bs + pil;
+        xtn = live ? ld2(a.tx, o) : make_double2(0, 0);
+        xrn = live ? ld2(a.rx, o) : make_double2(0, 0);
+#endif
+    };
+#if WCE_FC_EARLY_FIRST
+    if (g < ng) load(g);   // the first tile's loads under the staging below
+#endif
+    for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
+        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
+        sh.sc[i * ACS + j] = ld2(st->Mu, i * CLD + j);   // Mu zero-padded 64 x 64
+    }
+    for (int e = threadIdx.x; e < 4 * APPLY_ROWS; e += 256) {
+        const int p = e / APPLY_ROWS, k = e - p * APPLY_ROWS;
+        sh.wp[e] = ld2(st->Wp, p * NPAD + k);
+    }
+    const double *txp = tx_pre ? tx_pre : st->tx_pre;
+    if (threadIdx.x < NPAD) sh.tp[threadIdx.x] = threadIdx.x < NSC ? ld2(txp, threadIdx.x) : make_double2(0, 0);
+    __syncthreads();
+    if (g >= ng) return;
+#if !WCE_FC_EARLY_FIRST
+    load(g);
+#endif
+    const double rb = 1.0 / st->bcoef;
+    for (; g < ng; g += stride) {
+        const int64_t f0 = 16 * g, fa = f0 + ml;
+        double ar[KSTEPS], ai[KSTEPS];
+#if WCE_FC_TP_LDS
+        ref_h(rpn, sh.tp, kl, fa < a.n, ar, ai);
+#else
+        ref_h(rpn, reinterpret_cast<const double2 *>(txp), kl, fa < a.n, ar, ai);
+#endif
+#if WCE_FC_PILOT_PF
+        const double2 xt = xtn, xr = xrn;
+#endif
+#if !WCE_FC_LATE_LOAD
+        if (g + stride < ng) load(g + stride);   // next tile, under this one's work
+#endif
+        double w[4];
+        ref_w4(sh.wp, ar, ai, kl, w);
+#if WCE_FC_PILOT_PF
+        RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s(w, xt, xr, kl, rb)};
+#else
+        RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s4(w, a, fa, rb)};
+#endif
+        if (kl == 0) sh.s[wv][ml] = out.sm;
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out.sv[r] = sh.s[wv][kl + 4 * r];
+        wave_lds_sync();   // the next tile rewrites sh.s[wv]
+        apply_tile3<false>(sh.sc, nullptr, ar, ai, ml, kl, out);
+#if WCE_FC_LATE_LOAD
+        if (g + stride < ng) load(g + stride);
+#endif
+    }
+}
+
+// The variant path's w: full rows of w (zero off the pilots) from the frames'
+// h rows, ref_w4's arithmetic and lanes (one 16-frame tile per wave)
+__global__ __launch_bounds__(256) void ref_w_kernel(const State *__restrict__ st, const double *__restrict__ X,
+                                                    int64_t xs, double *W, int64_t ws, int64_t n)
+{
+    __shared__ double2 wp[4 * APPLY_ROWS];
+    for (int e = threadIdx.x; e < 4 * APPLY_ROWS; e += 256) {
+        const int p = e / APPLY_ROWS, k = e - p * APPLY_ROWS;
+        wp[e] = ld2(st->Wp, p * NPAD + k);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
+    if (f0 >= n) return;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t fa = f0 + ml;
+    double ar[KSTEPS], ai[KSTEPS];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        const double2 v = (fa < n && j < NSC) ? ld2(X, fa * xs + j) : make_double2(0, 0);
+        ar[s] = v.x;
+        ai[s] = v.y;
+    }
+    double w[4];
+    ref_w4(wp, ar, ai, kl, w);
+    if (fa >= n) return;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        const int j = 4 * s + kl;
+        if (j >= NSC) continue;
+        const int p = j == WCE_P0 ? 0 : j == WCE_P1 ? 1 : j == WCE_P2 ? 2 : j == WCE_P3 ? 3 : -1;
+        st2(W, fa * ws + j, make_double2(p >= 0 ? w[p < 0 ? 0 : p] : 0.0, 0.0));
     }
 }
 
@@ -3594,14 +3586,14 @@ int launch_mmse_apply(const State *st, const double *W, double *H, int64_t strid
     // 256 CUs); below that one wave round of matvec_kernel is as fast or faster
     // (profiles/r02_ab_apply.txt)
     const int64_t tiles = (n + 15) / 16;
-    if (tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * WCE_APPLY_WG_PER_CU) {
+    if (tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * APPLY_WG_PER_CU) {
         const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
         hipLaunchKernelGGL((matvec_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                            st->C, nullptr, W, stride, H, nullptr, stride, n, skip);
         return hip_status(hipGetLastError());
     }
     static_assert(APPLY_WAVES == LS_WAVES, "tile_blocks counts LS_WAVES waves per workgroup");
-    const int64_t blocks = tile_blocks(tiles, APPLY_WAVES * WCE_APPLY_WG_PER_CU);
+    const int64_t blocks = tile_blocks(tiles, APPLY_WAVES * APPLY_WG_PER_CU);
     hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st->C, W, stride, H,
                        stride, n, skip);
     return hip_status(hipGetLastError());
@@ -3634,15 +3626,21 @@ int launch_matvec(const double *M1, const double *M2, const double *X, int64_t x
 }
 
 int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
-                  double *uw, double *ww, int64_t wld, bool hout, void *stream)
+                  void *stream)
 {
     if (a.n <= 0) return WCE_OK;
-    if (a.split || !rx_pre) return WCE_EINVAL;
-    const int64_t blocks = (a.n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
-    const dim3 g((unsigned)blocks), b(256);
-    hipStream_t s = (hipStream_t)stream;
-    if (hout) hipLaunchKernelGGL(ref_fc_kernel<true>, g, b, 0, s, st, a, rx_pre, ps, tx_pre, uw, ww, wld);
-    else hipLaunchKernelGGL(ref_fc_kernel<false>, g, b, 0, s, st, a, rx_pre, ps, tx_pre, uw, ww, wld);
+    if (a.split || !rx_pre || !a.w) return WCE_EINVAL;
+    const int64_t blocks = tile_blocks((a.n + 15) / 16, APPLY_WAVES * FC_WG_PER_CU);
+    hipLaunchKernelGGL(ref_fc_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, rx_pre, ps,
+                       tx_pre);
+    return hip_status(hipGetLastError());
+}
+
+int launch_ref_w(const State *st, const double *X, int64_t xs, double *W, int64_t ws, int64_t n, void *stream)
+{
+    if (n <= 0) return WCE_OK;
+    const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
+    hipLaunchKernelGGL(ref_w_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, X, xs, W, ws, n);
     return hip_status(hipGetLastError());
 }
 

@@ -235,6 +235,19 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
                     Mw[j * n + c] = mk((long double)(creal_d(F[j * n + c]) - cimag_d(F[j * n + c])), 0.0L);
             put(st->Mg, invF);
             put(st->Mw, Mw);
+            // w_P folded: q(g) = re g - im g is real-linear in (re h, im h)
+            for (int p = 0; p < 4; p++)
+                for (int k = 0; k < n; k++) {
+                    long double ar = 0.0L, ai = 0.0L;
+                    for (int c = 0; c < n; c++) {
+                        const long double m = __real__ Mw[PILOT[p] * n + c];
+                        const long double gr = __real__ invF[c * n + k], gi = __imag__ invF[c * n + k];
+                        ar += m * (gr - gi);
+                        ai -= m * (gr + gi);
+                    }
+                    st->Wp[2 * (p * NPAD + k)] = (double)ar;
+                    st->Wp[2 * (p * NPAD + k) + 1] = (double)ai;
+                }
         } else {
             for (int i = 0; i < n * n; i++) {
                 rhs[i] = F[i];

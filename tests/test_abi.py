@@ -231,3 +231,26 @@ def test_c_host_multi_device_runs(args):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "frames/s aggregate" in r.stdout and "non-finite frames (max over devices): 0;" in r.stdout
     assert "mismatching device 0: 0" in r.stdout
+
+
+def test_ref_pilot_row_map(wce, golden, oracle):
+    """State::Wp (round 5): w at the pilots of REF's per-frame covariance,
+    folded into one real map of (re h, im h), against main.c's chain in long
+    double (main.c:186-203: g = invF h, q = re g - im g, w = FH^T q with FH[c][r]
+    = re F[r][c] - im F[r][c]) on random h: within 1e-15 of the chain's scale."""
+    r = golden["ref"]
+    blob = wce.state_blob(r["pre_tx"][0], r["pre_rx"][0], r["ow2"], wce.MMSE_REF)
+    off = 4 * 64 * 64 * 16                                   # past C, Mg, Mu, Mw
+    Wp = blob[off:off + 4 * 64 * 16].view(np.float64).reshape(4, 64, 2)
+    assert not np.any(Wp[:, N:])
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    Mw = (F.real.astype(np.float64) - F.imag.astype(np.float64)).astype(np.longdouble)   # rounded through double
+    rng = np.random.default_rng(4)
+    for _ in range(8):
+        h = (rng.standard_normal(N) + 1j * rng.standard_normal(N)) * 0.01
+        g = invF @ h.astype(np.clongdouble)
+        q = g.real - g.imag
+        w_ref = np.array([np.sum(Mw[p] * q) for p in (5, 19, 33, 47)])
+        w = Wp[:, :N, 0] @ h.real + Wp[:, :N, 1] @ h.imag
+        scale = np.abs(Mw[[5, 19, 33, 47]]) @ np.abs(q)
+        assert np.all(np.abs(w - w_ref.astype(np.float64)) <= 1e-15 * scale), (w, w_ref)

@@ -14,7 +14,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
-ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm"], default="config5")
+ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm", "fcref", "c5ref_fc"],
+                default="config5")
 ap.add_argument("--taps", type=int, default=8, help="lowrank: L-tap PDP covariance (rank L; 53 = decay 0.5)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--frames", type=int, default=262144)
@@ -37,6 +38,8 @@ for d in args.dirs:
     elif args.leg in ("lowrank", "cm"):   # cm: the same ctx on the constant-modulus operator (wce_ctx_set_modulus)
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rank(args.taps))
+    elif args.leg in ("fcref", "c5ref_fc"):
+        ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_REF)
     else:
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_TEXTBOOK)
     tx, rx, pre = m.DeviceArray((n, NB, N)), m.DeviceArray((n, NB, N)), m.DeviceArray((n, N))
@@ -51,6 +54,23 @@ for d in args.dirs:
         f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.ALL, st.handle))(ctx, fr, o, st, m)
         keep += outs + [eq]
         check = outs[4]
+    elif args.leg in ("fcref", "c5ref_fc"):   # REF + FRAME_COV: PS_MMSE alone / all 5 + eq (fp64)
+        ctx.reserve(n)
+        fr = ctx.frames(tx, rx, n, rx_pre=pre)
+        if args.leg == "fcref":
+            H = m.DeviceArray((n, N))
+            o = m.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+            mk = m.PS_MMSE | m.FRAME_COV
+            keep.append(H)
+        else:
+            outs = [m.DeviceArray((n, N)) for _ in range(5)]
+            eq = m.DeviceArray((n, NB, N))
+            o = m.Outputs(*(x.addr for x in outs), eq.addr, N, NB * N, N, 0, 0)
+            mk = m.ALL | m.FRAME_COV
+            keep += outs + [eq]
+            H = outs[4]
+        f = (lambda c, fr, o, st, mk: lambda: c.estimate(fr, o, mk, st.handle))(ctx, fr, o, st, mk)
+        check = H
     elif args.leg in ("headline", "lowrank", "cm"):
         if args.leg == "cm":
             ctx.set_modulus(tx.rows(0)[0, 0])
