@@ -3398,19 +3398,20 @@ __device__ __forceinline__ void ref_h(const double2 (&rp)[KSTEPS], const double2
     }
 }
 
-// s of frame ml of the tile from the lane's own pilot kl (x, rx of block blk):
-// the 4 pilot terms meet in every lane of the frame through 3 lane swaps and
-// are summed in pilot order (ref_sum4), so each lane holds the same bits
-__device__ __forceinline__ double2 ref_s(const double (&w)[4], double2 xt, double2 xr, int kl, double rb)
+// s of frame ml of the tile from the lane's own pilot kl (x, rx of block blk).
+// ref_sum4's ((t0 + t1) + (t2 + t3)) rb is symmetric under every pairing the
+// lane swaps produce (fp addition commutes), so each lane of the frame forms
+// it as ((own + own^16) + (the same pair sum of lane ^32)) rb: the same bits
+// in all four lanes, and the same bits as ref_sum4 over the pilots in order.
+__device__ __forceinline__ double2 ref_s(double w0, double w1, double w2, double w3, double2 xt, double2 xr, int kl,
+                                         double rb)
 {
-    const double wk = kl == 0 ? w[0] : kl == 1 ? w[1] : kl == 2 ? w[2] : w[3];
-    const double2 t0 = ref_term(make_double2(wk, 0.0), xt, xr);
-    const double2 t1 = shfl_xor_c(t0, 16), t2 = shfl_xor_c(t0, 32), t3 = shfl_xor_c(t0, 48);
-    auto pick = [&](int p) {   // pilot p's term sits in lane (p ^ kl) swaps away
-        const int d = p ^ kl;
-        return d == 0 ? t0 : d == 1 ? t1 : d == 2 ? t2 : t3;
-    };
-    return ref_sum4(pick(0), pick(1), pick(2), pick(3), rb);
+#pragma clang fp contract(off)
+    const double wk = (kl & 2) ? ((kl & 1) ? w3 : w2) : ((kl & 1) ? w1 : w0);
+    const double2 t = ref_term(make_double2(wk, 0.0), xt, xr);
+    const double2 u = cadd(t, shfl_xor_c(t, 16));    // t_{kl} + t_{kl ^ 1}
+    const double2 v = shfl_xor_c(u, 32);              // t_{kl ^ 2} + t_{kl ^ 3}
+    return make_double2((u.x + v.x) * rb, (u.y + v.y) * rb);
 }
 // the same from all 4 pilots loaded by every lane of the frame
 __device__ __forceinline__ double2 ref_s4(const double (&w)[4], const SolveArgs &a, int64_t fa, double rb)
@@ -3424,22 +3425,15 @@ __device__ __forceinline__ double2 ref_s4(const double (&w)[4], const SolveArgs 
 }
 
 #ifndef WCE_FC_PILOT_PF
-#define WCE_FC_PILOT_PF 1
-#endif
-#ifndef WCE_FC_TP_LDS
-#define WCE_FC_TP_LDS 1
-#endif
-#ifndef WCE_FC_LATE_LOAD
-#define WCE_FC_LATE_LOAD 0
+#define WCE_FC_PILOT_PF 0
 #endif
 #ifndef WCE_FC_EARLY_FIRST
-#define WCE_FC_EARLY_FIRST 1
+#define WCE_FC_EARLY_FIRST 0
 #endif
 constexpr int FC_WG_PER_CU = 2;
 struct RefFcShared {
     double2 sc[APPLY_ROWS * ACS];        // Mu rows 0..55 (apply_kernel's staging, no Re + Im copy)
     double2 wp[4 * APPLY_ROWS];          // {Ar, Ai} at the 4 pilots, j < 56
-    double2 tp[NPAD];                    // tx_pre
     double2 s[APPLY_WAVES][16];          // s of each wave's current tile
 };
 static_assert(FC_WG_PER_CU * sizeof(RefFcShared) <= 160 * 1024, "two workgroups per CU");
@@ -3503,7 +3497,6 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
         sh.wp[e] = ld2(st->Wp, p * NPAD + k);
     }
     const double *txp = tx_pre ? tx_pre : st->tx_pre;
-    if (threadIdx.x < NPAD) sh.tp[threadIdx.x] = threadIdx.x < NSC ? ld2(txp, threadIdx.x) : make_double2(0, 0);
     __syncthreads();
     if (g >= ng) return;
 #if !WCE_FC_EARLY_FIRST
@@ -3513,21 +3506,15 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
     for (; g < ng; g += stride) {
         const int64_t f0 = 16 * g, fa = f0 + ml;
         double ar[KSTEPS], ai[KSTEPS];
-#if WCE_FC_TP_LDS
-        ref_h(rpn, sh.tp, kl, fa < a.n, ar, ai);
-#else
         ref_h(rpn, reinterpret_cast<const double2 *>(txp), kl, fa < a.n, ar, ai);
-#endif
 #if WCE_FC_PILOT_PF
         const double2 xt = xtn, xr = xrn;
 #endif
-#if !WCE_FC_LATE_LOAD
         if (g + stride < ng) load(g + stride);   // next tile, under this one's work
-#endif
         double w[4];
         ref_w4(sh.wp, ar, ai, kl, w);
 #if WCE_FC_PILOT_PF
-        RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s(w, xt, xr, kl, rb)};
+        RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s(w[0], w[1], w[2], w[3], xt, xr, kl, rb)};
 #else
         RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s4(w, a, fa, rb)};
 #endif
@@ -3537,9 +3524,6 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
         for (int r = 0; r < 4; ++r) out.sv[r] = sh.s[wv][kl + 4 * r];
         wave_lds_sync();   // the next tile rewrites sh.s[wv]
         apply_tile3<false>(sh.sc, nullptr, ar, ai, ml, kl, out);
-#if WCE_FC_LATE_LOAD
-        if (g + stride < ng) load(g + stride);
-#endif
     }
 }
 

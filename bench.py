@@ -1077,9 +1077,10 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
     preambles, one HBM pass (ref_ls_elem_kernel: one (frame, subcarrier)
     element per thread).  frame_cov_*: the same with WCE_MMSE_FRAME_COV, i.e.
     each frame's PS_MMSE from its own LT_LS as main.c:37-53 / 148 chain them
-    (round 4: ref_fc_kernel forms the factors, then the same one-pass kernel;
-    the factor rows' HBM round trip, 2 x 848 + 4 x 64 B per frame, is not
-    algorithmic and shows in `traffic`).  Bytes per frame, SURVEY 8(d): rx 15x53 + tx block 0 +
+    (round 5: ref_fc_kernel writes each frame's PS_MMSE itself -- LT_LS, w
+    at the pilots from the folded map, u = Mu h on f64 MFMA, H = u s -- and
+    the one-pass kernel writes the LS family + eq; the factor kernel's extra
+    rx_pre read, 848 B per frame, shows in `traffic`).  Bytes per frame, SURVEY 8(d): rx 15x53 + tx block 0 +
     rx_pre in, 5 H + eq out = 31,376 (fp64) / 23,320 (LS + eq stored fp32); the
     kernel reads only tx's 4 pilots of block 0, so it moves 784 B less
     (30,592 / 22,536: its minimum I/O, the rate quoted as `achieved`)."""
@@ -1112,15 +1113,16 @@ def bench_config5_ref(wce, ctx_ref, stream, n, reps):
         # WRITE_SIZE runs 5% (fp64) / 11% (fp32) over the output bytes: 53-element
         # rows end in partial 64-B sectors; FETCH_SIZE = streamed rx / rx_pre (x2,
         # the gfx950 correction) + the 8 pilot sectors per frame (counted in full)
-        k, src = pmc_leg(leg, n, out_b * n, tol=0.12) if leg != "config5_ref_fc_f32" else (None, "fp32 FRAME_COV leg not profiled")
+        ls_b = out_b - (N * 16 if fc else 0)   # FRAME_COV: PS_MMSE leaves from ref_fc_kernel
+        k, src = pmc_leg(leg, n, ls_b * n, tol=0.12) if leg != "config5_ref_fc_f32" else (None, "fp32 FRAME_COV leg not profiled")
         traffic = hbm_bytes(k, narrow_fetch_kib=BYTES_PILOT_SECTORS * n / 1024.0) if k else None
-        if fc and traffic is not None:   # + the factor kernel's rx_pre in, u and w rows out (16-frame tiles)
-            kf, _ = pmc_leg("config5_ref_fc_factors", n, 0.0, waves=(n + 15) // 16)
-            traffic = traffic + hbm_bytes(kf) if kf else None
+        if fc and traffic is not None:   # + ref_fc_kernel: rx_pre and the pilots in, H out
+            kf, _ = pmc_leg("config5_ref_fc_factors", n, N * 16.0 * n, tol=0.12)
+            traffic = traffic + hbm_bytes(kf, narrow_fetch_kib=BYTES_PILOT_SECTORS * n / 1024.0) if kf else None
         bad = sum(ctx_ref.nonfinite_scan(h, n, f32=(f32 and i < 4), stream=s)[1] for i, h in enumerate(outs))
         bad += ctx_ref.nonfinite_scan(eq, n * NBLK, f32=f32, stream=s)[1]
         res[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3),
-                      "kernels": "ref_fc_kernel<false> (per-frame u, w) + ref_ls_elem_kernel<true>" if fc else
+                      "kernels": "ref_fc_kernel (PS_MMSE) + ref_ls_elem_kernel<true> (LS family + eq)" if fc else
                                  "ref_ls_elem_kernel<true>",
                       "roofline": {"bound": "hbm", "kernel": "ref_ls_elem_kernel", "achieved": ach,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
@@ -1303,18 +1305,20 @@ def bench_frame_cov(wce, make_ctx, stream, n, reps):
         t = time_events(wce, stream, f, reps)
         out[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3), "nonfinite_frames": ctx_scan(c, H, n, s)}
         if m == wce.MMSE_REF:
-            # one launch (ref_fc_kernel<true>): rx_pre 848 + 8 pilots 128 in, H 848 out
+            # one launch (ref_fc_kernel): rx_pre 848 + 8 pilots 128 in, H 848 out
             alg = (N * 16 + 8 * 16 + N * 16) * n
-            k, src = pmc_leg("frame_cov_ref", n, N * 16.0 * n, waves=(n + 15) // 16)
+            k, src = pmc_leg("frame_cov_ref", n, N * 16.0 * n, tol=0.12)   # persistent grid: check the output bytes
             gbs = alg / (t * 1e-3) / 1e9
-            out[label].update({"kernel": "ref_fc_kernel<true> (LT_LS, g / u on f64 MFMA, w at the pilot rows, H = u s)",
+            out[label].update({"kernel": "ref_fc_kernel (LT_LS, w at the pilots from the folded map, u = Mu h on "
+                                         "f64 MFMA, H = u s)",
                                "roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                             "frac": gbs / PEAK_HBM_GBS, "algorithmic_bytes": alg,
                                             "traffic": hbm_bytes(k, narrow_fetch_kib=BYTES_PILOT_SECTORS * n / 1024.0)
                                             if k else None, "pmc_source": src,
-                                            # executed: per 16-frame tile 2 x 4 x 14 x 3 (g, u: 3M) + 3 x 14
-                                            # (w) v_mfma_f64_16x16x4 of 2,048 flop
-                                            "mfma_executed_tflops": (2 * 4 * KSTEPS_MFMA * 3 + 3 * KSTEPS_MFMA) * 2048
+                                            # executed: per 16-frame tile u = Mu h in the 3M form, rows 0..47
+                                            # 3 x 14 x 3 v_mfma_f64_16x16x4 (2,048 flop), rows 48..52 14 x 6
+                                            # v_mfma_f64_4x4x4_4b (512 flop)
+                                            "mfma_executed_tflops": (3 * KSTEPS_MFMA * 3 * 2048 + KSTEPS_MFMA * 6 * 512)
                                             * ((n + 15) // 16) / (t * 1e-3) / 1e12}})
         del c
     return out

@@ -1,76 +1,94 @@
-"""Regenerate README.md's numbers table from profiles/<round>_bench.json
-(the same committed evidence tools/design_numbers.py uses for DESIGN.md).
-usage: python tools/readme_numbers.py [r02]"""
+"""Regenerate README.md's numbers table from a bench line, stating its source.
+
+The line is bench.py's compact final stdout line (round 5+): the driver's own
+record of it (BENCH_rNN.json, field "parsed") when one exists, else the
+builder's copy (profiles/rNN_bench.json, run through gpurun on a fresh box of
+the same pool).  Legs the compact line summarises come from its "legs".
+usage: python tools/readme_numbers.py [BENCH_r05.json | profiles/r05_bench.json]
+       (default: the newest BENCH_r*.json with a parsed line, else the newest profiles/r*_bench.json)"""
+import glob
 import json
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-rnd = sys.argv[1] if len(sys.argv) > 1 else "r02"
-d = json.loads(open(os.path.join(REPO, "profiles", f"{rnd}_bench.json")).read().strip().splitlines()[-1])
-r = d["roofline"]
-ls, l65 = d["ls_config2"]["b1048576"], d["ls_config2"]["b65536"]
-rb = d["ref_mode"]["b1048576"]
-rr = rb["roofline"]
-cov, ap, hp, cb = d["cov_mode"], d["apply_kernel"], d["host_pipeline"], d["cpu_baseline"]
+
+
+def load(path):
+    d = json.load(open(path))
+    if "parsed" in d:   # the driver's record: the line it parsed from stdout
+        return d["parsed"], f"the driver's `{os.path.basename(path)}` ({d.get('where', 'MI355X')})"
+    return d, f"`profiles/{os.path.basename(path)}` (builder run on a gpurun box)"
+
+
+def pick():
+    if len(sys.argv) > 1:
+        return sys.argv[1]
+    for p in sorted(glob.glob(os.path.join(REPO, "BENCH_r*.json")), reverse=True):
+        d = json.load(open(p))
+        if d.get("parsed") and "legs" in d["parsed"]:
+            return p
+    return sorted(glob.glob(os.path.join(REPO, "profiles", "r*_bench.json")))[-1]
+
+
+path = pick()
+d, src = load(path)
+if not d:
+    raise SystemExit(f"{path}: no parsed bench line")
+r, lg, cb = d["roofline"], d.get("legs", {}), d.get("cpu_baseline", {})
 refc = cb.get("reference_code", {})
-c4, c5, fe, lc = d["config4"], d["config5_sharded"], d["front_end"], d["ldc_convert"]
 bd = r.get("board") or {}
+
+
+def g(name, key, fmt="{:.3g}", default="n/a"):
+    v = lg.get(name, {}).get(key)
+    return fmt.format(v) if isinstance(v, (int, float)) else default
+
+
+def fps(name, frames=1 << 20, key="ms"):
+    v = lg.get(name, {}).get(key)
+    return f"{frames / (v * 1e-3):.3g}" if isinstance(v, (int, float)) and v > 0 else "n/a"
+
+
 rows = [
     ("PS_MMSE, 65,536 frames (headline, TEXTBOOK)",
      f"{d['value']:.3g} frames/s; {100 * r['frac']:.1f}% of the FP64 spec peak by SURVEY's F_alg "
-     f"({100 * r['frac_executed']:.1f}% by executed flops), with the board at its power cap "
-     f"({bd.get('socket_power_W', 0):.0f} W, {bd.get('gfx_clock_MHz', 0):.0f} MHz). Within 4.5e-13 of the long double "
-     f"closed form on frames with any channel"),
-    ("PS_MMSE, 1,048,576 frames (BASELINE configs[3] batch, one GPU)", f"{c4['frames_per_s']:.3g} frames/s"),
+     f"({100 * r.get('frac_executed', 0):.1f}% by executed flops); board {bd.get('socket_power_W', 0):.0f} W, "
+     f"{bd.get('gfx_clock_MHz', 0):.0f} MHz. Within 1e-10 of the long double closed form on sampled frames of this "
+     f"very batch (`tests/test_headline_batch_gpu.py`)"),
+    ("PS_MMSE, 1,048,576 frames (BASELINE configs[3] batch, one GPU)", f"{g('config4', 'frames_per_s')} frames/s"),
     ("all 5 estimators + equalization, fp64 solve / fp32 LS outputs, 1,048,576 frames (configs[4] as named, one GPU)",
-     f"{c5['frames_per_s']:.3g} frames/s, every output finite, oracle-checked at full size"),
+     f"{g('config5_sharded', 'frames_per_s')} frames/s ({g('config5_sharded', 'ms_per_step', '{:.2f}')} ms), every "
+     f"output finite"),
     ("PS_MMSE, REF (`main.c`) semantics",
-     f"{d['ref_mode']['frames_per_s_per_gpu']:.2g} frames/s at 65,536 frames; {rb['frames_per_s']:.2g} at 1,048,576 "
-     f"({rr['achieved'] / 1000:.1f} TB/s algorithmic, {rr['achieved_sector_GBs'] / 1000:.1f} TB/s on the pilot-sector "
-     f"floor; the 8 pilot reads per frame are the limit, `profiles/r02_ubench_hbm.txt`)"),
+     f"{fps('ref_mode', 65536, 'ms_per_step')} frames/s at 65,536 frames; "
+     f"{1048576 / (lg['ref_mode']['b1M']['ms'] * 1e-3):.3g} at 1,048,576 "
+     f"({100 * lg['ref_mode']['b1M']['frac']:.0f}% of 8 TB/s on its algorithmic bytes)"
+     if "b1M" in lg.get("ref_mode", {}) else "n/a"),
     ("PS_MMSE, dense model covariance (COV)",
-     f"{cov['frames_per_s_per_gpu']:.2g} frames/s (solve {cov['solve_tflops']:.1f} TF = "
-     f"{100 * cov['solve_frac_fp64_peak']:.0f}% of FP64 peak; MFMA `C·W` {ap['achieved_tflops']:.1f} TF algorithmic, "
-     f"{ap.get('executed_tflops', 0):.1f} TF executed, pipe busy {100 * ap.get('mfma_busy_frac_pmc', 0):.0f}% by PMC of "
-     f"same-size launches)"),
-]
-lr = d.get("cov_lowrank", {})
-if lr:
-    rows.append(("PS_MMSE, model covariance = a 4 / 8 / 16 / 24 / 53-tap power-delay profile (COV low-rank paths: "
-                 "Toeplitz / tap-domain Gram)",
-                 " / ".join(f"{lr[L]['frames_per_s']:.3g}" for L in ("L4", "L8", "L16", "L24", "L53") if L in lr)
-                 + " frames/s, ≤2.3e-13 from the long double solve (≤1.5e-11 at rank 1)"))
-    cm = lr.get("L53", {}).get("constant_modulus")
-    if cm:
-        rows.append(("the same, 53 taps, BPSK frames on the shared operator (`wce_ctx_set_modulus`)",
-                     f"{cm['frames_per_s']:.3g} frames/s ({cm['speedup_vs_per_frame']:.1f}× the per-frame solve)"))
-c5r = d.get("config5_ref", {})
-if c5r:
-    rows.append(("configs[4] in `main.c` semantics (REF + LS family + eq), 1,048,576 frames",
-                 f"{c5r['fp64']['frames_per_s']:.3g} frames/s fp64 ({c5r['fp64']['roofline']['achieved'] / 1000:.2f} TB/s); "
-                 f"{c5r['mixed_fp64_solve_fp32_ls']['frames_per_s']:.3g} with fp32 LS outputs; with each frame's PS_MMSE "
-                 f"on its own LT_LS (FRAME_COV, as main.c:37-53) {c5r['frame_cov_fp64']['frames_per_s']:.3g}"
-                 if "frame_cov_fp64" in c5r else ""))
-rows += [
-    ("LT_LS + PS_Linear (config 2)",
-     f"{l65['frames_per_s']:.2g} frames/s at 65,536 frames ({l65['achieved_GBs'] / 1000:.1f} TB/s algorithmic); "
-     f"{ls['frames_per_s']:.2g} at 1,048,576 ({ls['achieved_GBs'] / 1000:.1f} TB/s algorithmic"
-     + (f", {ls['real_GBs'] / 1000:.1f} TB/s of PMC-measured HBM traffic" if "real_GBs" in ls else "")
-     + "; ±8% with where the buffers land in HBM)"),
-    ("front end, 15 blocks per frame",
-     f"{fe['blocks']['frames_per_s']:.2g} frames/s, {fe['blocks']['achieved_GBs'] / 1000:.1f} TB/s"),
-    ("reference-format (`long double complex`) conversion on the device",
-     f"{lc['to_complex']['achieved_GBs'] / 1000:.1f} TB/s, bit-identical to the C casts"),
+     f"{fps('cov_mode', 65536, 'ms_per_step')} frames/s (solve {100 * lg.get('cov_mode', {}).get('solve_frac_fp64_peak', 0):.0f}% "
+     f"of FP64 peak); MFMA `C·W` {g('apply_kernel', 'achieved_tflops', '{:.1f}')} TF"),
+    ("PS_MMSE, model covariance = a 4 / 8 / 16 / 24 / 53-tap power-delay profile",
+     " / ".join(fps("lowrank_" + L, 65536) for L in ("L4", "L8", "L16", "L24", "L53")) + " frames/s"),
+    ("configs[4] in `main.c` semantics (REF + LS family + eq), 1,048,576 frames",
+     f"{fps('config5_ref_fp64')} frames/s fp64; {fps('config5_ref_mixed_fp64_solve_fp32_ls')} with fp32 LS outputs; "
+     f"with each frame's PS_MMSE on its own LT_LS (FRAME_COV, as main.c:37-53) {fps('config5_ref_frame_cov_fp64')}"),
+    ("REF PS_MMSE with each frame's own LT_LS (FRAME_COV), 65,536 frames",
+     f"{fps('frame_cov_ref', 65536, 'ms_per_step')} frames/s ({g('frame_cov_ref', 'ms_per_step', '{:.4f}')} ms)"),
+    ("LT_LS + PS_Linear (config 2), 1,048,576 frames",
+     f"{fps('ls_config2', 1 << 20, 'avg_launch_ms')} frames/s ({100 * lg.get('ls_config2', {}).get('frac', 0):.0f}% of "
+     f"8 TB/s algorithmic)"),
+    ("front end, 15 blocks per frame, 65,536 frames",
+     f"{fps('front_blocks', 65536)} frames/s ({100 * lg.get('front_blocks', {}).get('frac', 0):.0f}% of 8 TB/s)"),
     ("headline with frames in host memory (PCIe-inclusive)",
-     f"{hp['frames_per_s']:.2g} frames/s, {hp['pcie_GBs']:.0f} GB/s over PCIe (~{100 * hp['frac_of_h2d_bound']:.0f}% "
+     f"{g('host_pipeline', 'frames_per_s', '{:.2g}')} frames/s (~{100 * lg.get('host_pipeline', {}).get('frac_of_h2d_bound', 0):.0f}% "
      f"of the H2D copy bound)"),
-    (f"CPU (oracle fp64 port, {cb['cores']} cores)",
-     f"{cb['value']:.2g} frames/s, its H within 2.3e-12 of the GPU's; the reference's own per-frame functions in a "
-     f"frames-parallel OpenMP loop: {refc['ls_config2_omp']['value']:.2g} LS, {refc['mmse_ref_mode_omp']['value']:.2g} "
+    (f"CPU (oracle fp64 port, {cb.get('cores', '?')} cores)",
+     f"{cb.get('value', 0):.2g} frames/s; the reference's own functions, frames-parallel OpenMP: "
+     f"{refc.get('ls_config2_omp', {}).get('value', 0):.2g} LS, {refc.get('mmse_ref_mode_omp', {}).get('value', 0):.2g} "
      f"REF MMSE; its PS_MMSE as written takes ~230 s per frame and returns NaN"),
 ]
-table = (f"## Numbers (one MI355X, `profiles/{rnd}_bench.json`; boxes differ by a few %)\n\n| Workload | Rate |\n|---|---|\n"
+table = (f"## Numbers (one MI355X; source: {src})\n\n| Workload | Rate |\n|---|---|\n"
          + "".join(f"| {q} | {v} |\n" for q, v in rows) + "\n")
 p = os.path.join(REPO, "README.md")
 s = open(p).read()
