@@ -3398,23 +3398,12 @@ __device__ __forceinline__ void ref_h(const double2 (&rp)[KSTEPS], const double2
     }
 }
 
-// s of frame ml of the tile from the lane's own pilot kl (x, rx of block blk).
-// ref_sum4's ((t0 + t1) + (t2 + t3)) rb is symmetric under every pairing the
-// lane swaps produce (fp addition commutes), so each lane of the frame forms
-// it as ((own + own^16) + (the same pair sum of lane ^32)) rb: the same bits
-// in all four lanes, and the same bits as ref_sum4 over the pilots in order.
-__device__ __forceinline__ double2 ref_s(double w0, double w1, double w2, double w3, double2 xt, double2 xr, int kl,
-                                         double rb)
-{
-#pragma clang fp contract(off)
-    const double wk = (kl & 2) ? ((kl & 1) ? w3 : w2) : ((kl & 1) ? w1 : w0);
-    const double2 t = ref_term(make_double2(wk, 0.0), xt, xr);
-    const double2 u = cadd(t, shfl_xor_c(t, 16));    // t_{kl} + t_{kl ^ 1}
-    const double2 v = shfl_xor_c(u, 32);              // t_{kl ^ 2} + t_{kl ^ 3}
-    return make_double2((u.x + v.x) * rb, (u.y + v.y) * rb);
-}
-// the same from all 4 pilots loaded by every lane of the frame
-__device__ __forceinline__ double2 ref_s4(const double (&w)[4], const SolveArgs &a, int64_t fa, double rb)
+// s of frame fa from its 4 pilots (x, rx of block blk), loaded by every lane
+// of the frame (the same addresses: one request each), summed in pilot order
+// (ref_sum4): the same bits in all four lanes and as the REF read-out kernels.
+// (Round 5 A/B, profiles/r05_ab_ref_fc.txt: prefetching the pilots with the
+// next tile, or issuing them at the tile's start, was slower every time.)
+__device__ __forceinline__ double2 ref_s(const double (&w)[4], const SolveArgs &a, int64_t fa, double rb)
 {
     if (fa >= a.n) return make_double2(0, 0);
     const int64_t o = fa * a.fs + (int64_t)a.blk * a.bs;
@@ -3424,12 +3413,6 @@ __device__ __forceinline__ double2 ref_s4(const double (&w)[4], const SolveArgs 
     return ref_sum4(t[0], t[1], t[2], t[3], rb);
 }
 
-#ifndef WCE_FC_PILOT_PF
-#define WCE_FC_PILOT_PF 0
-#endif
-#ifndef WCE_FC_EARLY_FIRST
-#define WCE_FC_EARLY_FIRST 0
-#endif
 constexpr int FC_WG_PER_CU = 2;
 struct RefFcShared {
     double2 sc[APPLY_ROWS * ACS];        // Mu rows 0..55 (apply_kernel's staging, no Re + Im copy)
@@ -3463,31 +3446,6 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
                                                                    const double *__restrict__ tx_pre)
 {
     __shared__ RefFcShared sh;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int ml = lane & 15, kl = lane >> 4;
-    const int pil = kl == 0 ? WCE_P0 : kl == 1 ? WCE_P1 : kl == 2 ? WCE_P2 : WCE_P3;
-    const int64_t ng = (a.n + 15) / 16;
-    const int64_t stride = (int64_t)gridDim.x * APPLY_WAVES;
-    int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + wv;
-    // the next tile's inputs: the preamble at the lane's subcarriers, pilot kl of block blk
-    double2 rpn[KSTEPS], xtn, xrn;
-    auto load = [&](int64_t gt) {
-        const int64_t fa = 16 * gt + ml;
-        const bool live = fa < a.n;
-#pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) {
-            const int j = 4 * s + kl;
-            rpn[s] = (live && j < NSC) ? ld2_nt(rx_pre, fa * ps + j) : make_double2(0, 0);
-        }
-#if WCE_FC_PILOT_PF
-        const int64_t o = fa * a.fs + (int64_t)a.blk * a.bs + pil;
-        xtn = live ? ld2(a.tx, o) : make_double2(0, 0);
-        xrn = live ? ld2(a.rx, o) : make_double2(0, 0);
-#endif
-    };
-#if WCE_FC_EARLY_FIRST
-    if (g < ng) load(g);   // the first tile's loads under the staging below
-#endif
     for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
         const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
         sh.sc[i * ACS + j] = ld2(st->Mu, i * CLD + j);   // Mu zero-padded 64 x 64
@@ -3496,28 +3454,36 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
         const int p = e / APPLY_ROWS, k = e - p * APPLY_ROWS;
         sh.wp[e] = ld2(st->Wp, p * NPAD + k);
     }
-    const double *txp = tx_pre ? tx_pre : st->tx_pre;
     __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t ng = (a.n + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * APPLY_WAVES;
+    int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + wv;
     if (g >= ng) return;
-#if !WCE_FC_EARLY_FIRST
-    load(g);
-#endif
+    const double2 *txp = reinterpret_cast<const double2 *>(tx_pre ? tx_pre : st->tx_pre);
     const double rb = 1.0 / st->bcoef;
+    // the next tile's preamble at the lane's subcarriers, in flight under this tile's work
+    double2 rpn[KSTEPS];
+    auto load = [&](int64_t gt) {
+        const int64_t fa = 16 * gt + ml;
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl;
+            rpn[s] = (fa < a.n && j < NSC) ? ld2_nt(rx_pre, fa * ps + j) : make_double2(0, 0);
+        }
+    };
+    load(g);
     for (; g < ng; g += stride) {
         const int64_t f0 = 16 * g, fa = f0 + ml;
+        const bool live = fa < a.n;
         double ar[KSTEPS], ai[KSTEPS];
-        ref_h(rpn, reinterpret_cast<const double2 *>(txp), kl, fa < a.n, ar, ai);
-#if WCE_FC_PILOT_PF
-        const double2 xt = xtn, xr = xrn;
-#endif
+        ref_h(rpn, txp, kl, live, ar, ai);
         if (g + stride < ng) load(g + stride);   // next tile, under this one's work
         double w[4];
         ref_w4(sh.wp, ar, ai, kl, w);
-#if WCE_FC_PILOT_PF
-        RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s(w[0], w[1], w[2], w[3], xt, xr, kl, rb)};
-#else
-        RefFcStore out{a.w, a.ws, f0, a.n, {}, ref_s4(w, a, fa, rb)};
-#endif
+        const double2 sfr = ref_s(w, a, fa, rb);
+        RefFcStore out{a.w, a.ws, f0, a.n, {}, sfr};
         if (kl == 0) sh.s[wv][ml] = out.sm;
         wave_lds_sync();
 #pragma unroll

@@ -166,12 +166,23 @@ def pmc_leg(leg: str, frames: int, write_bytes: float, tol: float = 0.02, waves:
     the launch's algorithmic output bytes `write_bytes` within `tol`.
     Returns (counters, source file) or (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_legs.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_legs.json")), reverse=True)
     if not files:
         return None, "no profiles/*_pmc_legs.json"
-    d = json.load(open(files[-1])).get(leg)
+    # the newest legs file that profiled this leg's CURRENT kernel (a round
+    # re-profiles only the legs whose kernel changed)
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from prof_leg import LEGS
+    want = LEGS.get(leg, (None,))[0]
+    d, src = None, None
+    for f in files:
+        c = json.load(open(f)).get(leg)
+        if c and c.get("kernel") == want:
+            d, src = c, f
+            break
     if not d:
-        return None, f"leg {leg} not profiled"
+        return None, f"leg {leg} ({want}) not profiled"
+    files = [src]
     if d["frames"] != frames:
         return None, f"profiled at {d['frames']} frames, bench launch is {frames}"
     k = d["counters"]
