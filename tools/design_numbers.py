@@ -8,8 +8,17 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 rnd = sys.argv[1] if len(sys.argv) > 1 else "r02"
-d = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_bench.json")))
-legs = json.load(open(os.path.join(REPO, "profiles", f"{rnd}_pmc_legs.json")))
+# round 5+: the full record is the extras file beside the compact bench line
+_full = os.path.join(REPO, "profiles", f"{rnd}_bench_extras.json")
+d = json.load(open(_full if os.path.exists(_full) else os.path.join(REPO, "profiles", f"{rnd}_bench.json")))
+# PMC legs: the newest profile of each leg up to this round (a round re-profiles only the legs it changed)
+import glob  # noqa: E402
+legs, leg_src = {}, {}
+for _f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_legs.json"))):
+    if os.path.basename(_f)[:3] <= rnd:
+        _l = json.load(open(_f))
+        legs.update(_l)
+        leg_src.update({k: os.path.basename(_f) for k in _l})
 r = d["roofline"]
 refc = d["cpu_baseline"].get("reference_code", {})
 rows = []   # (quantity, value); None entries are skipped (never a blank table line)
@@ -179,7 +188,7 @@ if h:
     busy = 3 * v["SQ_ACTIVE_INST_VALU"] / v["SQ_WAVE_CYCLES"]
     traffic = (2 * h["counters"]["FETCH_SIZE"] + h["counters"]["WRITE_SIZE"]) * 1024 / 1e6
     pmc = (f"**PMC**, `mmse_solve_fc_kernel` alone at the bench's launch size (65,536 frames, {h['dispatches']} "
-           f"dispatches per pass), per frame (= per wave). Source: `profiles/{rnd}_pmc_legs.json` "
+           f"dispatches per pass), per frame (= per wave). Source: `profiles/{leg_src.get('headline', rnd + '_pmc_legs.json')}` "
            f"(`tools/pmc_legs.sh`, one pass per counter group).\n"
            f"- {v['SQ_INSTS_VALU']:,.0f} VALU instructions, of which {v['SQ_INSTS_VALU_FMA_F64']:,.0f} are `FMA_F64` and "
            f"{v['SQ_INSTS_VALU_MUL_F64']:,.0f} `MUL_F64`.\n"
