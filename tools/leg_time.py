@@ -43,6 +43,8 @@ def main():
             r = bench.bench_cov_lowrank(
                 wce, lambda R: wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], device=0, Rhh=R), stream,
                 tx, rx, B, args.reps)
+        elif leg == "small_batch":
+            r = bench.bench_small_batch(wce, mk(wce.MMSE_TEXTBOOK), stream)
         else:
             raise SystemExit(f"unknown leg {leg}")
         print(json.dumps({leg: r}), flush=True)
