@@ -2663,12 +2663,13 @@ __device__ __forceinline__ void cm_rows3(const double *__restrict__ M, int nt, c
     hr = p1 - p2;
     hi = (p3 - p1) - p2;
 }
-// Two launches: CPLX = false checks every frame, finishes the tiles whose
-// matching frames are all real (flags 1) and marks matching non-real frames
-// 2; CPLX = true (its own register allocation: the correction holds all of
-// H1) finishes the tiles holding a 2, and exits at once elsewhere.
-template <bool CPLX>
-__global__ __launch_bounds__(256) void cm_kernel(const State *__restrict__ st, SolveArgs a, uint8_t *__restrict__ flags)
+// Two launches: cm_real_kernel (below, persistent) checks every frame,
+// finishes the tiles whose matching frames are all real (flags 1) and marks
+// matching non-real frames 2; cm_cplx_kernel (its own register allocation: the
+// correction holds all of H1) finishes the tiles holding a 2, and exits at
+// once elsewhere.
+__global__ __launch_bounds__(256) void cm_cplx_kernel(const State *__restrict__ st, SolveArgs a,
+                                                      uint8_t *__restrict__ flags)
 {
     const int lane = threadIdx.x & 63;
     const int64_t f0 = ((int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6)) * 16;
@@ -2676,7 +2677,7 @@ __global__ __launch_bounds__(256) void cm_kernel(const State *__restrict__ st, S
     const int ml = lane & 15, kl = lane >> 4;
     const int64_t fa = f0 + ml;
     const bool live = fa < a.n;
-    if (CPLX && __ballot(live && flags[fa] == 2) == 0) return;   // (wave-uniform) nothing left here
+    if (__ballot(live && flags[fa] == 2) == 0) return;   // (wave-uniform) nothing left here
     const int64_t base = live ? fa * a.fs + (int64_t)a.blk * a.bs : 0;
     const uint64_t xm = st->xmask;
     const double ac = st->acoef;
@@ -2699,24 +2700,9 @@ __global__ __launch_bounds__(256) void cm_kernel(const State *__restrict__ st, S
     const uint64_t bb = __ballot(bad), cb = __ballot(cplx);
     const uint32_t ok = ~(uint32_t)((bb | (bb >> 16) | (bb >> 32) | (bb >> 48)) & 0xffffu) & 0xffffu;
     const uint32_t cx = (uint32_t)((cb | (cb >> 16) | (cb >> 32) | (cb >> 48)) & 0xffffu) & ok;
-    if (!CPLX && kl == 0 && live) flags[fa] = !((ok >> ml) & 1u) ? 0 : (cx != 0 ? 2 : 1);
+    (void)cx;
     if (ok == 0) return;                        // (wave-uniform) no frame of this tile matches
     const bool mine = (ok >> ml) & 1u;
-    if (!CPLX && cx != 0) return;               // (wave-uniform) the CPLX launch finishes this tile
-    if (!CPLX) {                                // real symbols: H = K (conj x o rx), block by block
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            v4d hr, hi;
-            cm_rows3(st->Kcm, nt, yr, yi, ml, kl, hr, hi);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * nt + 4 * r + kl;
-                if (mine && i < NSC) st2(a.w, fa * a.ws + i, make_double2(hr[r], hi[r]));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return;
-    }
     // non-real symbols in the tile: all of H1 first (it is the correction's input)
     double h1r[16], h1i[16];   // row 4 s + kl at index s (s = 14, 15: padding rows 56..63)
 #pragma unroll
@@ -3529,6 +3515,76 @@ __global__ __launch_bounds__(256) void ref_w_kernel(const State *__restrict__ st
     }
 }
 
+// The constant-modulus operator's real-symbol pass (round 4's cm_kernel<false>),
+// persistent: K staged once per workgroup in LDS as apply_kernel stages C
+// (plus Re + Im, 3M form), each wave walking 16-frame tiles.  Per tile: x, rx
+// loads, the |x|^2 pattern check and flags, y = conj(x)
+// o rx in the MFMA A layout, H = K y for the matching frames of tiles whose
+// matching frames are all real (apply_tile3: rows 48..52 on 4x4x4); tiles with
+// a matching non-real frame are left to cm_cplx_kernel.
+struct CmStore {
+    double *H;
+    int64_t hs, f0;
+    uint32_t ok;   // bit m: frame f0 + m matches the pattern
+    __device__ void row16(int r, int i, double2 v) const
+    {
+        const int m = (threadIdx.x & 63) / 16 + 4 * r;
+        if ((ok >> m) & 1u) st2(H, (f0 + m) * hs + i, v);
+    }
+    __device__ void row4(int i, double2 v) const
+    {
+        const int m = threadIdx.x & 15;
+        if ((ok >> m) & 1u) st2(H, (f0 + m) * hs + i, v);
+    }
+};
+// (Round 5 A/B, profiles/r05_ab_cm.txt: the next tile's loads prefetched spill
+// at 2 workgroups per CU and lose at 1.)
+__global__ __launch_bounds__(256, APPLY_WG_PER_CU) void cm_real_kernel(const State *__restrict__ st, SolveArgs a,
+                                                                      uint8_t *__restrict__ flags)
+{
+    __shared__ double2 sc[APPLY_ROWS * ACS];
+    __shared__ double scs[APPLY_ROWS * ACS];   // Re k + Im k (3M form)
+    for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
+        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
+        const double2 c = ld2(st->Kcm, i * CLD + j);   // Kcm zero-padded 64 x 64
+        sc[i * ACS + j] = c;
+        scs[i * ACS + j] = c.x + c.y;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int ml = lane & 15, kl = lane >> 4;
+    const int64_t ng = (a.n + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * APPLY_WAVES;
+    const uint64_t xm = st->xmask;
+    for (int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6); g < ng; g += stride) {
+        const int64_t f0 = 16 * g, fa = f0 + ml;
+        const bool live = fa < a.n;
+        const int64_t base = live ? fa * a.fs + (int64_t)a.blk * a.bs : 0;
+        double yr[KSTEPS], yi[KSTEPS];
+        bool bad = !live, cplx = false;
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl;
+            double2 x = make_double2(0, 0), r = x;
+            if (live && j < NSC) {
+                x = ld2(a.tx, base + j);
+                r = ld2(a.rx, base + j);
+                if (!((xm >> j) & 1ull)) x = make_double2(0, 0);
+                bad |= fma(x.x, x.x, x.y * x.y) != st->pcm[j];
+                cplx |= x.y != 0.0;
+            }
+            yr[s] = fma(x.x, r.x, x.y * r.y);    // conj(x) rx
+            yi[s] = fma(x.x, r.y, -x.y * r.x);
+        }
+        const uint64_t bb = __ballot(bad), cb = __ballot(cplx);
+        const uint32_t ok = ~(uint32_t)((bb | (bb >> 16) | (bb >> 32) | (bb >> 48)) & 0xffffu) & 0xffffu;
+        const uint32_t cx = (uint32_t)((cb | (cb >> 16) | (cb >> 32) | (cb >> 48)) & 0xffffu) & ok;
+        if (kl == 0 && live) flags[fa] = !((ok >> ml) & 1u) ? 0 : (cx != 0 ? 2 : 1);
+        if (ok == 0 || cx != 0) continue;        // (wave-uniform) nothing to do / cm_cplx_kernel's tile
+        apply_tile3<true>(sc, scs, yr, yi, ml, kl, CmStore{a.w, a.ws, f0, ok});
+    }
+}
+
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream,
                       const uint8_t *skip)
 {
@@ -3599,8 +3655,9 @@ int launch_cm(const State *st, const SolveArgs &a, uint8_t *flags, void *stream)
     if (a.n <= 0) return WCE_OK;
     if (a.split || !flags) return WCE_EINVAL;
     const int64_t blocks = (a.n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
-    hipLaunchKernelGGL(cm_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, flags);
-    hipLaunchKernelGGL(cm_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, flags);
+    const int64_t pb = tile_blocks((a.n + 15) / 16, APPLY_WAVES * APPLY_WG_PER_CU);
+    hipLaunchKernelGGL(cm_real_kernel, dim3((unsigned)pb), dim3(256), 0, (hipStream_t)stream, st, a, flags);
+    hipLaunchKernelGGL(cm_cplx_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, flags);
     return hip_status(hipGetLastError());
 }
 

@@ -52,8 +52,8 @@ LEGS = {
     "lowrank24": ("mmse_lr_kernel<3, true>", 65536),     # tap-domain Gram (diagonal Rhh, round 4)
     "lowrank53": ("mmse_lr_kernel<0, true>", 65536),     # the same at full rank, spectrum 2e11
     "lowrank8_1m": ("mmse_lr_lane_staged_kernel<8, 2, true>", 1 << 20),   # block 0 only, frame_stride 53
-    "cm16": ("cm_kernel<false>", 65536),         # constant-modulus operator path, 16-tap PDP (round 4)
-    "cm53": ("cm_kernel<false>", 65536),         # the same, 53-tap exp(-0.5 k) (wide spectrum)
+    "cm16": ("cm_real_kernel", 65536),         # constant-modulus operator path, 16-tap PDP (round 4)
+    "cm53": ("cm_real_kernel", 65536),         # the same, 53-tap exp(-0.5 k) (wide spectrum)
 }
 
 
