@@ -18,7 +18,7 @@ constexpr int32_t STATE_LAYOUT = 8;   // State layout version: bump with every c
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
-// others (one RCCL broadcast of sizeof(State) = wce_state_size() bytes, ~430 KB).
+// others (one RCCL broadcast of sizeof(State) = wce_state_size() bytes, ~491 KB).
 // Complex values are {re, im} fp64.
 constexpr int LRL_RMAX = 8;                          // ranks on the lane-per-frame low-rank kernel
 constexpr int LRL_NP = LRL_RMAX * (LRL_RMAX + 1) / 2;  // packed lower-triangle entries of its Gram matrix
