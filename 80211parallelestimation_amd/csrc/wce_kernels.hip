@@ -3588,16 +3588,11 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void cm_real_kernel(const Sta
 int launch_mmse_apply(const State *st, const double *W, double *H, int64_t stride, int64_t n, void *stream,
                       const uint8_t *skip)
 {
-    // the streaming kernel once every wave gets >= 4 tiles (131,072 frames on
-    // 256 CUs); below that one wave round of matvec_kernel is as fast or faster
-    // (profiles/r02_ab_apply.txt)
+    if (n <= 0) return WCE_OK;
+    // the streaming kernel at every size (round 5, profiles/r05_ab_apply.txt:
+    // 65,536 frames 39.0 -> 34.5 us against one tile per wave of matvec_kernel,
+    // bit-identical; round 2's opposite finding predates the 4x4x4 tail rows)
     const int64_t tiles = (n + 15) / 16;
-    if (tiles < 4 * (int64_t)cu_count() * APPLY_WAVES * APPLY_WG_PER_CU) {
-        const int64_t blocks = (n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);
-        hipLaunchKernelGGL((matvec_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                           st->C, nullptr, W, stride, H, nullptr, stride, n, skip);
-        return hip_status(hipGetLastError());
-    }
     static_assert(APPLY_WAVES == LS_WAVES, "tile_blocks counts LS_WAVES waves per workgroup");
     const int64_t blocks = tile_blocks(tiles, APPLY_WAVES * APPLY_WG_PER_CU);
     hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st->C, W, stride, H,

@@ -417,26 +417,28 @@ def main():
                 res["cov_mode"]["solve_pmc_source"] = csrc
             # MFMA counters of exactly this launch (65,536 frames = 4,096 waves of 16
             # frames): the 'apply' leg of tools/pmc_legs.sh
-            ka, asrc = pmc_leg("apply", B, N * 16.0 * B, waves=4 * ((B + 63) // 64))
-            app = {"kernel": "matvec_kernel<false,false,1> = H = C W (v_mfma_f64_16x16x4), COV mode",
+            # its counters from same-size launches (tools/pmc_legs.sh 'apply'); the
+            # grid is capped at 2 workgroups per CU, so check the output bytes
+            ka, asrc = pmc_leg("apply", B, N * 16.0 * B, tol=0.12)
+            app = {"kernel": "apply_kernel = H = C W (v_mfma_f64_16x16x4 + 4x4x4_4b tail rows, C in LDS), COV mode",
                    "avg_launch_ms": t_apply, "achieved_tflops": ach_apply,
                    "frac_fp64_peak": ach_apply / PEAK_FP64_TFLOPS, "pmc_source": asrc,
                    "algorithmic_bytes": 2 * N * 16 * B}
             if ka:
-                waves = 4 * ((B + 63) // 64)
+                tiles = (B + 15) // 16
                 mfma = ka["SQ_INSTS_VALU_MFMA_F64"]             # wave-level f64 MFMA instructions per launch
-                app.update({"waves": waves, "mfma_insts_per_wave": mfma / waves,
+                app.update({"tiles": tiles, "mfma_insts_per_tile": mfma / tiles,
                             "traffic": hbm_bytes(ka),
                             "executed_tflops": mfma_flops(ka) / (t_apply * 1e-3) / 1e12,
                             "mfma_busy_frac_pmc": ka["SQ_VALU_MFMA_BUSY_CYCLES"] / (ka["GRBM_GUI_ACTIVE"] / 8.0 * 256 * 4),
                             "note": "executed = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 flop; 3M (Gauss) form, three real "
-                                    "products per complex one: per 16-frame tile 168 v_mfma_f64_16x16x4 (4 row blocks "
-                                    "of 16, 3 chains x 14 k-steps), 64 x 56 zero-padded (53 x 53 useful); achieved "
-                                    "counts the 4-product 8 n^2 flop of the contract; busy = "
+                                    "products per complex one: per 16-frame tile rows 0..47 3 x 14 x 3 "
+                                    "v_mfma_f64_16x16x4, rows 48..52 14 x 6 v_mfma_f64_4x4x4_4b (56 x 56 executed, "
+                                    "53 x 53 useful); achieved counts the 4-product 8 n^2 flop of the contract; busy = "
                                     "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs)"})
-            # the same product at 1,048,576 frames (the configs[3] batch): past 131,072
-            # frames mmse_apply switches to apply_kernel (C staged in LDS, each wave
-            # streaming 16-frame tiles with the next tile's W loaded under the MFMAs).
+            # the same product at 1,048,576 frames (the configs[3] batch): apply_kernel
+            # (C staged in LDS, each wave streaming 16-frame tiles with the next
+            # tile's W loaded under the MFMAs), 16 tiles per wave.
             # W = the 65,536 solved frames tiled 16 times (device copies), so the
             # operands are real solutions, not zeros.
             nbig = 16 * B

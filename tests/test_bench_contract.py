@@ -112,11 +112,16 @@ def test_leg_rooflines(full):
         if r["traffic"] is not None:
             assert r["traffic"] > 0.95 * r["sector_floor_bytes"]
     app = line.get("apply_kernel")
-    if app and "waves" in app:
+    if app and "waves" in app:   # rounds <= 4: matvec_kernel, one 16-frame tile per wave
         # 3M form: 4 row blocks x 14 k-steps x 3 chains of v_mfma_f64_16x16x4 per 16-frame tile
         assert app["waves"] == 4096 and abs(app["mfma_insts_per_wave"] - 168) < 1e-6
         # executed MFMA flops vs the contract's 8 n^2 per frame: 168 x 2,048 per tile against 16 x 8 x 53^2
         ratio = 168 * 2048 / (16 * 8 * 53 * 53)
+        assert abs(app["executed_tflops"] / app["achieved_tflops"] - ratio) < 0.05 * ratio
+    elif app and "tiles" in app:   # round 5+: apply_kernel at every size
+        # rows 0..47: 3 x 14 x 3 v_mfma_f64_16x16x4; rows 48..52: 14 x 6 v_mfma_f64_4x4x4_4b
+        assert app["tiles"] == 4096 and abs(app["mfma_insts_per_tile"] - (126 + 84)) < 1e-6
+        ratio = (126 * 2048 + 84 * 512) / (16 * 8 * 53 * 53)
         assert abs(app["executed_tflops"] / app["achieved_tflops"] - ratio) < 0.05 * ratio
 
 

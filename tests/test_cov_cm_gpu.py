@@ -125,9 +125,9 @@ def test_constant_modulus_batch(gpu_wce, golden, oracle, L, decay, kern):
 
 
 def test_constant_modulus_large_batch_apply_skip(gpu_wce, golden, oracle):
-    """Dense C at 140,011 frames: the per-frame path's H = C W runs
-    apply_kernel (past 131,072 frames), which must leave the constant-modulus
-    frames' H alone (skip flags); matvec_kernel is the small-batch case above."""
+    """Dense C at 140,011 frames: the per-frame path's H = C W (apply_kernel,
+    several tiles per wave at this size) must leave the constant-modulus
+    frames' H alone (skip flags)."""
     wce = gpu_wce
     inp = golden["inputs"]
     R = pdp_rhh(53, 0.12)

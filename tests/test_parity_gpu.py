@@ -176,10 +176,10 @@ def test_mfma_apply_exact_integers(gpu_wce, golden):
 
 
 def test_apply_kernels_agree_bitwise(gpu_wce, golden):
-    """H = C W on real (non-integer) data: the streaming apply_kernel (batches
-    from 131,072 frames) and matvec_kernel (smaller batches) run the same three
-    Gauss chains (3M form) in the same order, so a frame's H does not depend on
-    the batch size; both within 1e-12 of numpy's W C^T."""
+    """H = C W on real (non-integer) data at two batch sizes: the streaming
+    apply_kernel runs every size since round 5 (a grid capped at 2 workgroups
+    per CU, each wave walking its tiles), so a frame's H does not depend on the
+    batch size or on which wave took its tile; within 1e-12 of numpy's W C^T."""
     inp = golden["inputs"]
     rng = np.random.default_rng(5)
     pdp = np.exp(-0.12 * np.arange(N))
@@ -195,8 +195,8 @@ def test_apply_kernels_agree_bitwise(gpu_wce, golden):
     W = rng.standard_normal((big, N)) + 1j * rng.standard_normal((big, N))
     dW = gpu_wce.DeviceArray.from_numpy(W)
     dHb, dHs = gpu_wce.DeviceArray((big, N), zero=True), gpu_wce.DeviceArray((small, N), zero=True)
-    ctx.mmse_apply(dW, dHb, big)      # apply_kernel
-    ctx.mmse_apply(dW, dHs, small)    # matvec_kernel
+    ctx.mmse_apply(dW, dHb, big)      # 16 tiles per wave
+    ctx.mmse_apply(dW, dHs, small)    # one tile per wave
     gpu_wce.synchronize()
     hb, hs = dHb.numpy(), dHs.numpy()
     assert np.array_equal(hb[:small], hs)

@@ -5,7 +5,7 @@ average over the dispatches of a pass is an average over same-size launches.
 
 legs (bench.py field -> kernel, frames per launch):
   headline   roofline            mmse_solve_fc_kernel             65,536 (TEXTBOOK, 1 wave/frame)
-  apply      apply_kernel        matvec_kernel<false,false,1>     65,536 (COV H = C W, 16 frames/wave)
+  apply      apply_kernel        apply_kernel                     65,536 (COV H = C W, persistent since round 5)
   cov_solve  cov_mode            mmse_solve_kernel<false>         65,536 (COV dense solve)
   ref        ref_mode.b1048576   mmse_ref_flat_kernel          1,048,576 (REF, main.c semantics)
   ls         ls_config2          ls_flat_kernel                1,048,576 (LT_LS + PS_Linear)
@@ -32,8 +32,8 @@ N, NBLK = 53, 15
 
 LEGS = {
     "headline": ("mmse_solve_fc_kernel", 65536),
-    "apply": ("matvec_kernel<false, false, 1>", 65536),
-    "apply1m": ("apply_kernel", 1 << 20),             # the streaming apply past 131,072 frames
+    "apply": ("apply_kernel", 65536),                # round 5: the streaming kernel at every size
+    "apply1m": ("apply_kernel", 1 << 20),             # the same at configs[3]'s batch
     "cov_solve": ("mmse_solve_kernel<false>", 65536),
     "ref": ("mmse_ref_flat_kernel", 1 << 20),
     "ls": ("ls_elem_kernel", 1 << 20),
