@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
-ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm", "fcref", "c5ref_fc"],
+ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm", "fcref", "c5ref_fc", "refmm"],
                 default="config5")
 ap.add_argument("--taps", type=int, default=8, help="lowrank: L-tap PDP covariance (rank L; 53 = decay 0.5)")
 ap.add_argument("--rounds", type=int, default=5)
@@ -38,7 +38,7 @@ for d in args.dirs:
     elif args.leg in ("lowrank", "cm"):   # cm: the same ctx on the constant-modulus operator (wce_ctx_set_modulus)
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rank(args.taps))
-    elif args.leg in ("fcref", "c5ref_fc"):
+    elif args.leg in ("fcref", "c5ref_fc", "refmm"):
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_REF)
     else:
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_TEXTBOOK)
@@ -71,7 +71,7 @@ for d in args.dirs:
             H = outs[4]
         f = (lambda c, fr, o, st, mk: lambda: c.estimate(fr, o, mk, st.handle))(ctx, fr, o, st, mk)
         check = H
-    elif args.leg in ("headline", "lowrank", "cm"):
+    elif args.leg in ("headline", "lowrank", "cm", "refmm"):   # refmm: REF PS_MMSE (mmse_ref_flat_kernel)
         if args.leg == "cm":
             ctx.set_modulus(tx.rows(0)[0, 0])
         H = m.DeviceArray((n, N))
