@@ -171,3 +171,32 @@ def test_ref_fused_factor_kernel_equals_four_launches(gpu_wce, golden, oracle, m
         hls = oracle.lt_ls(tpre, p[f])
         exp = oracle.mmse_ref_repaired(t[f, 2], x[f, 2], F, inp["ow2"], hls, invF)
         assert normrel(H[f], exp) < TOL, f
+
+
+@pytest.mark.parametrize("B", [1, 15, 16, 17, 33])
+def test_ref_fc_kernel_small_ragged_batches(gpu_wce, golden, oracle, B):
+    """ref_fc_kernel (persistent, 16-frame tiles) on batches of 1..33 frames:
+    the last tile partially live, waves without a tile leaving at once; each
+    frame against main.c's PS_MMSE with its own LT_LS (the bit-exact oracle),
+    and the four-launch variant bit for bit."""
+    wce = gpu_wce
+    lib = wce.load()
+    r = golden["ref"]
+    inp = golden["inputs"]
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
+    tx, rx, pre = wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, N))
+    ctx.synth(tx, rx, pre, B, seed=0x1F0 + B)
+    wce.synchronize()
+    t, x, p = tx.numpy(), rx.numpy(), pre.numpy()
+    got = {}
+    try:
+        for v in (0, 1):
+            assert lib.wce_debug_set_variant(4, v) == 0
+            got[v] = ctx.estimate_host(t, x, rx_pre=p, mask=wce.PS_MMSE | wce.FRAME_COV)["ps_mmse"]
+    finally:
+        assert lib.wce_debug_set_variant(4, 0) == 0
+    assert np.array_equal(got[0], got[1])
+    F, invF = from_split(r["F"]), from_split(r["invF"])
+    for f in range(B):
+        exp = oracle.mmse_ref_repaired(t[f, 0], x[f, 0], F, inp["ow2"], oracle.lt_ls(inp["tx_pre"], p[f]), invF)
+        assert normrel(got[0][f], exp) < TOL, f
