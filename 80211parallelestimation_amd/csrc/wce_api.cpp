@@ -40,9 +40,11 @@ struct wce_ctx {
 };
 
 static constexpr int64_t WS_LD = 64;   // row stride (complex) of the workspace vectors
-// workspace arrays of [frames][WS_LD] complex: h | g | u | w | aux (per-block
-// MMSE dots).  MATLAB block averaging without FRAME_COV uses arrays 0..3 as
-// the per-block W rows [frames * 4][WS_LD].
+// workspace arrays of [frames][WS_LD] complex: h | u | w | (unused) | aux
+// (per-block MMSE dots; the constant-modulus flags).  FRAME_COV uses h, u, w
+// (REF in C semantics none: ref_fc_kernel writes H directly); MATLAB block
+// averaging without FRAME_COV uses arrays 0..3 as the per-block W rows
+// [frames * 4][WS_LD].
 static constexpr int64_t WS_ARRAYS = 5;
 
 static thread_local std::string g_err;
