@@ -524,25 +524,32 @@ int wce_ctx_reserve(wce_ctx *c, int64_t n)
 // REF the folded pilot-row map), into the solve arguments.  lt_ready: the
 // caller's LT_LS output already holds H_LT.  REF in C semantics takes one
 // launch (ref_fc_kernel) that writes H = u s itself and sets *done.
+// REF in C semantics runs ref_fc_kernel: one launch, no workspace.  The fused
+// LS epilogue after it must be ref_ls_elem_kernel (the default REF_LS form);
+// the wave-per-frame form takes the general path.
+static bool ref_fc_path(const wce_ctx *c, const wce_frames *in, const wce::SolveArgs &sa)
+{
+    return c->mode == WCE_MMSE_REF && sa.ref_pilots && in->semantics == WCE_SEM_C &&
+           wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0 && wce::variant_value(wce::WCE_VARIANT_REF_LS) == 0;
+}
+
 static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *out, bool lt_ready,
                           wce::SolveArgs &sa, double *ws, bool *done, void *stream)
 {
     const int64_t n = in->n_frames;
     if (!in->rx_pre) return fail(WCE_EINVAL, "WCE_MMSE_FRAME_COV needs per-frame preambles (rx_pre)");
     int rc = WCE_OK;
-    double *hw = ws, *uw = hw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
     const State *st = c->d_state;
     *done = false;
-    // the fused LS epilogue after it must be ref_ls_elem_kernel (the default
-    // REF_LS form); the wave-per-frame form takes the path below
-    if (c->mode == WCE_MMSE_REF && sa.ref_pilots && in->semantics == WCE_SEM_C &&
-        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0 && wce::variant_value(wce::WCE_VARIANT_REF_LS) == 0) {
+    if (ref_fc_path(c, in, sa)) {
         rc = wce::launch_ref_fc(st, sa, reinterpret_cast<const double *>(in->rx_pre), in->pre_stride,
                                 reinterpret_cast<const double *>(in->tx_pre), stream);
         if (rc) return fail(rc, "ref_fc launch (frame covariance)");
         *done = true;
         return WCE_OK;
     }
+    if (!ws) return fail(WCE_EINVAL, "frame covariance workspace missing");
+    double *hw = ws, *uw = hw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
     const double *h = hw;
     int64_t hs = WS_LD;
     if (lt_ready) {
@@ -629,7 +636,7 @@ static int estimate_impl(wce_ctx *c, const wce_frames *in, const wce_outputs *ou
     if (split && n * sa.nblk > INT32_MAX) return fail(WCE_EINVAL, "n_frames * 4 > 2^31 - 1 (MATLAB semantics)");
     std::unique_lock<std::mutex> lk;
     double *ws = nullptr;
-    if (fc || split || cm) {
+    if ((fc && !ref_fc_path(c, in, sa)) || split || cm) {
         wce::Workspace *w = fixed;
         if (!w) {
             w = stream_ws(c, stream, lk);
