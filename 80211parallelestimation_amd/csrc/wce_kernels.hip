@@ -19,10 +19,15 @@
 //                           full-wave publish per pivot, dot_factor); a second
 //                           bordered row (w o x)^T leaves s = w^T X z in the
 //                           Schur complement; H = u s, one launch.
-//   mmse_solve_kernel       dense C (COV): block-cyclic square-root-free LDL',
+//   mmse_solve_kernel       dense C (COV): row-per-lane Cholesky keeping L,
 //                           blocked back-substitution, W = X z;
-//   matvec_kernel           then H = C W on v_mfma_f64_16x16x4_f64 (also the
-//                           per-frame covariance factors, MATLAB block mean).
+//   apply_kernel            then H = C W on v_mfma_f64_16x16x4_f64 + 4x4x4_4b
+//                           (persistent, C staged in LDS, 3M complex form).
+//   matvec_kernel         the same MFMA product with M from L2: the per-frame
+//                         covariance factor u = Mu h, MATLAB's block mean.
+//   ref_fc_kernel         REF PS_MMSE with each frame's own LT_LS covariance
+//                         (main.c:37-53 + 148-212), one persistent launch.
+//   cm_real_kernel        constant-modulus operator H = K (conj(x) o rx).
 //   mmse_solve_ls_kernel  config 5: either solve with the LS family and
 //                         equalization of the same frame in its epilogue.
 //   fc_finish_kernel      MATLAB averaging of the per-block s values.
@@ -31,8 +36,6 @@
 #include <hip/hip_runtime.h>
 #include "wce_internal.h"
 #include "wce_device.h"
-
-// A/B and timing-only switches (tools/variants.sh); defaults are the product.
 
 namespace wce {
 

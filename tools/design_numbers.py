@@ -94,7 +94,7 @@ if lr:
         row("rank 8 at 1,048,576 frames (two-workgroups-per-CU build)",
             f"{b8['ms_per_step']:.3f} ms ({b8['frames_per_s']:.3g} frames/s, {100 * b8['roofline']['frac']:.0f}% of HBM)")
 ap = d["apply_kernel"]
-row("`matvec_kernel` as `H = C·W` (f64 MFMA, COV mode, 65,536 frames = 4,096 waves)",
+row("`apply_kernel` as `H = C·W` (f64 MFMA, COV mode, 65,536 frames = 4,096 16-frame tiles; persistent since round 5)",
     f"{ap['achieved_tflops']:.1f} TFLOP/s algorithmic = {100 * ap['frac_fp64_peak']:.0f}% of FP64 peak; "
     + (f"{ap['executed_tflops']:.1f} TFLOP/s executed; MFMA pipe busy {100 * ap['mfma_busy_frac_pmc']:.0f}% (PMC of "
        f"same-size launches); traffic {ap['traffic'] / 1e6:.0f} MB vs {ap['algorithmic_bytes'] / 1e6:.0f} MB algorithmic"
