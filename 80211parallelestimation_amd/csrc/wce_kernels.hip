@@ -530,6 +530,7 @@ constexpr int CVS = 9;    // row stride (complex) of the panel transpose buffer
 template <int R0>
 struct SolveLdsT {
     static constexpr int ROW0 = R0;
+    static constexpr bool TAP_MAPS = false;   // TapsLds: the tap <-> column maps stay in LDS
     __device__ int ci(int row, int c) const { return (row - R0) * CVS + c; }   // conv element (row, c)
     double2 u[2][64];     // pivot column k (unscaled A[:, k]) ping-pong
     double2 x[64];        // masked tx of the frame (diagonal of X), 0 past 53
@@ -541,7 +542,7 @@ struct SolveLdsT {
             double rd[64];    // r_k = 1 / d_k, 0 past 52
         };
         double2 conv[(56 - R0) * CVS];   // row-per-lane panels: block column -> rows (to_rows)
-        struct {                  // the tap-domain Gram's DFT pair tables (lr_dft53p), past blk / z / rd
+        struct {                  // the tap-domain Gram's DFT pair tables (dft_pairs), past blk / z / rd
             double2 pad_bzr[160];
             double2 pa[32], pb[32];   // c_k + c_{53-k}, c_k - c_{53-k}, k = 1..26 (complex vectors)
             double2 rp[32];           // the same for the real vector |x|^2, {sum, difference}
@@ -551,6 +552,17 @@ struct SolveLdsT {
 using SolveLds = SolveLdsT<0>;
 static_assert(sizeof(SolveLds::tp.pad_bzr) == 2 * sizeof(SolveLds::blk) + sizeof(SolveLds::rd),
               "the tap pair tables start past blk / z / rd");
+// The tap-domain kernel at K0 = 0: the tap <-> column maps, s_j and E are
+// loaded with the frame (one memory round trip instead of three serialized
+// ones); the maps stay in LDS past the factorisation.  E stays in
+// SolveLds::u[0] until the factorisation reuses it and is reloaded for the
+// read-out: keeping it too (13,184 B per wave) measured 2.6% slower, the
+// maps alone 1.6% faster (profiles/r05_ab_taps.txt).
+struct TapsLds : SolveLds {
+    static constexpr bool TAP_MAPS = true;
+    uint8_t tap[64], col[64];   // State::tap_of / col_of (col 0xff: no column)
+};
+static_assert(sizeof(TapsLds) == 12288, "12 waves of the tap kernel per CU");
 // conv element (row, c) at (row - R0) * 9 + c (SolveLdsT::ci): the odd row
 // stride keeps both the block-cyclic stores and the row reads bank-conflict
 // free (an XOR swizzle of an unpadded buffer measured 1% slower: address VALU).
@@ -1563,20 +1575,28 @@ __device__ __forceinline__ double2 lr_dft53_split(const double2 *e, const double
     return xs[lane < NSC ? lane : 0];
 }
 
+// the Gram column -> tap map: kept in LDS (TapsLds) or staged in u[1]
+template <typename L>
+__device__ __forceinline__ int taps_tap(const L &s, const int *tapl, int j)
+{
+    if constexpr (L::TAP_MAPS) return s.tap[j];
+    else return tapl[j];
+}
 template <int K0, typename L = SolveLds>
 __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s, double2 (&A)[RB][RB],
-                                             int lane, int p, int q, double ac, double bc)
+                                             int lane, int p, int q, double ac, double bc, double sl)
 {
     constexpr int RMAX = NSC - 8 * K0;   // Gram column of the border (row 53)
     constexpr int NB = RB - K0;
     const bool act = lane < NSC;
     {   // tables: E, p = |x|^2, v = x o conj(rx)
         const double2 xl = s.x[lane], rl = s.rx[lane];
-        s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
+        if constexpr (!L::TAP_MAPS) s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
         s.u[1][lane] = cmul(xl, cconj(rl));
         s.rd[lane] = fma(xl.x, xl.x, xl.y * xl.y);
     }
     wave_lds_sync();
+    const double2 *E = s.u[0];
     dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
     if (lane >= 1 && lane <= NSC / 2) {
         const double u = s.rd[lane], w = s.rd[NSC - lane];
@@ -1601,7 +1621,7 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
 #pragma unroll 2
         for (int j = 0; j < NSC / 4; ++j) {
             const int k = k0 + j;
-            const double2 w = ld_e(s.u[0], o), va = s.tp.pa[k], vb = s.tp.pb[k];
+            const double2 w = ld_e(E, o), va = s.tp.pa[k], vb = s.tp.pb[k];
             const double2 pp = s.tp.rp[k];   // {p_k + p_{53-k}, p_k - p_{53-k}}
             q.x = fma(pp.x, w.x, q.x);
             q.y = fma(-pp.y, w.y, q.y);
@@ -1645,23 +1665,25 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
     int *tapl = reinterpret_cast<int *>(s.u[1]);   // column j -> its tap (256 B of u[1]) ...
     double *bl = reinterpret_cast<double *>(tapl + 64);   // ... and M's diagonal term b / lambda_j (b past r)
     const int r = st->cov_rank;
-    {
-        tapl[lane] = st->tap_of[lane];
-        const double sl = st->col_s[lane];
+    if constexpr (L::TAP_MAPS) {
         bl[lane] = lane < r ? bc / (sl * sl) : bc;
+    } else {
+        tapl[lane] = st->tap_of[lane];
+        const double sg = st->col_s[lane];
+        bl[lane] = lane < r ? bc / (sg * sg) : bc;
     }
     wave_lds_sync();
 #pragma unroll
     for (int m = 0; m < NB; ++m) {
         const int j1 = p + 8 * m;
         const bool v1 = j1 < r;
-        const int t1 = tapl[j1];
+        const int t1 = taps_tap(s, tapl, j1);
         const double d1 = bl[j1];
 #pragma unroll
         for (int n = 0; n <= m; ++n) {
             const int j2 = q + 8 * n;
             const bool v2 = j2 < r;
-            const int t2 = tapl[j2];
+            const int t2 = taps_tap(s, tapl, j2);
             int dd = t1 - t2;
             dd += dd < 0 ? NSC : 0;
             double2 e;
@@ -1693,10 +1715,19 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     const int p = lane >> 3, q = lane & 7;
     const bool act = lane < NSC;
     const double ac = st->acoef, bc = st->bcoef;
+    double sl = 0.0;
     {
         const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
         const double2 r = act ? ld2(a.rx, base + lane) : make_double2(0, 0);
         const bool inx = act && ((st->xmask >> lane) & 1ull);
+        if constexpr (L::TAP_MAPS) {   // E and the tap maps in the frame's round trip
+            const double2 e = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
+            const int tp = st->tap_of[lane], cl = st->col_of[lane];
+            sl = st->col_s[lane];
+            s.u[0][lane] = e;
+            s.tap[lane] = (uint8_t)tp;
+            s.col[lane] = (uint8_t)cl;
+        }
         s.x[lane] = inx ? t : make_double2(0, 0);
         s.rx[lane] = r;
     }
@@ -1706,7 +1737,7 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
         for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
-    lr_gram_taps<K0>(st, s, A, lane, p, q, ac, bc);
+    lr_gram_taps<K0>(st, s, A, lane, p, q, ac, bc, sl);
     dense_chol<K0>(A, s, p, q, lane);
     double rq[RB];
 #pragma unroll
@@ -1718,30 +1749,37 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     back_blocks_from<RB - 1, K0>(A, P, rq, s, p, q, lane);
     wave_lds_sync();
     // c_t = s_t t_col(t) = w_col(t) on lane t (w_j = z[8 K0 + j], the scaled system's solution); E back into u[0]
-    const int col = act ? st->col_of[lane] : -1;
-    const double ts = st->tap_s[lane];
+    int col;
+    if constexpr (L::TAP_MAPS) {
+        const int c8 = s.col[lane];
+        col = act && c8 != 0xff ? c8 : -1;
+    } else {
+        col = act ? st->col_of[lane] : -1;
+    }
     {
         const double2 wj = s.z[8 * K0 + (col < 0 ? 0 : col)];
         s.u[1][lane] = col < 0 ? make_double2(0.0, 0.0) : wj;
         s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
     }
     wave_lds_sync();
+    const double2 *E = s.u[0];
     dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
     wave_lds_sync();
     const double2 xl = s.x[lane];   // re-read: nothing of the frame stays live across the factorisation
-    double2 y = lr_dft53_split<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z);   // y_k = sum_t c_t E[k t]
+    double2 y = lr_dft53_split<false>(E, s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z);   // y_k = sum_t c_t E[k t]
     if (__ballot(act && xl.y != 0.0) != 0) {   // complex symbols: y += U U^H [(x - conj x) o rho] / b
         const double2 rho = csub(s.rx[lane], cscale(cmul(xl, y), ac));   // b Ryy^-1 rx
         s.blk[lane] = act ? make_double2(-2.0 * xl.y * rho.y, 2.0 * xl.y * rho.x) : make_double2(0, 0);
         wave_lds_sync();   // (also: every lane's read-out reads of the pair tables are done)
         dft_pairs(s.blk, s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
-        const double2 w = lr_dft53_split<true>(s.u[0], s.tp.pa, s.tp.pb, s.blk[0], lane, s.z);   // w_t = sum_k conj(E[k t]) v_k
+        const double2 w = lr_dft53_split<true>(E, s.tp.pa, s.tp.pb, s.blk[0], lane, s.z);   // w_t = sum_k conj(E[k t]) v_k
+        const double ts = st->tap_s[lane];
         s.u[1][lane] = act ? cscale(w, ts * ts / bc) : make_double2(0.0, 0.0);
         wave_lds_sync();
         dft_pairs(s.u[1], s.tp.pa, s.tp.pb, lane);
         wave_lds_sync();
-        y = cadd(y, lr_dft53_split<false>(s.u[0], s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z));
+        y = cadd(y, lr_dft53_split<false>(E, s.tp.pa, s.tp.pb, s.u[1][0], lane, s.z));
     }
     return y;
 }
@@ -1751,7 +1789,7 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
 // K0 = 0 (r > 45: a Gram system as large as Ryy itself) holds all 28
 // register blocks through the product build: 2 waves/SIMD; K0 = 1: 156.
 // TAPS: the tap-domain Gram (State::cov_taps), registers as the dense solve's.
-constexpr int TAPS_WAVES_K0 = SOLVE_WAVES_PER_SIMD;   // the tap form at K0 = 0 (168 VGPRs, 13 spilled at 3 waves/SIMD)
+constexpr int TAPS_WAVES_K0 = SOLVE_WAVES_PER_SIMD;   // the tap form at K0 = 0 (168 VGPRs, 16 B/lane of scratch at 3 waves/SIMD; 36 before the tap maps moved to LDS)
 // K0 >= 2: the LDS holds only rows 8 K0 .. 55 of the panel transposes
 // (SolveLdsT<8 K0>: 9.9 KB per wave at K0 = 2 instead of 12.2), so 4 waves per
 // SIMD fit a CU's 160 KB where 3.25 did.
@@ -1765,7 +1803,7 @@ constexpr int lr_waves(int k0, bool taps)
 template <int K0, bool TAPS = false>
 __global__ __launch_bounds__(64, lr_waves(K0, TAPS)) void mmse_lr_kernel(const State *__restrict__ st, SolveArgs a)
 {
-    __shared__ SolveLdsT<lr_row0(K0)> s;
+    __shared__ std::conditional_t<TAPS && K0 == 0, TapsLds, SolveLdsT<lr_row0(K0)>> s;
     const int64_t g = blockIdx.x;
     const int64_t f = a.split ? g / a.nblk : g;
     const int b = a.split ? (int)(g - f * a.nblk) : 0;
