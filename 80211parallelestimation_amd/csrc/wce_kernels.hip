@@ -3412,16 +3412,14 @@ __device__ __forceinline__ void ref_h(const double2 (&rp)[KSTEPS], const double2
                                       double (&ar)[KSTEPS], double (&ai)[KSTEPS])
 {
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
+    for (int s = 0; s < KSTEPS; ++s) {   // tp: tx_pre staged in LDS, zero past 52
         const int j = 4 * s + kl;
-        double2 h = make_double2(0, 0);
-        if (live && j < NSC && j != WCE_DC) {
-            const double2 t = tp[j];   // tx_pre (LDS: re-read per tile, not held in registers)
-            const double cq = t.x - t.y;
-            h = cdiv(make_double2(cq * rp[s].x, cq * rp[s].y), make_double2(cq * t.x, cq * t.y));
-        }
-        ar[s] = h.x;
-        ai[s] = h.y;
+        const double2 t = tp[j];
+        const double cq = t.x - t.y;
+        const double2 h = cdiv(make_double2(cq * rp[s].x, cq * rp[s].y), make_double2(cq * t.x, cq * t.y));
+        const bool on = live && j < NSC && j != WCE_DC;
+        ar[s] = on ? h.x : 0.0;
+        ai[s] = on ? h.y : 0.0;
     }
 }
 
@@ -3429,7 +3427,11 @@ __device__ __forceinline__ void ref_h(const double2 (&rp)[KSTEPS], const double2
 // of the frame (the same addresses: one request each), summed in pilot order
 // (ref_sum4): the same bits in all four lanes and as the REF read-out kernels.
 // (Round 5 A/B, profiles/r05_ab_ref_fc.txt: prefetching the pilots with the
-// next tile, or issuing them at the tile's start, was slower every time.)
+// next tile, or issuing them at the tile's start, was slower every time.  The
+// kernel loads and uses them BEFORE it issues the next tile's preamble: after
+// those, their wait also covered the next tile's loads (one vmcnt, retired in
+// order); with tx_pre staged in LDS instead of 14 branch-guarded global loads
+// per tile: 50.6 -> 47.2 us per 65,536 frames, profiles/r05_ab_lat.txt.)
 __device__ __forceinline__ double2 ref_s(const double (&w)[4], const SolveArgs &a, int64_t fa, double rb)
 {
     if (fa >= a.n) return make_double2(0, 0);
@@ -3445,6 +3447,7 @@ struct RefFcShared {
     double2 sc[APPLY_ROWS * ACS];        // Mu rows 0..55 (apply_kernel's staging, no Re + Im copy)
     double2 wp[4 * APPLY_ROWS];          // {Ar, Ai} at the 4 pilots, j < 56
     double2 s[APPLY_WAVES][16];          // s of each wave's current tile
+    double2 tp[APPLY_ROWS];              // tx_pre, zero past 52
 };
 static_assert(FC_WG_PER_CU * sizeof(RefFcShared) <= 160 * 1024, "two workgroups per CU");
 
@@ -3481,6 +3484,8 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
         const int p = e / APPLY_ROWS, k = e - p * APPLY_ROWS;
         sh.wp[e] = ld2(st->Wp, p * NPAD + k);
     }
+    if (threadIdx.x < APPLY_ROWS)
+        sh.tp[threadIdx.x] = threadIdx.x < NSC ? ld2(tx_pre ? tx_pre : st->tx_pre, threadIdx.x) : make_double2(0, 0);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ml = lane & 15, kl = lane >> 4;
@@ -3488,7 +3493,7 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
     const int64_t stride = (int64_t)gridDim.x * APPLY_WAVES;
     int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + wv;
     if (g >= ng) return;
-    const double2 *txp = reinterpret_cast<const double2 *>(tx_pre ? tx_pre : st->tx_pre);
+    const double2 *txp = sh.tp;
     const double rb = 1.0 / st->bcoef;
     // the next tile's preamble at the lane's subcarriers, in flight under this tile's work
     double2 rpn[KSTEPS];
@@ -3506,10 +3511,10 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
         const bool live = fa < a.n;
         double ar[KSTEPS], ai[KSTEPS];
         ref_h(rpn, txp, kl, live, ar, ai);
-        if (g + stride < ng) load(g + stride);   // next tile, under this one's work
         double w[4];
         ref_w4(sh.wp, ar, ai, kl, w);
         const double2 sfr = ref_s(w, a, fa, rb);
+        if (g + stride < ng) load(g + stride);   // next tile, under this one's MFMAs
         RefFcStore out{a.w, a.ws, f0, a.n, {}, sfr};
         if (kl == 0) sh.s[wv][ml] = out.sm;
         wave_lds_sync();
@@ -3585,6 +3590,8 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void cm_real_kernel(const Sta
 {
     __shared__ double2 sc[APPLY_ROWS * ACS];
     __shared__ double scs[APPLY_ROWS * ACS];   // Re k + Im k (3M form)
+    __shared__ double spcm[APPLY_ROWS];        // the |x|^2 pattern, j < 56
+    if (threadIdx.x < APPLY_ROWS) spcm[threadIdx.x] = st->pcm[threadIdx.x];
     for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
         const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
         const double2 c = ld2(st->Kcm, i * CLD + j);   // Kcm zero-padded 64 x 64
@@ -3603,19 +3610,30 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void cm_real_kernel(const Sta
         const int64_t base = live ? fa * a.fs + (int64_t)a.blk * a.bs : 0;
         double yr[KSTEPS], yi[KSTEPS];
         bool bad = !live, cplx = false;
+        {   // every load of the tile issued before the first use: one memory round trip
+            // (loads under a per-step branch waited one by one: 14 round trips per tile;
+            // 67 -> 63 us per 65,536 frames, 990 -> 863 us per 1,048,576, profiles/r05_ab_lat.txt)
+            double2 xs[KSTEPS], rs[KSTEPS];
 #pragma unroll
-        for (int s = 0; s < KSTEPS; ++s) {
-            const int j = 4 * s + kl;
-            double2 x = make_double2(0, 0), r = x;
-            if (live && j < NSC) {
-                x = ld2(a.tx, base + j);
-                r = ld2(a.rx, base + j);
-                if (!((xm >> j) & 1ull)) x = make_double2(0, 0);
-                bad |= fma(x.x, x.x, x.y * x.y) != st->pcm[j];
-                cplx |= x.y != 0.0;
+            for (int s = 0; s < KSTEPS; ++s) {
+                const int j = 4 * s + kl, jc = j < NSC ? j : NSC - 1;   // clamped: a valid address, never used
+                xs[s] = ld2(a.tx, base + jc);
+                rs[s] = ld2(a.rx, base + jc);
             }
-            yr[s] = fma(x.x, r.x, x.y * r.y);    // conj(x) rx
-            yi[s] = fma(x.x, r.y, -x.y * r.x);
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s) {
+                const int j = 4 * s + kl;
+                const bool on = live && j < NSC;
+                double2 x = make_double2(0, 0), r = x;
+                if (on) {
+                    x = ((xm >> j) & 1ull) ? xs[s] : make_double2(0, 0);
+                    r = rs[s];
+                    bad |= fma(x.x, x.x, x.y * x.y) != spcm[j];
+                    cplx |= x.y != 0.0;
+                }
+                yr[s] = fma(x.x, r.x, x.y * r.y);    // conj(x) rx
+                yi[s] = fma(x.x, r.y, -x.y * r.x);
+            }
         }
         const uint64_t bb = __ballot(bad), cb = __ballot(cplx);
         const uint32_t ok = ~(uint32_t)((bb | (bb >> 16) | (bb >> 32) | (bb >> 48)) & 0xffffu) & 0xffffu;
