@@ -14,10 +14,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
 
-@pytest.mark.skipif(not shutil.which("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
-def test_no_dpp_source_hazards():
+@pytest.fixture(scope="module")
+def asm_text():
+    if not shutil.which("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not installed")
     import isa_check
-    text = isa_check.compile_asm()
+    return isa_check.compile_asm()
+
+
+def test_no_dpp_source_hazards(asm_text):
+    import isa_check
+    text = asm_text
     n = sum(1 for i in isa_check.instructions(text) if "_dpp" in i.split()[0])
     assert n > 600, "the headline's DPP in-panel FMAs are missing"
     assert isa_check.dpp_hazards(text) == []
@@ -49,3 +56,26 @@ def test_compiler_dpp_after_a_label_is_the_compilers():
     dpp = "v_mov_b32_dpp v30, v24 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
     assert isa_check.dpp_hazards(f"s_or_b64 exec, exec, s[0:1]\n.LBB0_3:\n{dpp}\n") == []
     assert len(isa_check.dpp_hazards(f"v_mov_b32 v24, v2\n{dpp}\n")) == 1
+
+
+def test_streaming_kernels_issue_their_loads_together(asm_text):
+    """Round 5 found two streaming MFMA kernels whose per-tile loads sat under
+    per-element branches, each waited before the next was issued (14 memory
+    round trips per tile instead of one): a regression guard on the compiled
+    code (tools/isa_check.py --rounds; profiles/r05_ab_lat.txt)."""
+    import isa_check
+    bodies = isa_check.kernel_bodies(asm_text)
+    rounds = {n: isa_check.load_rounds(b) for n, b in bodies.items()}
+    cm = [r for n, r in rounds.items() if "cm_real_kernel" in n]
+    fc = [r for n, r in rounds.items() if "ref_fc_kernel" in n]
+    assert cm and fc
+    assert max(cm) <= 3, rounds
+    assert max(fc) <= 6, rounds
+
+
+def test_load_rounds_counts_serialized_loads():
+    import isa_check
+    serial = ["global_load_dwordx4 v[0:3], v[0:1], off", "s_waitcnt vmcnt(0)"] * 3
+    together = ["global_load_dwordx4 v[0:3], v[0:1], off"] * 3 + ["s_waitcnt vmcnt(0)"]
+    assert isa_check.load_rounds(serial) == 2
+    assert isa_check.load_rounds(together) == 0

@@ -108,7 +108,47 @@ def compile_asm(flags=()):
     return text
 
 
+def kernel_bodies(text: str):
+    """{mangled kernel name: its instruction lines} of a compiled .s file."""
+    out, name, buf = {}, None, []
+    for line in text.splitlines():
+        m = re.match(r"^(_Z[A-Za-z0-9_]+):", line)
+        if m:
+            name, buf = m.group(1), []
+            continue
+        if name:
+            buf.append(line)
+            if "s_endpgm" in line:
+                out[name] = buf
+                name = None
+    return out
+
+
+def load_rounds(body) -> int:
+    """Serialized global-memory round trips, counted statically: the number of
+    global loads issued after a vmcnt wait that itself followed a load (a load
+    that could not be issued with the ones before it).  A kernel whose loads sit
+    under per-element branches, each waited before the next is issued, scores
+    one per load (round 5: cm_real_kernel 14 -> 2, ref_fc_kernel 16 -> 5).
+    Branch-guarded cold paths count too: compare a kernel with itself."""
+    state, n = None, 0
+    for line in body:
+        t = line.strip().split(";")[0].strip()
+        if t.startswith("global_load") or t.startswith("buffer_load"):
+            if state == "W":
+                n += 1
+            state = "L"
+        elif "vmcnt(" in t and state == "L":
+            state = "W"
+    return n
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--rounds":   # serialized load round trips per kernel
+        text = open(sys.argv[2]).read() if len(sys.argv) > 2 else compile_asm()
+        for name, body in sorted(kernel_bodies(text).items()):
+            print(f"{load_rounds(body):4d}  {name}")
+        return
     text = open(sys.argv[1]).read() if len(sys.argv) > 1 else compile_asm()
     n_dpp = sum(1 for i in instructions(text) if "_dpp" in i.split()[0])
     bad = dpp_hazards(text)
