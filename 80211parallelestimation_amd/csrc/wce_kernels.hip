@@ -2169,13 +2169,29 @@ __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_
         __shared__ LrLaneLds s[4];
         const double2 *Pg = reinterpret_cast<const double2 *>(st->Pk);
         const double2 *Ug = reinterpret_cast<const double2 *>(st->U);
-        if constexpr (TQ) {
-            for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x)
-                sP[e] = ld2(st->dft, ((e / NPR) * (e % NPR)) % NSC);
-        } else {
-            for (int e = threadIdx.x; e < NSC * NPR; e += blockDim.x) sP[e] = Pg[(e / NPR) * LRL_NP + e % NPR];
+        {   // P_k (TQ: E[k s]) and U: every load issued before the first LDS store
+            constexpr int NP = NSC * NPR, NU = NSC * R;
+            constexpr int IP = (NP + 255) / 256, IU = (NU + 255) / 256;
+            double2 vp[IP], vu[IU];
+#pragma unroll
+            for (int it = 0; it < IP; ++it) {
+                const int e = min((int)threadIdx.x + 256 * it, NP - 1);
+                if constexpr (TQ) vp[it] = ld2(st->dft, ((e / NPR) * (e % NPR)) % NSC);
+                else vp[it] = Pg[(e / NPR) * LRL_NP + e % NPR];
+            }
+#pragma unroll
+            for (int it = 0; it < IU; ++it) {
+                const int e = min((int)threadIdx.x + 256 * it, NU - 1);
+                vu[it] = Ug[(e / R) * CLD + e % R];
+            }
+            // stores unguarded: a thread past the end rewrites the last element with
+            // the value it loaded from there (a guard lets the compiler sink the
+            // loads into it, one round trip each)
+#pragma unroll
+            for (int it = 0; it < IP; ++it) sP[min((int)threadIdx.x + 256 * it, NP - 1)] = vp[it];
+#pragma unroll
+            for (int it = 0; it < IU; ++it) sU[min((int)threadIdx.x + 256 * it, NU - 1)] = vu[it];
         }
-        for (int e = threadIdx.x; e < NSC * R; e += blockDim.x) sU[e] = Ug[(e / R) * CLD + e % R];
         __syncthreads();
         lr_lane_body<R, true, true, TQ>(st, a, &s[threadIdx.x >> 6], 64, sP, sU);
     } else {
@@ -3210,6 +3226,34 @@ constexpr int APPLY_WG_PER_CU = 2;
 constexpr int ACS = 58;
 // staged rows of C: 56 (rows 48..55 are the last ones read)
 constexpr int APPLY_ROWS = 56;
+// A 56 x 56 complex matrix (global rows of stride CLD, zero-padded 64 x 64)
+// into LDS rows of stride ACS, and Re + Im beside it when scs: every thread's
+// 13 loads issued before its first LDS store.  The plain strided loop waited
+// each load before its store, 13 memory round trips at the start of every
+// workgroup (profiles/r05_ab_stage.txt).
+constexpr int STAGE_N = APPLY_ROWS * 4 * KSTEPS;   // 3,136 elements
+constexpr int STAGE_IT = (STAGE_N + 255) / 256;    // 13 per thread of a 256-thread workgroup
+__device__ __forceinline__ void stage_load(const double *M, double2 (&v)[STAGE_IT])
+{
+#pragma unroll
+    for (int it = 0; it < STAGE_IT; ++it) {
+        const int e = min((int)threadIdx.x + 256 * it, STAGE_N - 1);   // past the end: a valid address, not stored
+        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
+        v[it] = ld2(M, i * CLD + j);
+    }
+}
+__device__ __forceinline__ void stage_store(const double2 (&v)[STAGE_IT], double2 *sc, double *scs)
+{
+#pragma unroll
+    for (int it = 0; it < STAGE_IT; ++it) {
+        const int e = (int)threadIdx.x + 256 * it;
+        if (e < STAGE_N) {
+            const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
+            sc[i * ACS + j] = v[it];
+            if (scs) scs[i * ACS + j] = v[it].x + v[it].y;
+        }
+    }
+}
 __device__ __forceinline__ void apply_load(const double *X, int64_t xs, int64_t n, int64_t g, int ml, int kl,
                                            double2 (&w)[KSTEPS], bool done = false)
 {
@@ -3338,11 +3382,10 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void apply_kernel(const doubl
 {
     __shared__ double2 sc[APPLY_ROWS * ACS];
     __shared__ double scs[APPLY_ROWS * ACS];   // Re c + Im c (3M form)
-    for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
-        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
-        const double2 c = ld2(M, i * CLD + j);   // M zero-padded 64 x 64
-        sc[i * ACS + j] = c;
-        scs[i * ACS + j] = c.x + c.y;
+    {
+        double2 v[STAGE_IT];
+        stage_load(M, v);   // M zero-padded 64 x 64
+        stage_store(v, sc, scs);
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -3476,16 +3519,16 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
                                                                    const double *__restrict__ tx_pre)
 {
     __shared__ RefFcShared sh;
-    for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
-        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
-        sh.sc[i * ACS + j] = ld2(st->Mu, i * CLD + j);   // Mu zero-padded 64 x 64
+    {   // Mu, the pilot-row map and tx_pre in one memory round trip
+        const int e = min((int)threadIdx.x, 4 * APPLY_ROWS - 1), p = e / APPLY_ROWS, k = e - p * APPLY_ROWS;
+        const double2 wpv = ld2(st->Wp, p * NPAD + k);
+        const double2 tpv = ld2(tx_pre ? tx_pre : st->tx_pre, min((int)threadIdx.x, NSC - 1));
+        double2 v[STAGE_IT];
+        stage_load(st->Mu, v);   // Mu zero-padded 64 x 64
+        if (threadIdx.x < 4 * APPLY_ROWS) sh.wp[threadIdx.x] = wpv;
+        if (threadIdx.x < APPLY_ROWS) sh.tp[threadIdx.x] = threadIdx.x < NSC ? tpv : make_double2(0, 0);
+        stage_store(v, sh.sc, nullptr);
     }
-    for (int e = threadIdx.x; e < 4 * APPLY_ROWS; e += 256) {
-        const int p = e / APPLY_ROWS, k = e - p * APPLY_ROWS;
-        sh.wp[e] = ld2(st->Wp, p * NPAD + k);
-    }
-    if (threadIdx.x < APPLY_ROWS)
-        sh.tp[threadIdx.x] = threadIdx.x < NSC ? ld2(tx_pre ? tx_pre : st->tx_pre, threadIdx.x) : make_double2(0, 0);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ml = lane & 15, kl = lane >> 4;
@@ -3591,12 +3634,12 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void cm_real_kernel(const Sta
     __shared__ double2 sc[APPLY_ROWS * ACS];
     __shared__ double scs[APPLY_ROWS * ACS];   // Re k + Im k (3M form)
     __shared__ double spcm[APPLY_ROWS];        // the |x|^2 pattern, j < 56
-    if (threadIdx.x < APPLY_ROWS) spcm[threadIdx.x] = st->pcm[threadIdx.x];
-    for (int e = threadIdx.x; e < APPLY_ROWS * 4 * KSTEPS; e += 256) {
-        const int i = e / (4 * KSTEPS), j = e - i * (4 * KSTEPS);
-        const double2 c = ld2(st->Kcm, i * CLD + j);   // Kcm zero-padded 64 x 64
-        sc[i * ACS + j] = c;
-        scs[i * ACS + j] = c.x + c.y;
+    {
+        const double pc = st->pcm[threadIdx.x & (NPAD - 1)];
+        double2 v[STAGE_IT];
+        stage_load(st->Kcm, v);   // Kcm zero-padded 64 x 64
+        if (threadIdx.x < APPLY_ROWS) spcm[threadIdx.x] = pc;
+        stage_store(v, sc, scs);
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
