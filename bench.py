@@ -376,7 +376,7 @@ def main():
     if not args.no_extras and dist.rank == 0:
         try:
             # the general path: dense C (WCE_MMSE_COV, full-rank model Rhh): solve with
-            # back-substitution, then H = C W on the f64 MFMA (matvec_kernel).
+            # back-substitution, then H = C W on the f64 MFMA (apply_kernel).
             # Rank 0 only; no collective.
             reps = max(5, args.steps)
             pdp = np.exp(-0.12 * np.arange(N))
@@ -460,7 +460,7 @@ def main():
             # its MFMA counters from same-size launches (tools/pmc_legs.sh apply1m);
             # the grid is capped at 2 workgroups per CU, so check the output bytes:
             # WRITE_SIZE runs ~9% over them (the 5-row last output tile writes
-            # partial 64-B sectors, as matvec_kernel's does)
+            # partial 64-B sectors)
             kb, bsrc = pmc_leg("apply1m", nbig, N * 16.0 * nbig, tol=0.12)
             app["frames_1M"]["pmc_source"] = bsrc
             if kb:

@@ -4,7 +4,7 @@ WiFi_channel_estimation_PS_MMSE.m:29-32).
 Ryy = a X C X^H + b I depends on a frame's symbols only through P = |x|^2 and
 their phases; for PSK frames P is the batch's.  K = (a C P + b I)^-1 C is then
 formed once (80 bits, host) and a matching frame takes H = K (conj x o rx)
-(+ the correction for non-real x) on f64 MFMA (cm_kernel); every other frame
+(+ the correction for non-real x) on f64 MFMA (cm_real_kernel, cm_cplx_kernel); every other frame
 runs the per-frame kernels, which skip the flagged ones.  Checked here:
   - every frame against the long double unified solve with C formed in 80
     bits (oracle_py.mmse_unified) at 1e-10, sampled;
