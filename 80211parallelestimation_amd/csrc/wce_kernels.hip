@@ -509,15 +509,19 @@ __global__ __launch_bounds__(256) void ref_ls_elem_kernel(const State *__restric
 // shrinking trailing matrix evenly over lanes.  Row 53 holds conj(rx), so the
 // factorisation of [[Ryy, rx], [rx', *]] also runs the forward solve.
 //
-// Square-root-free LDL' (Ryy = L D L', L unit lower): step k needs only
-// r_k = 1/d_k (v_rcp_f64 + 2 Newton steps), no sqrt and no IEEE divide.
-// Columns stay UNSCALED in registers (u = L d): r_k is applied once to the
-// broadcast column operand, and folded into the back-substitution sums, so
-// the factorisation never rewrites a column under a divergent branch (which
-// costs phi copies on every step).  One-step lookahead: the block column
-// holding k+1 is updated first, the next pivot is formed and its column is
-// published to the other half of a ping-pong LDS buffer, then the bulk of
-// step k is issued, hiding the pivot chain and the LDS round trip.
+// Cholesky (Ryy = L L'): pivot k publishes c_k = u_k / sqrt(d_k) (one
+// v_rsq_f64 and a third-order refinement step, rsq_nr / rsq_uniform), so both
+// rank-1 operands are read as published.  Each 8-column panel runs row-per-lane
+// (chol_panel: lane l holds A[l][8 KB + c], one full-wave store publishes the
+// pivot column, in-panel operands by DPP64 row_newbcast); the trailing blocks
+// stay block-cyclic.  One-step lookahead: the column holding k + 1 is updated
+// first, the next pivot formed and published to the other half of a ping-pong
+// LDS buffer, then the bulk of step k is issued, hiding the pivot chain and the
+// LDS round trip.  Dead lanes (upper halves of diagonal blocks, padding row
+// 55, panel rows above the pivot) are off in EXEC for their FMAs (cmsub_live):
+// the kernels run at the board's power cap, and the saved lane energy is clock.
+// (Round 1's square-root-free LDL' on the block-cyclic grid was retired in
+// round 4; DESIGN.md s5 has the measurements.)
 // =====================================================================
 constexpr int RB = 7;     // 7 x 8 = 56 >= 54 rows
 typedef double v4d __attribute__((ext_vector_type(4)));   // one v_mfma_f64_16x16x4 accumulator
