@@ -2744,19 +2744,30 @@ __global__ __launch_bounds__(256) void cm_cplx_kernel(const State *__restrict__ 
     const double ac = st->acoef;
     double yr[KSTEPS], yi[KSTEPS];
     bool bad = !live, cplx = false;
+    {   // every load of the tile issued before the first use (cm_real_kernel's form;
+        // QPSK frames 138 -> 131 us per 65,536, 1.16 -> 1.01 ms per 524,288, profiles/r05_ab_cmq.txt)
+        double2 xs[KSTEPS], rs[KSTEPS];
+        double pcs[KSTEPS];
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-        const int j = 4 * s + kl;
-        double2 x = make_double2(0, 0), r = x;
-        if (live && j < NSC) {
-            x = ld2(a.tx, base + j);
-            r = ld2(a.rx, base + j);
-            if (!((xm >> j) & 1ull)) x = make_double2(0, 0);
-            bad |= fma(x.x, x.x, x.y * x.y) != st->pcm[j];
-            cplx |= x.y != 0.0;
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl, jc = j < NSC ? j : NSC - 1;
+            xs[s] = ld2(a.tx, base + jc);
+            rs[s] = ld2(a.rx, base + jc);
+            pcs[s] = st->pcm[jc];
         }
-        yr[s] = fma(x.x, r.x, x.y * r.y);    // conj(x) rx
-        yi[s] = fma(x.x, r.y, -x.y * r.x);
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl;
+            double2 x = make_double2(0, 0), r = x;
+            if (live && j < NSC) {
+                x = ((xm >> j) & 1ull) ? xs[s] : make_double2(0, 0);
+                r = rs[s];
+                bad |= fma(x.x, x.x, x.y * x.y) != pcs[s];
+                cplx |= x.y != 0.0;
+            }
+            yr[s] = fma(x.x, r.x, x.y * r.y);    // conj(x) rx
+            yi[s] = fma(x.x, r.y, -x.y * r.x);
+        }
     }
     const uint64_t bb = __ballot(bad), cb = __ballot(cplx);
     const uint32_t ok = ~(uint32_t)((bb | (bb >> 16) | (bb >> 32) | (bb >> 48)) & 0xffffu) & 0xffffu;
@@ -2777,20 +2788,27 @@ __global__ __launch_bounds__(256) void cm_cplx_kernel(const State *__restrict__ 
         }
         __builtin_amdgcn_sched_barrier(0);
     }
-    // y2 = (x - conj x) o (rx - a x o H1): the frame's loads again (L2-resident)
+    // y2 = (x - conj x) o (rx - a x o H1): the frame's loads again (L2-resident), all issued first
+    {
+        double2 xs[KSTEPS], rs[KSTEPS];
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-        const int j = 4 * s + kl;
-        double2 x = make_double2(0, 0), r = x;
-        if (mine && j < NSC) {
-            x = ld2(a.tx, base + j);
-            r = ld2(a.rx, base + j);
-            if (!((xm >> j) & 1ull)) x = make_double2(0, 0);
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl, jc = j < NSC ? j : NSC - 1;
+            xs[s] = ld2(a.tx, base + jc);
+            rs[s] = ld2(a.rx, base + jc);
         }
-        const double2 rho = csub(r, cscale(cmul(x, make_double2(h1r[s], h1i[s])), ac));
-        yr[s] = -2.0 * x.y * rho.y;
-        yi[s] = 2.0 * x.y * rho.x;
-        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // 4 subcarriers' loads in flight at a time
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+            const int j = 4 * s + kl;
+            double2 x = make_double2(0, 0), r = x;
+            if (mine && j < NSC) {
+                x = ((xm >> j) & 1ull) ? xs[s] : make_double2(0, 0);
+                r = rs[s];
+            }
+            const double2 rho = csub(r, cscale(cmul(x, make_double2(h1r[s], h1i[s])), ac));
+            yr[s] = -2.0 * x.y * rho.y;
+            yi[s] = 2.0 * x.y * rho.x;
+        }
     }
     const double rb = 1.0 / st->bcoef;
 #pragma unroll

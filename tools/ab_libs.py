@@ -14,7 +14,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
-ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm", "fcref", "c5ref_fc", "refmm"],
+ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm", "cmq", "fcref", "c5ref_fc",
+                                 "refmm"],
                 default="config5")
 ap.add_argument("--taps", type=int, default=8, help="lowrank: L-tap PDP covariance (rank L; 53 = decay 0.5)")
 ap.add_argument("--rounds", type=int, default=5)
@@ -35,17 +36,28 @@ for d in args.dirs:
     if args.leg in ("dense", "apply"):
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rhh())
-    elif args.leg in ("lowrank", "cm"):   # cm: the same ctx on the constant-modulus operator (wce_ctx_set_modulus)
+    elif args.leg in ("lowrank", "cm", "cmq"):   # cm(q): the same ctx on the constant-modulus operator (wce_ctx_set_modulus)
         import prof_leg
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rank(args.taps))
     elif args.leg in ("fcref", "c5ref_fc", "refmm"):
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_REF)
     else:
         ctx = m.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], m.MMSE_TEXTBOOK)
-    tx, rx, pre = m.DeviceArray((n, NB, N)), m.DeviceArray((n, NB, N)), m.DeviceArray((n, N))
-    ctx.synth(tx, rx, pre, n, seed=0x80211)
+    if args.leg == "cmq":   # QPSK frames (non-real symbols of one modulus: cm_real_kernel flags, cm_cplx_kernel solves)
+        rng = np.random.default_rng(7)
+        A = 8.8753
+        xq = A * (rng.choice([-1.0, 1.0], (n, 1, N)) + 1j * rng.choice([-1.0, 1.0], (n, 1, N))) / np.sqrt(2)
+        xq[:, :, 26] = 0
+        hq = 1e-2 * np.exp(1j * rng.uniform(0, 2 * np.pi, (n, 1, 1)))
+        rq = hq * xq + np.sqrt(inp["ow2"] / 2) * (rng.standard_normal(xq.shape) + 1j * rng.standard_normal(xq.shape))
+        tx, rx = m.DeviceArray.from_numpy(xq), m.DeviceArray.from_numpy(rq)
+        pre = None
+        keep = [tx, rx]
+    else:
+        tx, rx, pre = m.DeviceArray((n, NB, N)), m.DeviceArray((n, NB, N)), m.DeviceArray((n, N))
+        ctx.synth(tx, rx, pre, n, seed=0x80211)
+        keep = [tx, rx, pre]
     m.synchronize()   # synth runs on the null stream; the legs on st
-    keep = [tx, rx, pre]
     if args.leg == "config5":
         outs = [m.DeviceArray((n, N), np.complex64) for _ in range(4)] + [m.DeviceArray((n, N))]
         eq = m.DeviceArray((n, NB, N), np.complex64)
@@ -71,11 +83,13 @@ for d in args.dirs:
             H = outs[4]
         f = (lambda c, fr, o, st, mk: lambda: c.estimate(fr, o, mk, st.handle))(ctx, fr, o, st, mk)
         check = H
-    elif args.leg in ("headline", "lowrank", "cm", "refmm"):   # refmm: REF PS_MMSE (mmse_ref_flat_kernel)
+    elif args.leg in ("headline", "lowrank", "cm", "cmq", "refmm"):   # refmm: REF PS_MMSE (mmse_ref_flat_kernel)
         if args.leg == "cm":
             ctx.set_modulus(tx.rows(0)[0, 0])
+        if args.leg == "cmq":
+            ctx.set_modulus(xq[0, 0])
         H = m.DeviceArray((n, N))
-        fr = ctx.frames(tx, rx, n)
+        fr = ctx.frames(tx, rx, n, frame_stride=N, block_stride=N) if args.leg == "cmq" else ctx.frames(tx, rx, n)
         o = m.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
         f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.PS_MMSE, st.handle))(ctx, fr, o, st, m)
         keep.append(H)
