@@ -67,9 +67,11 @@ def test_streaming_kernels_issue_their_loads_together(asm_text):
     bodies = isa_check.kernel_bodies(asm_text)
     rounds = {n: isa_check.load_rounds(b) for n, b in bodies.items()}
     cm = [r for n, r in rounds.items() if "cm_real_kernel" in n]
+    cc = [r for n, r in rounds.items() if "cm_cplx_kernel" in n]   # K / C fragments stay L2 reads per k-step
     fc = [r for n, r in rounds.items() if "ref_fc_kernel" in n]
-    assert cm and fc
+    assert cm and cc and fc
     assert max(cm) <= 3, rounds
+    assert max(cc) <= 65, rounds   # 90 with the per-subcarrier loads
     assert max(fc) <= 6, rounds
 
 
