@@ -2598,6 +2598,14 @@ __device__ __forceinline__ bool tile_done(const uint8_t *__restrict__ skip, int6
     const int64_t f = f0 + (lane & 15);
     return __ballot(f < n && skip[f] == 0) == 0;
 }
+// bit m: frame f0 + m of the tile exists and is not flagged done -- one load per
+// lane per tile, where a per-store skip[] test waited a round trip per store
+__device__ __forceinline__ uint32_t tile_keep(const uint8_t *__restrict__ skip, int64_t f0, int64_t n, int lane)
+{
+    const int64_t f = f0 + (lane & 15);
+    const bool k = f < n && !(skip && skip[f]);
+    return (uint32_t)__ballot(k) & 0xffffu;
+}
 
 // H = C W (and the per-frame-covariance factors) in the 3M (Gauss) form: three
 // real MFMA chains per complex product, P1 = sum Re w Re c, P2 = sum Im w Im c,
@@ -3381,20 +3389,20 @@ __device__ __forceinline__ void apply_tile3(const double2 *sc, const double *scs
     if (kl == 0) out.row4(52, make_double2(a1 - b1, (g1 - a1) - b1));   // rows 53..55: padding, never stored
 }
 
-// apply_kernel's stores: H = C W rows of the live, not-skipped frames
+// apply_kernel's stores: H = C W rows of the live, not-skipped frames (tile_keep)
 struct ApplyStore {
     double *Y;
-    int64_t ys, f0, n;
-    const uint8_t *skip;
+    int64_t ys, f0;
+    uint32_t keep;   // bit m: frame f0 + m
     __device__ void row16(int r, int i, double2 v) const
     {
-        const int64_t fr = f0 + (threadIdx.x & 63) / 16 + 4 * r;
-        if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, v);
+        const int m = (threadIdx.x & 63) / 16 + 4 * r;
+        if ((keep >> m) & 1u) st2(Y, (f0 + m) * ys + i, v);
     }
     __device__ void row4(int i, double2 v) const
     {
-        const int64_t fr = f0 + (threadIdx.x & 15);
-        if (fr < n && !(skip && skip[fr])) st2(Y, fr * ys + i, v);
+        const int m = threadIdx.x & 15;
+        if ((keep >> m) & 1u) st2(Y, (f0 + m) * ys + i, v);
     }
 };
 
@@ -3417,7 +3425,8 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void apply_kernel(const doubl
     int64_t g = (int64_t)blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6);
     if (g >= ng) return;
     double2 wn[KSTEPS];
-    apply_load(X, xs, n, g, ml, kl, wn, tile_done(skip, 16 * g, n, lane));
+    uint32_t kn = tile_keep(skip, 16 * g, n, lane);
+    apply_load(X, xs, n, g, ml, kl, wn, kn == 0);
     for (; g < ng; g += stride) {
         double ar[KSTEPS], ai[KSTEPS];
 #pragma unroll
@@ -3425,11 +3434,13 @@ __global__ __launch_bounds__(256, APPLY_WG_PER_CU) void apply_kernel(const doubl
             ar[s] = wn[s].x;
             ai[s] = wn[s].y;
         }
-        if (g + stride < ng)   // next tile, under this one's MFMAs
-            apply_load(X, xs, n, g + stride, ml, kl, wn, tile_done(skip, 16 * (g + stride), n, lane));
-        const int64_t f0 = 16 * g;
-        if (tile_done(skip, f0, n, lane)) continue;
-        apply_tile3<true>(sc, scs, ar, ai, ml, kl, ApplyStore{Y, ys, f0, n, skip});
+        const uint32_t keep = kn;
+        if (g + stride < ng) {   // next tile, under this one's MFMAs
+            kn = tile_keep(skip, 16 * (g + stride), n, lane);
+            apply_load(X, xs, n, g + stride, ml, kl, wn, kn == 0);
+        }
+        if (keep == 0) continue;
+        apply_tile3<true>(sc, scs, ar, ai, ml, kl, ApplyStore{Y, ys, 16 * g, keep});
     }
 }
 
