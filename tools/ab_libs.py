@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
 ap.add_argument("--leg", choices=["config5", "headline", "dense", "apply", "r1dense", "lowrank", "cm", "cmq", "fcref", "c5ref_fc",
-                                 "refmm"],
+                                 "refmm", "fctb"],
                 default="config5")
 ap.add_argument("--taps", type=int, default=8, help="lowrank: L-tap PDP covariance (rank L; 53 = decay 0.5)")
 ap.add_argument("--rounds", type=int, default=5)
@@ -66,10 +66,10 @@ for d in args.dirs:
         f = (lambda c, fr, o, st, m: lambda: c.estimate(fr, o, m.ALL, st.handle))(ctx, fr, o, st, m)
         keep += outs + [eq]
         check = outs[4]
-    elif args.leg in ("fcref", "c5ref_fc"):   # REF + FRAME_COV: PS_MMSE alone / all 5 + eq (fp64)
+    elif args.leg in ("fcref", "c5ref_fc", "fctb"):   # REF / TEXTBOOK (fctb) + FRAME_COV: PS_MMSE alone / all 5 + eq (fp64)
         ctx.reserve(n)
         fr = ctx.frames(tx, rx, n, rx_pre=pre)
-        if args.leg == "fcref":
+        if args.leg in ("fcref", "fctb"):
             H = m.DeviceArray((n, N))
             o = m.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
             mk = m.PS_MMSE | m.FRAME_COV
