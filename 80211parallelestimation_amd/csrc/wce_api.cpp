@@ -550,6 +550,17 @@ static int prep_frame_cov(wce_ctx *c, const wce_frames *in, const wce_outputs *o
     }
     if (!ws) return fail(WCE_EINVAL, "frame covariance workspace missing");
     double *hw = ws, *uw = hw + n * WS_LD * 2, *ww = uw + n * WS_LD * 2;
+    if (c->mode == WCE_MMSE_TEXTBOOK && in->semantics == WCE_SEM_C && !lt_ready &&
+        wce::variant_value(wce::WCE_VARIANT_REF_FC) == 0) {   // LT_LS and u = Mu h in one launch
+        rc = wce::launch_fc_u(st, reinterpret_cast<const double *>(in->rx_pre), in->pre_stride,
+                              reinterpret_cast<const double *>(in->tx_pre), uw, WS_LD, n, stream);
+        if (rc) return fail(rc, "fc_u launch (frame covariance)");
+        sa.cu = uw;
+        sa.cw = nullptr;
+        sa.cs = WS_LD;
+        sa.hout = 1;
+        return WCE_OK;
+    }
     const double *h = hw;
     int64_t hs = WS_LD;
     if (lt_ready) {

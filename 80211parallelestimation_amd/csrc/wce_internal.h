@@ -227,6 +227,9 @@ const char *lr_kernel_name(int k0, int rank, int taps, int64_t units);
 // pilots from State::Wp, s, u = Mu h and H = u s to a.w
 int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
                   void *stream);
+// TEXTBOOK per-frame covariance, C semantics: LT_LS of each preamble and u = Mu h in one launch (u rows at U, stride us)
+int launch_fc_u(const State *st, const double *rx_pre, int64_t ps, const double *tx_pre, double *U, int64_t us,
+                int64_t n, void *stream);
 // the same w as full rows W[f] (zero off the pilots) from h rows X[f] (the variant path)
 int launch_ref_w(const State *st, const double *X, int64_t xs, double *W, int64_t ws, int64_t n, void *stream);
 // H[f] = mean of X rows 4f .. 4f+3 (MATLAB block average, left to right)
@@ -247,9 +250,10 @@ constexpr int WCE_VARIANT_LR = 3;     // WCE_MMSE_COV low-rank path: 0 = ranks 1
                                       // to rounding (~1e-15), not bitwise; the staged builds bitwise.
                                       // A diagonal Rhh runs the wave kernel's tap-domain Gram
                                       // (mmse_lr_kernel<K0, true>); 5 = the product Gram there instead
-constexpr int WCE_VARIANT_REF_FC = 4;  // REF + WCE_MMSE_FRAME_COV, C semantics: 0 = ref_fc_kernel (LT_LS, the
-                                      // g / u / w products and the read-out in one launch, default), 1 = the
-                                      // LT_LS pass + two matvec launches + the REF read-out; bit-identical
+constexpr int WCE_VARIANT_REF_FC = 4;  // WCE_MMSE_FRAME_COV, C semantics: 0 = ref_fc_kernel (REF: LT_LS, the
+                                      // u / w products and the read-out in one launch; TEXTBOOK: LT_LS and
+                                      // u = Mu h in one launch; default), 1 = the LT_LS pass + the matvec
+                                      // launches (+ the REF read-out); bit-identical
 constexpr int WCE_VARIANT_COUNT = 5;
 int variant_value(int which);
 int set_variant(int which, int value);

@@ -3546,7 +3546,11 @@ struct RefFcStore {
 
 // Persistent: each wave walks 16-frame tiles g, g + stride, ... with the next
 // tile's preamble in flight under this tile's work; Mu and Wp staged once per
-// workgroup.
+// workgroup.  UOUT (TEXTBOOK per-frame covariance, C semantics): the same
+// LT_LS and u = Mu h (Mu = F conj(F) / 53 there), u stored to a.w (row stride
+// a.ws) for the solve, no w / s / read-out -- one launch where the general
+// path runs the LT_LS pass and matvec_kernel (bit-identical to them).
+template <bool UOUT>
 __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *__restrict__ st, SolveArgs a,
                                                                    const double *__restrict__ rx_pre, int64_t ps,
                                                                    const double *__restrict__ tx_pre)
@@ -3587,6 +3591,11 @@ __global__ __launch_bounds__(256, FC_WG_PER_CU) void ref_fc_kernel(const State *
         const bool live = fa < a.n;
         double ar[KSTEPS], ai[KSTEPS];
         ref_h(rpn, txp, kl, live, ar, ai);
+        if constexpr (UOUT) {
+            if (g + stride < ng) load(g + stride);   // next tile, under this one's MFMAs
+            apply_tile3<false>(sh.sc, nullptr, ar, ai, ml, kl, ApplyStore{a.w, a.ws, f0, tile_keep(nullptr, f0, a.n, lane)});
+            continue;
+        }
         double w[4];
         ref_w4(sh.wp, ar, ai, kl, w);
         const double2 sfr = ref_s(w, a, fa, rb);
@@ -3767,8 +3776,23 @@ int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int
     if (a.n <= 0) return WCE_OK;
     if (a.split || !rx_pre || !a.w) return WCE_EINVAL;
     const int64_t blocks = tile_blocks((a.n + 15) / 16, APPLY_WAVES * FC_WG_PER_CU);
-    hipLaunchKernelGGL(ref_fc_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, rx_pre, ps,
-                       tx_pre);
+    hipLaunchKernelGGL(ref_fc_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, rx_pre,
+                       ps, tx_pre);
+    return hip_status(hipGetLastError());
+}
+
+int launch_fc_u(const State *st, const double *rx_pre, int64_t ps, const double *tx_pre, double *U, int64_t us,
+                int64_t n, void *stream)
+{
+    if (n <= 0) return WCE_OK;
+    if (!rx_pre || !U) return WCE_EINVAL;
+    SolveArgs a{};
+    a.n = n;
+    a.w = U;
+    a.ws = us;
+    const int64_t blocks = tile_blocks((n + 15) / 16, APPLY_WAVES * FC_WG_PER_CU);
+    hipLaunchKernelGGL(ref_fc_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, st, a, rx_pre,
+                       ps, tx_pre);
     return hip_status(hipGetLastError());
 }
 

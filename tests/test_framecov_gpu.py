@@ -200,3 +200,43 @@ def test_ref_fc_kernel_small_ragged_batches(gpu_wce, golden, oracle, B):
     for f in range(B):
         exp = oracle.mmse_ref_repaired(t[f, 0], x[f, 0], F, inp["ow2"], oracle.lt_ls(inp["tx_pre"], p[f]), invF)
         assert normrel(got[0][f], exp) < TOL, f
+
+
+@pytest.mark.parametrize("B,mask_name", [(1037, "MMSE"), (1037, "MMSE_LIN_EQ"), (1, "MMSE"), (17, "MMSE"), (33, "MMSE_LIN_EQ")])
+def test_textbook_fused_factor_kernel_equals_general_path(gpu_wce, golden, oracle, B, mask_name):
+    """TEXTBOOK + FRAME_COV in C semantics without an LT_LS output: LT_LS of
+    each preamble and u = Mu h (Mu = F conj(F) / 53) in one launch
+    (ref_fc_kernel<UOUT>, round 5) where the general path (variant
+    WCE_VARIANT_REF_FC = 1) runs the LT_LS pass and matvec_kernel.  Same
+    arithmetic, so H and every output are bit-identical: ragged batches (1,
+    17, 33, 1,037 frames), block 2, a caller tx_pre, a non-dense output
+    stride; sampled frames against the long double solve with the frame's
+    own C_f (WiFi_channel_estimation_PS_MMSE.m:26-33 on its own H_LT)."""
+    wce = gpu_wce
+    lib = wce.load()
+    inp = golden["inputs"]
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_TEXTBOOK)
+    tx, rx, pre = wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, NBLK, N)), wce.DeviceArray((B, N))
+    ctx.synth(tx, rx, pre, B, seed=0x7B + B)
+    wce.synchronize()
+    t, x, p = tx.numpy(), rx.numpy(), pre.numpy()
+    tpre = inp["tx_pre"] * (1.0 + 0.0j)
+    mask = {"MMSE": wce.PS_MMSE, "MMSE_LIN_EQ": wce.PS_MMSE | wce.PS_LINEAR | wce.EQUALIZE}[mask_name] | wce.FRAME_COV
+    got = {}
+    try:
+        for v in (0, 1):
+            assert lib.wce_debug_set_variant(4, v) == 0
+            got[v] = ctx.estimate_host(t, x, rx_pre=p, mask=mask, block=2, tx_pre=tpre)
+    finally:
+        assert lib.wce_debug_set_variant(4, 0) == 0
+    for k in got[0]:
+        assert np.array_equal(got[0][k], got[1][k]), k
+    H = got[0]["ps_mmse"]
+    assert np.isfinite(H).all()
+    F = oracle.fmatrix()
+    ones = np.ones(N, np.uint8)
+    for f in sorted({0, B // 2, B - 1}):
+        hls = oracle.lt_ls(tpre, p[f])
+        C = oracle.mmse_textbook_cmatrix(F, hls)
+        exp = oracle.mmse_unified(C, ones, 1, inp["ow2"], t[f, 2], x[f, 2])
+        assert normrel(H[f], exp) < TOL, f
