@@ -1303,8 +1303,10 @@ def ctx_scan(c, H, n, s):
 
 def bench_frame_cov(wce, make_ctx, stream, n, reps):
     """PS_MMSE with each frame's own preamble covariance (WCE_MMSE_FRAME_COV,
-    SURVEY 8(f)-4): LT_LS per frame, two (REF: three) batched MFMA matvecs for
-    the rank-1 factors of C_f, then the dense per-frame solve."""
+    SURVEY 8(f)-4), C semantics.  TEXTBOOK: LT_LS per frame and the rank-1
+    factor u = Mu h on f64 MFMA in one launch (ref_fc_kernel<UOUT>), then the
+    dense per-frame solve; REF: LT_LS, the factors and the read-out in one
+    launch (ref_fc_kernel)."""
     s = stream.handle
     out = {"workload": f"{n} frames, per-frame preamble, PS_MMSE | FRAME_COV"}
     for label, m in (("textbook", wce.MMSE_TEXTBOOK), ("ref", wce.MMSE_REF)):
@@ -1320,6 +1322,8 @@ def bench_frame_cov(wce, make_ctx, stream, n, reps):
             f()
         t = time_events(wce, stream, f, reps)
         out[label] = {"ms_per_step": t, "frames_per_s": n / (t * 1e-3), "nonfinite_frames": ctx_scan(c, H, n, s)}
+        if m == wce.MMSE_TEXTBOOK:
+            out[label]["kernels"] = "ref_fc_kernel<UOUT> (LT_LS, u = Mu h) + mmse_solve_fc_kernel"
         if m == wce.MMSE_REF:
             # one launch (ref_fc_kernel): rx_pre 848 + 8 pilots 128 in, H 848 out
             alg = (N * 16 + 8 * 16 + N * 16) * n
