@@ -13,8 +13,8 @@ legs (bench.py field -> kernel, frames per launch):
   front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
   config5    config5_sharded     mmse_solve_ls_kernel<true,true,true>  1,048,576 (all 5 + eq, fp32 LS)
   config5_ref(_f32) config5_ref   ref_ls_elem_kernel<true>      1,048,576 (REF + LS family + eq, fp64 / fp32 LS)
-  config5_ref_fc(_factors)       ref_ls_elem_kernel<true> / ref_fc_kernel  1,048,576 (the same | FRAME_COV)
-  frame_cov_ref frame_cov.ref    ref_fc_kernel                    65,536 (REF PS_MMSE | FRAME_COV: one launch)
+  config5_ref_fc(_factors)       ref_ls_elem_kernel<true> / ref_fc_kernel<false>  1,048,576 (the same | FRAME_COV)
+  frame_cov_ref frame_cov.ref    ref_fc_kernel<false>             65,536 (REF PS_MMSE | FRAME_COV: one launch)
   lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_staged_kernel<L, 1, true> (L <= 8) / mmse_lr_quad_kernel<L, true> (L <= 16) /
                                  mmse_lr_kernel<K0, true> (tap-domain Gram)  65,536 (COV, L-tap PDP: rank L)
   lowrank8_1m cov_lowrank.L8.frames_1048576  mmse_lr_lane_staged_kernel<8, 2, true>  1,048,576 (block 0 only)
@@ -44,8 +44,8 @@ LEGS = {
     "config5_ref": ("ref_ls_elem_kernel<true>", 1 << 20),
     "config5_ref_f32": ("ref_ls_elem_kernel<true>", 1 << 20),
     "config5_ref_fc": ("ref_ls_elem_kernel<true>", 1 << 20),          # REF + FRAME_COV, all 5 + eq (round 4) ...
-    "config5_ref_fc_factors": ("ref_fc_kernel", 1 << 20),     # ... and its PS_MMSE kernel (same workload, round 5)
-    "frame_cov_ref": ("ref_fc_kernel", 65536),        # REF + FRAME_COV, PS_MMSE only: the whole step
+    "config5_ref_fc_factors": ("ref_fc_kernel<false>", 1 << 20),     # ... and its PS_MMSE kernel (same workload, round 5)
+    "frame_cov_ref": ("ref_fc_kernel<false>", 65536),        # REF + FRAME_COV, PS_MMSE only: the whole step
     "lowrank4": ("mmse_lr_lane_staged_kernel<4, 1, true>", 65536),     # Toeplitz Gram (taps 0..3, round 4)
     "lowrank8": ("mmse_lr_lane_staged_kernel<8, 1, true>", 65536),
     "lowrank16": ("mmse_lr_quad_kernel<16, true>", 65536),
