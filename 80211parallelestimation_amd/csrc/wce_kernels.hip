@@ -1588,15 +1588,14 @@ __device__ __forceinline__ int taps_tap(const L &s, const int *tapl, int j)
 }
 template <int K0, typename L = SolveLds>
 __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s, double2 (&A)[RB][RB],
-                                             int lane, int p, int q, double ac, double bc, double sl)
+                                             int lane, int p, int q, double ac, double bc, double sl, int tpi)
 {
     constexpr int RMAX = NSC - 8 * K0;   // Gram column of the border (row 53)
     constexpr int NB = RB - K0;
     const bool act = lane < NSC;
     {   // tables: E, p = |x|^2, v = x o conj(rx)
         const double2 xl = s.x[lane], rl = s.rx[lane];
-        if constexpr (!L::TAP_MAPS) s.u[0][lane] = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
-        s.u[1][lane] = cmul(xl, cconj(rl));
+        s.u[1][lane] = cmul(xl, cconj(rl));   // (E is in u[0] since the frame's staging)
         s.rd[lane] = fma(xl.x, xl.x, xl.y * xl.y);
     }
     wave_lds_sync();
@@ -1669,13 +1668,8 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
     int *tapl = reinterpret_cast<int *>(s.u[1]);   // column j -> its tap (256 B of u[1]) ...
     double *bl = reinterpret_cast<double *>(tapl + 64);   // ... and M's diagonal term b / lambda_j (b past r)
     const int r = st->cov_rank;
-    if constexpr (L::TAP_MAPS) {
-        bl[lane] = lane < r ? bc / (sl * sl) : bc;
-    } else {
-        tapl[lane] = st->tap_of[lane];
-        const double sg = st->col_s[lane];
-        bl[lane] = lane < r ? bc / (sg * sg) : bc;
-    }
+    if constexpr (!L::TAP_MAPS) tapl[lane] = tpi;
+    bl[lane] = lane < r ? bc / (sl * sl) : bc;
     wave_lds_sync();
 #pragma unroll
     for (int m = 0; m < NB; ++m) {
@@ -1719,18 +1713,20 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     const int p = lane >> 3, q = lane & 7;
     const bool act = lane < NSC;
     const double ac = st->acoef, bc = st->bcoef;
-    double sl = 0.0;
-    {
+    double sl;
+    int tpi;
+    {   // E, the column -> tap map and s_j in the frame's round trip (E to u[0] now; the map to
+        // LDS at the tap stage, or at once with TAP_MAPS, which also keeps tap -> column)
         const double2 t = act ? ld2(a.tx, base + lane) : make_double2(0, 0);
         const double2 r = act ? ld2(a.rx, base + lane) : make_double2(0, 0);
         const bool inx = act && ((st->xmask >> lane) & 1ull);
-        if constexpr (L::TAP_MAPS) {   // E and the tap maps in the frame's round trip
-            const double2 e = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
-            const int tp = st->tap_of[lane], cl = st->col_of[lane];
-            sl = st->col_s[lane];
-            s.u[0][lane] = e;
-            s.tap[lane] = (uint8_t)tp;
-            s.col[lane] = (uint8_t)cl;
+        const double2 e = act ? ld2(st->dft, lane) : make_double2(0.0, 0.0);
+        tpi = st->tap_of[lane];
+        sl = st->col_s[lane];
+        s.u[0][lane] = e;
+        if constexpr (L::TAP_MAPS) {
+            s.tap[lane] = (uint8_t)tpi;
+            s.col[lane] = (uint8_t)st->col_of[lane];
         }
         s.x[lane] = inx ? t : make_double2(0, 0);
         s.rx[lane] = r;
@@ -1741,7 +1737,7 @@ __device__ __forceinline__ double2 lr_solve_taps(const State *__restrict__ st, c
     for (int aa = 0; aa < RB; ++aa)
 #pragma unroll
         for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = make_double2(0.0, 0.0);
-    lr_gram_taps<K0>(st, s, A, lane, p, q, ac, bc, sl);
+    lr_gram_taps<K0>(st, s, A, lane, p, q, ac, bc, sl, tpi);
     dense_chol<K0>(A, s, p, q, lane);
     double rq[RB];
 #pragma unroll
