@@ -1210,10 +1210,22 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
     const double ac = st->acoef, bc = st->bcoef;
     double2 A[RB][RB];
     const bool cbuild = !FC && ac != 0.0;
+    if constexpr (!DOT && !FC) {   // dense C: its 28 block loads in the frame's round trip
+        if (cbuild) {             // (M = C + diag(b / (a |x|^2)); C zero-padded: no bounds checks)
+#pragma unroll
+            for (int aa = 0; aa < RB; ++aa)
+#pragma unroll
+                for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
+        }
+    }
     {
         const bool act = lane < NSC;
-        const double2 t = !act ? make_double2(0, 0) : ld2(a.tx, base + lane);
-        const double2 r = !act ? make_double2(0, 0) : ld2(a.rx, base + lane);
+        // branch-free: both loads issued together (and with C's: one memory round trip
+        // where the dense path waited three, 655.7 -> 644.7 us, profiles/r05_ab_dense_early.txt)
+        const int lc = act ? lane : NSC - 1;
+        const double2 t0 = ld2(a.tx, base + lc), r0 = ld2(a.rx, base + lc);
+        const double2 t = act ? t0 : make_double2(0, 0);
+        const double2 r = act ? r0 : make_double2(0, 0);
         const bool inx = act && ((st->xmask >> lane) & 1ull);
         s.x[lane] = inx ? t : make_double2(0, 0);
         s.rx[lane] = r;
@@ -1255,11 +1267,7 @@ __device__ __forceinline__ double2 solve_block(const State *__restrict__ st, con
 #pragma unroll
                 for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = cmul(s.u[0][p + 8 * aa], s.u[1][q + 8 * bb]);
             wave_lds_sync();   // the factorisation reuses s.u[0]
-        } else if (cbuild) {   // M = C + diag(b / (a |x|^2))  (C zero-padded: no bounds checks)
-#pragma unroll
-            for (int aa = 0; aa < RB; ++aa)
-#pragma unroll
-                for (int bb = 0; bb <= aa; ++bb) A[aa][bb] = ld2(st->C, (p + 8 * aa) * CLD + q + 8 * bb);
+        } else if (cbuild) {   // M = C + diag(b / (a |x|^2)): C loaded with the frame (above)
         } else {
 #pragma unroll
             for (int aa = 0; aa < RB; ++aa)
