@@ -108,6 +108,7 @@ ABI = {
     "wce_ctx_set_modulus": [c_void_p, c_void_p],
     "wce_state_set_modulus": [c_void_p, c_size_t, c_void_p, c_void_p],
     "wce_debug_set_cm": [c_void_p, c_int],
+    "wce_debug_compat_state_builds": [],
     "wce_ctx_state": [c_void_p, POINTER(c_void_p), POINTER(c_size_t)],
     "wce_ctx_mark_ready": [c_void_p],
     "wce_state_size": [],
@@ -185,6 +186,8 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
         fn.restype = None if name in _VOID else (ctypes.c_char_p if name in _STR else c_int)
     lib.wce_state_size.restype = c_size_t
+    if hasattr(lib, "wce_debug_compat_state_builds"):
+        lib.wce_debug_compat_state_builds.restype = ctypes.c_ulonglong
     _lib = lib
     return lib
 

@@ -68,7 +68,108 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
     ap.add_argument("--extras-out", default=os.path.join("gpurun_out", "bench_extras.json"),
                     help="full per-leg JSON (the stdout line carries one-number summaries)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control path only: start the ranks, form the process group, barrier, max over ranks, "
+                         "print the line; no device is touched (with WCE_DIST_BACKEND=gloo)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the N
+    ranks here, one process per GPU, as the reference's mpirun does for
+    main_mpi.c (MPI_Init / MPI_Comm_size / MPI_Comm_rank, main_mpi.c:16-27,
+    687-688), through torch.distributed.run on 127.0.0.1.  This parent never
+    touches the GPU (no torch import, no HIP call), so no process that has
+    initialised a device is replaced or forked.  The children's stdout is
+    relayed line by line to stderr as it arrives (progress stays visible);
+    rank 0's final JSON line is checked -- n_gpus and the process group both
+    span N ranks -- and printed last on stdout.  Exit status: the launcher's
+    when any rank failed, 3 when the line is missing or does not span N."""
+    import subprocess
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print("bench: launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    last = None
+    for ln in p.stdout:
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            last = s
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc != 0:
+        print(f"bench: a rank failed (launcher exit {rc})", file=sys.stderr, flush=True)
+        return rc
+    try:
+        res = json.loads(last) if last else None
+    except ValueError:
+        res = None
+    if res is None:
+        print("bench: no result line from rank 0", file=sys.stderr, flush=True)
+        return 3
+    dc = res.get("dist_check") or {}
+    if res.get("n_gpus") != n or dc.get("group_size") != n or not dc.get("all_ranks_agree"):
+        print(f"bench: line does not span {n} ranks: n_gpus={res.get('n_gpus')} dist_check={dc}",
+              file=sys.stderr, flush=True)
+        return 3
+    print(last, flush=True)
+    return 0
+
+
+def check_world(gpus: int):
+    """None when this process should run the bench itself, else the exit
+    status: with a launcher (WORLD_SIZE set) the world must be --gpus ranks;
+    without one, --gpus N > 1 starts the N ranks (launch_ranks)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench: WORLD_SIZE={ws} but --gpus {gpus}; refusing to report a {ws}-rank run as {gpus}",
+                  file=sys.stderr, flush=True)
+            return 2
+        return None
+    if gpus < 1:
+        print(f"bench: --gpus {gpus}", file=sys.stderr, flush=True)
+        return 2
+    if gpus > 1:
+        return launch_ranks(gpus, sys.argv[1:])
+    return None
+
+
+def dry_run(args, dist):
+    """--dry-run: the N-rank control path without a device -- the process
+    group, the barriers and the max over ranks every timed leg uses -- and a
+    contract-shaped line (value null) from rank 0.  WCE_DRY_FAIL_RANK=r makes
+    rank r exit 1 after the group forms (the launcher's failure path)."""
+    dist.barrier()
+    if os.environ.get("WCE_DRY_FAIL_RANK") == str(dist.rank):
+        print(f"bench: dry run: rank {dist.rank} failing on request", file=sys.stderr, flush=True)
+        sys.exit(1)
+    t0 = time.perf_counter()
+    dist.barrier()
+    el = dist.max(time.perf_counter() - t0)
+    res = {"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": dist.world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f64", "data": "dry-run (no device)", "dry_run": True,
+           "barrier_ms_max": el * 1e3,
+           "config": {"workload": "dry run", "frames_per_gpu": args.frames_per_gpu,
+                      "global_frames": args.frames_per_gpu * dist.world,
+                      "parallelism": f"dp{dist.world} (frames sharded, 1 RCCL state broadcast)"},
+           "dist_check": dist.group_check()}
+    if dist.rank == 0:
+        print(json.dumps(res, separators=(",", ":")), flush=True)
+    dist.close()
 
 
 class Dist:
@@ -264,7 +365,12 @@ def time_events(wce, stream, fn, reps):
 
 def main():
     args = parse()
+    rc = check_world(args.gpus)
+    if rc is not None:
+        sys.exit(rc)
     dist = Dist()
+    if args.dry_run:
+        return dry_run(args, dist)
     import importlib
     wce = importlib.import_module("80211parallelestimation_amd")
     dev = dist.device if dist.world > 1 else 0

@@ -61,6 +61,10 @@ int wce_debug_set_cov_path(struct wce_ctx *ctx, int path);
 const char *wce_debug_lr_kernel(struct wce_ctx *ctx, long long units);
 /* A/B switch of the constant-modulus path (wce_ctx_set_modulus); on by default. */
 int wce_debug_set_cm(struct wce_ctx *ctx, int on);
+/* How many times the compat WiFi_channel_estimation_PS_MMSE built and
+ * uploaded its shared state (main.c:148's F / H_EST_LS / ow2): once per
+ * distinct (F, H_EST_LS, ow2), not once per call.  0 before the first call. */
+unsigned long long wce_debug_compat_state_builds(void);
 #ifdef __cplusplus
 }
 #endif

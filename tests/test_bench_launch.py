@@ -1,0 +1,73 @@
+"""bench.py --gpus N without a launcher starts N ranks itself (CPU: gloo, the
+--dry-run control path that never touches a device).  The driver's N-GPU
+command may or may not wrap bench.py in torch.distributed.run; either way the
+line must span N ranks or the run must fail (main_mpi.c:16-27, 687-688: the
+reference's mpirun world is what its timing covers)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240, **env):
+    e = dict(os.environ, WCE_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=REPO)
+
+
+def _line(p):
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    assert p.stdout.rstrip().endswith(lines[0])        # the line is the last thing on stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_spawns_n_ranks(n):
+    p = _run(["--gpus", str(n), "--dry-run", "--steps", "7", "--warmup", "2"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = _line(p)
+    assert r["n_gpus"] == n and r["dry_run"] is True
+    assert r["dist_check"] == {"backend": "gloo", "world_size_env": n, "group_size": n, "all_ranks_agree": True}
+    assert r["steps"] == 7 and r["warmup"] == 2
+    assert r["config"]["global_frames"] == n * r["config"]["frames_per_gpu"]
+    assert "launching %d ranks" % n in p.stderr
+
+
+def test_rank_failure_fails_the_run():
+    p = _run(["--gpus", "2", "--dry-run"], WCE_DRY_FAIL_RANK="1")
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_world_size_must_equal_gpus():
+    p = _run(["--gpus", "1", "--dry-run"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert p.returncode == 2 and "WORLD_SIZE=2 but --gpus 1" in p.stderr
+    p = _run(["--gpus", "8", "--dry-run"], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    assert p.returncode == 2
+
+
+def test_single_rank_dry_run_needs_no_launcher():
+    p = _run(["--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = _line(p)
+    assert r["n_gpus"] == 1 and r["dist_check"]["group_size"] == 1
+    assert "launching" not in p.stderr
+
+
+def test_launcher_parent_never_imports_torch():
+    """The parent must not initialise a GPU before its children start (an exec
+    or fork after HIP init is forbidden on the pool): check_world runs before
+    anything imports torch."""
+    src = open(os.path.join(REPO, "bench.py")).read()
+    main = src[src.index("def main():"):]
+    assert main.index("check_world(") < main.index("Dist()")
+    head = src[:src.index("def main():")]
+    assert "\nimport torch" not in head and "\nfrom torch" not in head

@@ -1,6 +1,8 @@
 """The CPU oracle pinned against the reference's own outputs (golden vectors
 produced by the compiled reference, tests/golden/make_golden.py) and against
 the MATLAB workspace matlab.mat.  No GPU needed."""
+import os
+
 import numpy as np
 import pytest
 
@@ -216,3 +218,35 @@ def test_mmse_formula_pins_vs_oracle(oracle, golden):
             for pin, want in checks:
                 worst = max(worst, float(normrel(from_split(pin), want)))
     assert worst < 5e-12, worst   # measured 2.0e-12 (rank 6 at ow2 = 1e-5: the cofactor inverse's own error)
+
+
+def test_textbook_closed_form_vs_mp_literal(oracle, golden):
+    """The oracle's long double closed form of the headline (TEXTBOOK) mode
+    against WiFi_channel_estimation_PS_MMSE.m:26-32 evaluated literally in
+    mpmath at 50 digits (tests/golden/make_textbook_mp.py) at the operating
+    ow2 = 9.6172e-8.  Measured max 2.9e-13 over the 13 frames: the closed
+    form's cancellation (uH rx - (uH v)(vH rx)/(s + vH v)) costs cond(Ryy) ~ 4e6
+    times long double's 1.1e-19, i.e. ~4e-13 is its floor -- the same with an
+    exact c, so it is not F's or H_LT's rounding; hence 1e-12 here."""
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "textbook_mp_pins.npz"))
+    inp = golden["inputs"]
+    assert float(d["ow2"]) == float(inp["ow2"])
+    F = oracle.fmatrix()
+    c = F @ (F.conj() @ oracle.lt_ls(inp["tx_pre"], inp["rx_pre"]) / N)
+    errs = [oracle.normrel(oracle.mmse_textbook_closed(c, d["tx"][i], d["rx"][i], d["ow2"]),
+                           d["H_hi"][i].astype(np.clongdouble) + d["H_lo"][i]) for i in range(len(d["tx"]))]
+    assert len(errs) == 13 and max(errs) < 1e-12, errs
+
+
+def test_textbook_mp_fixture_inputs_regenerate():
+    """The fixture's bench frames are the Python restatement of synth_kernel
+    (make_textbook_mp.synth_block0) of the bench's seed and H_LT: rerunning it
+    gives the stored inputs bit for bit (the GPU test ties them to the
+    device's own frames)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_textbook_mp as m
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "textbook_mp_pins.npz"))
+    for i in np.nonzero(d["kind"] == "bench")[0]:
+        t, r = m.synth_block0(int(d["bench_frame"][i]), d["h_shared"], float(d["ow2"]))
+        assert np.array_equal(t, d["tx"][i]) and np.array_equal(r, d["rx"][i])
