@@ -236,7 +236,10 @@ int launch_ref_w(const State *st, const double *X, int64_t xs, double *W, int64_
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
 // kernel variants for A/B timing (wce_debug_set_variant)
-constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = 512-element chunks (grid capped, default), 2 = uncapped grid
+constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = one element per thread, nontemporal stores
+                                      // (mmse_ref_elem_kernel, default), 3 = the same with plain stores,
+                                      // 1 = 512-element chunks on a capped grid (mmse_ref_flat_kernel, round 5),
+                                      // 2 = the chunks on an uncapped grid; bit-identical
 constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 2 = one element per thread (ls_elem_kernel, default),
                                       // 3 = the per-frame LIGHT ls_kernel
 constexpr int WCE_VARIANT_REF_LS = 2;  // REF PS_MMSE + LS family (+ eq), C semantics: 0 = ref_ls_elem_kernel

@@ -95,7 +95,7 @@ def launch_ranks(n: int, argv) -> int:
     import subprocess
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
-    env = dict(os.environ)
+    env = dict(os.environ, WCE_BENCH_LAUNCHER="bench.py --gpus %d" % n)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
     print("bench: launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
@@ -162,6 +162,7 @@ def dry_run(args, dist):
     res = {"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": dist.world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f64", "data": "dry-run (no device)", "dry_run": True,
+           "launcher": os.environ.get("WCE_BENCH_LAUNCHER", "external" if "WORLD_SIZE" in os.environ else None),
            "barrier_ms_max": el * 1e3,
            "config": {"workload": "dry run", "frames_per_gpu": args.frames_per_gpu,
                       "global_frames": args.frames_per_gpu * dist.world,
@@ -436,6 +437,7 @@ def main():
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "prewarm_s": args.prewarm_s, "nonfinite_frames": nonfinite,
+           "launcher": os.environ.get("WCE_BENCH_LAUNCHER", "external" if "WORLD_SIZE" in os.environ else None),
            # where this rank's timed region went: host enqueue of the K steps,
            # the wait for the stream, the closing barrier (rank 0's view)
            "timed_region_ms": {"enqueue": (t_enq - t0) * 1e3, "stream_sync": (t_done - t_enq) * 1e3,
@@ -672,7 +674,8 @@ def compact(res, extras_path):
     the extras file written beside it.  Must stay under COMPACT_LIMIT bytes
     (the driver keeps the last 8 KB of stdout; tests/test_bench_contract.py)."""
     out = _pick(res, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-                      "scaling", "vs_baseline", "dtype", "data", "prewarm_s", "nonfinite_frames", "timed_region_ms"))
+                      "scaling", "vs_baseline", "dtype", "data", "prewarm_s", "nonfinite_frames", "timed_region_ms",
+                      "launcher"))
     cfg = res.get("config", {})
     out["config"] = {"workload": "PS_MMSE %s, BASELINE configs[2]" % ("textbook" if "textbook" in cfg.get("workload", "")
                                                                      else "ref"),

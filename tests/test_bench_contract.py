@@ -179,6 +179,20 @@ def test_multirank_rehearsal_self_explaining():
     assert abs(c4["frames_per_s_per_gpu"] * 2 - c4["frames_per_s"]) / c4["frames_per_s"] < 1e-9
 
 
+def test_launcherless_rehearsal_spans_two_ranks():
+    """Round 6: `python3 bench.py --gpus 2` with NO torch.distributed.run
+    (gloo, both ranks on the one GPU of a gpurun box) -- bench.py started the
+    two ranks itself (launch_ranks), and the line it relayed spans them."""
+    path = _latest("r*_bench_2rank_gloo_rehearsal.json")
+    if os.path.basename(path) < "r06":
+        pytest.skip("rehearsal predates the launcher (round < 6)")
+    reh = json.loads(open(path).read().strip().splitlines()[-1])
+    assert reh["launcher"] == "bench.py --gpus 2"
+    assert reh["n_gpus"] == 2 and reh["dist_check"]["group_size"] == 2 and reh["dist_check"]["all_ranks_agree"]
+    assert reh["config"]["global_frames"] == 2 * reh["config"]["frames_per_gpu"]
+    assert abs(reh["value"] - reh["config"]["global_frames"] / (reh["ms_per_step"] * 1e-3)) / reh["value"] < 1e-6
+
+
 def test_dist_check_in_headline_line(line):
     dc = line.get("dist_check")
     if dc is None:

@@ -39,6 +39,7 @@ def test_gpus_n_spawns_n_ranks(n):
     assert r["steps"] == 7 and r["warmup"] == 2
     assert r["config"]["global_frames"] == n * r["config"]["frames_per_gpu"]
     assert "launching %d ranks" % n in p.stderr
+    assert r["launcher"] == "bench.py --gpus %d" % n
 
 
 def test_rank_failure_fails_the_run():
@@ -59,7 +60,7 @@ def test_single_rank_dry_run_needs_no_launcher():
     assert p.returncode == 0, p.stderr[-2000:]
     r = _line(p)
     assert r["n_gpus"] == 1 and r["dist_check"]["group_size"] == 1
-    assert "launching" not in p.stderr
+    assert "launching" not in p.stderr and r["launcher"] is None
 
 
 def test_launcher_parent_never_imports_torch():

@@ -21,6 +21,7 @@ def lib(gpu_wce):
     yield lib
     assert lib.wce_debug_set_variant(0, 0) == 0
     assert lib.wce_debug_set_variant(1, 2) == 0
+    assert lib.wce_debug_set_variant(4, 0) == 0
     assert lib.wce_debug_set_flat_chunk(ctypes.c_longlong(0)) == 0
 
 
@@ -54,8 +55,11 @@ def test_ref_variants_identical(gpu_wce, golden, lib, frame_cov):
     ctx.synth(tx, rx, pre, B, seed=0x2B)
     ctx.reserve(B)
     mask = gpu_wce.PS_MMSE | (gpu_wce.FRAME_COV if frame_cov else 0)
+    # per-frame factors reach the REF read-out through the four-launch
+    # FRAME_COV path (which 4 = 1); the default fuses it into ref_fc_kernel
+    assert lib.wce_debug_set_variant(4, 1 if frame_cov else 0) == 0
     got = []
-    for v in (0, 2):
+    for v in (0, 1, 2, 3, 4, 5):
         assert lib.wce_debug_set_variant(0, v) == 0
         H = gpu_wce.DeviceArray((B, N), zero=True)
         ctx.estimate(ctx.frames(tx, rx, B, rx_pre=pre if frame_cov else None),
@@ -63,7 +67,8 @@ def test_ref_variants_identical(gpu_wce, golden, lib, frame_cov):
         gpu_wce.synchronize()
         got.append(H.numpy())
     assert np.isfinite(got[0]).all()
-    assert np.array_equal(got[1], got[0])
+    for g in got[1:]:
+        assert np.array_equal(g, got[0])
 
 
 def test_ref_frame_cov_ls_variant_full_w_rows(gpu_wce, golden, lib):

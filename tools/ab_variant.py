@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--floor", action="store_true",
+                    help="ref: also time PS_Linear alone on the same frames (ls_elem_kernel: the same 8 pilot "
+                         "sectors in and 848 B out per frame, i.e. the REF read-out's traffic shape)")
     args = ap.parse_args()
     wce = importlib.import_module("80211parallelestimation_amd")
     import bench
@@ -88,6 +91,17 @@ def main():
                               for a, b in zip(got, ref_out))
                     print(f"variant {v}: outputs bit-identical to variant {args.variants[0]}: {same} "
                           f"(max |diff| / max |ref| = {dif:.2e})")
+    if args.floor and args.leg == "ref":
+        hl = wce.DeviceArray((n, N), zero=True)
+        ol = wce.Outputs(None, hl.addr, None, None, None, None, N, 0, 0, 0, 0)
+        lin = lambda: ctx.estimate(fr, ol, wce.PS_LINEAR, s)
+        for _ in range(3):
+            lin()
+        tl = [bench.time_events(wce, stream, lin, args.reps) for _ in range(args.rounds)]
+        t = float(np.median(tl))
+        print(f"same traffic shape, PS_Linear alone (ls_elem_kernel): median {t * 1e3:.1f} us  "
+              f"{(bench.BYTES_PILOT_SECTORS + N * 16) * n / (t * 1e-3) / 1e12:.2f} TB/s on the sector floor "
+              f"({', '.join(f'{x * 1e3:.0f}' for x in tl)})")
     for v, ts in times.items():
         t = float(np.median(ts))
         print(f"{args.leg} variant {v}: median {t * 1e3:.1f} us  min {min(ts) * 1e3:.1f}  "
