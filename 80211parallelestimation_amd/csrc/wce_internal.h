@@ -14,11 +14,11 @@ constexpr int NPAD = 64;          // one wave64 lane per subcarrier
 constexpr int CLD = 64;           // leading dimension of the zero-padded C (64 x 64)
 constexpr int PILOT[4] = {WCE_P0, WCE_P1, WCE_P2, WCE_P3};
 constexpr int32_t STATE_MAGIC = 0x80211;
-constexpr int32_t STATE_LAYOUT = 8;   // State layout version: bump with every change to struct State
+constexpr int32_t STATE_LAYOUT = 9;   // State layout version: bump with every change to struct State
 constexpr int COV_K0_MAX = 6;    // WCE_MMSE_COV low-rank path: last block row a Gram system can start at
 
 // The frame-independent shared state: everything one rank broadcasts to the
-// others (one RCCL broadcast of sizeof(State) = wce_state_size() bytes, ~491 KB).
+// others (one RCCL broadcast of sizeof(State) = wce_state_size() bytes, 371,632 B).
 // Complex values are {re, im} fp64.
 constexpr int LRL_RMAX = 8;                          // ranks on the lane-per-frame low-rank kernel
 constexpr int LRL_NP = LRL_RMAX * (LRL_RMAX + 1) / 2;  // packed lower-triangle entries of its Gram matrix
@@ -26,18 +26,20 @@ struct State {
     double C[CLD * CLD * 2];   // MMSE covariance operator, row-major, zero-padded to 64 x 64
                                // (65,536 B): kernels index it without bounds checks
     // Per-frame covariance (WCE_MMSE_FRAME_COV): C_f = u_f w_f^T is rank 1 in
-    // both modes, with u_f, w_f batched matrix-vector products of the frame's
-    // own H_LT (padded 64 x 64, row-major, applied on MFMA):
-    //   REF      g = Mg h (invF_ref), u = Mu h (F invF_ref), w = Mw q(g),
-    //            q = re g - im g, Mw[j][c] = re F[j][c] - im F[j][c] (main.c:186-203)
-    //   TEXTBOOK u = Mu h (F conj(F) / 53, ifft then F), w = conj(u)
-    double Mg[CLD * CLD * 2];
+    // both modes, with u_f = Mu h the batched matrix-vector product of the
+    // frame's own H_LT (padded 64 x 64, row-major, applied on MFMA):
+    //   REF      Mu = F invF_ref (main.c:186-203); w_f is needed at the 4
+    //            pilots only and comes from the folded real map Wp below
+    //   TEXTBOOK Mu = F conj(F) / 53 (ifft then F), w = conj(u)
     double Mu[CLD * CLD * 2];
-    double Mw[CLD * CLD * 2];
     // REF: w at the 4 pilot rows folded into one real map of h (round 5):
-    // w_p = sum_k Ar[p][k] re h_k + Ai[p][k] im h_k with Ar = Mw_P (re Mg - im Mg),
-    // Ai = -Mw_P (re Mg + im Mg), products in 80 bits (Mw_P = rows P of Mw);
-    // stored {Ar, Ai} pairs, Wp[2 (p NPAD + k)], zero past k = 52.
+    // main.c forms g = invF_ref h, q = re g - im g and w = Mw q with
+    // Mw[j][c] = re F[j][c] - im F[j][c]; here
+    // w_p = sum_k Ar[p][k] re h_k + Ai[p][k] im h_k with Ar = Mw_P (re invF - im invF),
+    // Ai = -Mw_P (re invF + im invF), products in 80 bits (Mw_P = rows P of Mw),
+    // so the fold rounds once where main.c rounds per step: parity with main.c
+    // is held by tolerance (1e-15 of scale on w, 1e-10 on H), not bitwise.
+    // Stored {Ar, Ai} pairs, Wp[2 (p NPAD + k)], zero past k = 52.
     double Wp[4 * NPAD * 2];
     double cvec[NPAD * 2];     // rank-1 factors of the shared C = u w^T: u = cvec and
     double cwvec[NPAD * 2];    // w = conj(cvec) (TEXTBOOK: c = F ifft(H_LT)) or w = cwvec
@@ -175,7 +177,9 @@ struct SolveArgs {
                               // writes W_b to w[g*ws] (or, with hout, cw . W_b to dots[g])
     double *dots;
     int32_t ref_pilots;       // REF (main.c): a = 0 and X = the 4 pilots -> mmse_ref_flat_kernel
-    int32_t mmse_done;        // H already written (REF frame covariance): the fused launch runs the LS family only
+    int32_t mmse_done;        // H already written (REF frame covariance): the fused launch runs the LS family only.
+                              // Honoured ONLY by launch_mmse_solve_ls's REF element path (ref_ls_elem_kernel);
+                              // every other SolveArgs launcher returns WCE_EINVAL when it is set
     const uint8_t *skip;      // per unit: nonzero = H already written (constant-modulus path); null = none
 };
 struct SynthArgs {
@@ -236,10 +240,11 @@ int launch_ref_w(const State *st, const double *X, int64_t xs, double *W, int64_
 int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_t n, void *stream);
 int set_flat_chunk(int64_t frames);   // wce_debug_set_flat_chunk
 // kernel variants for A/B timing (wce_debug_set_variant)
-constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = one element per thread, nontemporal stores
-                                      // (mmse_ref_elem_kernel, default), 3 = the same with plain stores,
-                                      // 1 = 512-element chunks on a capped grid (mmse_ref_flat_kernel, round 5),
-                                      // 2 = the chunks on an uncapped grid; bit-identical
+constexpr int WCE_VARIANT_REF = 0;    // REF PS_MMSE: 0 = by batch size (default: one element per thread,
+                                      // mmse_ref_elem_kernel, past REF_ELEM_FROM frames, else 512-element
+                                      // chunks on a capped grid, mmse_ref_flat_kernel), 1 = always the capped
+                                      // chunks, 2 = the chunks on an uncapped grid, 3 = always one element per
+                                      // thread; bit-identical
 constexpr int WCE_VARIANT_LS = 1;     // configs[1] LS: 2 = one element per thread (ls_elem_kernel, default),
                                       // 3 = the per-frame LIGHT ls_kernel
 constexpr int WCE_VARIANT_REF_LS = 2;  // REF PS_MMSE + LS family (+ eq), C semantics: 0 = ref_ls_elem_kernel

@@ -275,6 +275,9 @@ constexpr int FLAT_U = 8;                               // elements per lane per
 constexpr int FLAT_CHUNK = 64 * FLAT_U;                 // 512
 constexpr int FLAT_FR = (FLAT_CHUNK - 1) / NSC + 2;     // frames one chunk can touch: 11
 static_assert(4 * FLAT_FR <= 64, "one pilot per lane");
+// REF PS_MMSE: batches past this many frames (~the 256 MiB MALL at the 1,360 B
+// a frame's pilot sectors and H move) run mmse_ref_elem_kernel
+constexpr int64_t REF_ELEM_FROM = 196608;
 constexpr int64_t FLAT_MAX_FRAMES = 1ll << 26;          // per launch: e < 2^32
 // frames per launch of the flat kernels: FLAT_MAX_FRAMES, or a smaller
 // multiple of 32 set by wce_debug_set_flat_chunk so that tests reach the
@@ -440,34 +443,30 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
     }
 }
 
-// The same read-out with U (frame, subcarrier) elements per lane and no grid
-// stride (round 6; ls_elem_kernel's store pattern): lane l of a wave owns
-// elements e0 + 64 i + l, i < U, so every store instruction is one contiguous
-// 1 KB run.  The wave's 64 U elements touch at most REF_EFR(U) frames: lanes
-// 4j+p (j < REF_EFR) load frame ff + j's pilot pair p -- issued before the
-// block's u staging, so the two latencies overlap -- the same quad DPP sum
-// forms s_j, and each element takes its frame's s from lane 4j: by readlane
-// at U = 1 (no LDS round trip), from a per-wave LDS table past that.  No chunk
-// loop: the hardware keeps many such short waves in flight.  Arithmetic and
-// summation order are mmse_ref_flat_kernel's: outputs bit-identical.
-constexpr int ref_efr(int u) { return (64 * u - 1) / NSC + 2; }
-template <bool NT, int U>
+// The same read-out with one (frame, subcarrier) element per thread and no
+// grid stride (round 6; ls_elem_kernel's store pattern), for batches past the
+// MALL.  A wave's 64 consecutive elements touch at most 3 frames: lanes 4j+p
+// (j < 3) load frame ff + j's pilot pair p -- issued before the block's u
+// staging, so the two latencies overlap -- the same quad DPP sum forms s_j,
+// and each lane takes its frame's s from lane 4j by readlane (no LDS round
+// trip, no chunk loop: the hardware keeps many such short waves in flight).
+// Arithmetic and summation order are mmse_ref_flat_kernel's: outputs
+// bit-identical.  Measured (1,048,576 frames, profiles/r06_ab_ref_elem.txt):
+// 381 -> 337 us against the capped chunks; 2 or 4 elements per lane (462, 440),
+// plain stores (371), 128 / 512 / 1,024-thread blocks (375 / 340 / 365) lose.
 __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
                                                             uint32_t nfr)
 {
-    constexpr int FR = ref_efr(U);
-    static_assert(4 * FR <= 64, "one pilot per lane");
     __shared__ double2 s_u[64];
-    __shared__ double2 s_s[4][U > 1 ? FR : 1];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const bool shared = a.cs == 0;
     const uint32_t E = nfr * (uint32_t)NSC;
-    const uint32_t e0 = blockIdx.x * (256u * U) + (uint32_t)w * (64u * U);     // the wave's first element
+    const uint32_t e0 = blockIdx.x * 256u + (threadIdx.x & ~63u);     // the wave's first element
     const uint32_t ff = min(e0 / NSC, nfr - 1);
     const int pj = lane & 3;
     const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
-    double2 xt = make_double2(0, 0), xr = xt, wp = xt, uf[U];
-    if (lane < 4 * FR) {
+    double2 xt = make_double2(0, 0), xr = xt, wp = xt, uf = xt;
+    if (lane < 12) {
         const uint32_t fr = min(ff + (uint32_t)(lane >> 2), nfr - 1);
         const int64_t o = (f_begin + fr) * a.fs + (int64_t)a.blk * a.bs + pil;
         xt = ld2(a.tx, o);
@@ -475,50 +474,25 @@ __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restr
         const int64_t wo = shared ? pil : (f_begin + fr) * a.cs + pil;
         wp = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
     }
-    uint32_t fi[U], ki[U];
-#pragma unroll
-    for (int i = 0; i < U; ++i) {
-        const uint32_t e = e0 + 64u * i + lane;
-        fi[i] = min(e / NSC, nfr - 1);
-        ki[i] = e - fi[i] * NSC;
-        uf[i] = make_double2(0, 0);
-        if (!shared && e < E) uf[i] = ld2(a.cu, (f_begin + fi[i]) * a.cs + ki[i]);
-    }
+    const uint32_t e = e0 + lane;
+    const uint32_t f = min(e / NSC, nfr - 1), k = e - f * NSC;
+    if (!shared && e < E) uf = ld2(a.cu, (f_begin + f) * a.cs + k);
     if (shared && threadIdx.x < NSC) s_u[threadIdx.x] = ld2(a.cu, threadIdx.x);
     __syncthreads();
     const double rb = 1.0 / st->bcoef;
     const double2 sj = ref_sum4(quad_sum_c(ref_term(wp, xt, xr)), make_double2(0, 0), make_double2(0, 0),
                                 make_double2(0, 0), rb);
-    double2 sv[U];
-    if constexpr (U == 1) {
-        double sr[FR], si[FR];
+    double sr[3], si[3];
 #pragma unroll
-        for (int j = 0; j < FR; ++j) {
-            sr[j] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.x), 4 * j),
-                                     __builtin_amdgcn_readlane(__double2loint(sj.x), 4 * j));
-            si[j] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.y), 4 * j),
-                                     __builtin_amdgcn_readlane(__double2loint(sj.y), 4 * j));
-        }
-        const uint32_t j = fi[0] - ff;
-        sv[0] = make_double2(j == 0 ? sr[0] : j == 1 ? sr[1] : sr[2], j == 0 ? si[0] : j == 1 ? si[1] : si[2]);
-    } else {
-        if (lane < 4 * FR && pj == 0) s_s[w][lane >> 2] = sj;
-        wave_lds_sync();
-#pragma unroll
-        for (int i = 0; i < U; ++i) {
-            const uint32_t j = fi[i] - ff;
-            sv[i] = s_s[w][j < (uint32_t)FR ? j : FR - 1];
-        }
+    for (int j = 0; j < 3; ++j) {
+        sr[j] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.x), 4 * j),
+                                 __builtin_amdgcn_readlane(__double2loint(sj.x), 4 * j));
+        si[j] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.y), 4 * j),
+                                 __builtin_amdgcn_readlane(__double2loint(sj.y), 4 * j));
     }
-#pragma unroll
-    for (int i = 0; i < U; ++i) {
-        const uint32_t e = e0 + 64u * i + lane;
-        if (e < E) {
-            const double2 h = ref_out(shared ? s_u[ki[i]] : uf[i], sv[i]);
-            if constexpr (NT) st2_nt(a.w, (f_begin + fi[i]) * a.ws + ki[i], h);
-            else st2(a.w, (f_begin + fi[i]) * a.ws + ki[i], h);
-        }
-    }
+    const uint32_t j = f - ff;
+    const double2 s = make_double2(j == 0 ? sr[0] : j == 1 ? sr[1] : sr[2], j == 0 ? si[0] : j == 1 ? si[1] : si[2]);
+    if (e < E) st2_nt(a.w, (f_begin + f) * a.ws + k, ref_out(shared ? s_u[k] : uf, s));
 }
 
 // =====================================================================
@@ -3113,6 +3087,7 @@ int launch_ls(const State *st, const LsArgs &a, void *stream)
 
 int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 {
+    if (a.mmse_done) return WCE_EINVAL;   // only launch_mmse_solve_ls's REF element path honours it
     if (a.n <= 0) return WCE_OK;
     const int64_t waves = a.split ? a.n * a.nblk : a.n;
     if (waves > 0x7fffffffll) return WCE_EINVAL;
@@ -3123,20 +3098,18 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
     if (a.hout && a.ref_pilots && !a.split) {
         for (int64_t f0 = 0, fc = flat_chunk(); f0 < a.n; f0 += fc) {
             const int64_t nf = a.n - f0 < fc ? a.n - f0 : fc;
+            // past the MALL one element per thread (elem), inside it the chunks on a
+            // capped grid (flat): 65,536 frames 20.3 / 25.0 us, 131,072 43.1 / 49.2,
+            // 262,144 102.7 / 89.3, 1,048,576 380.9 / 338.7 (flat / elem)
             const int v = variant(WCE_VARIANT_REF);
-            if (v != 1 && v != 2) {       // U elements per lane, no grid stride (default: U = 1, nontemporal)
-                const int u = v == 4 ? 2 : v == 5 ? 4 : 1;
-                const dim3 g((unsigned)((nf * NSC + 256 * u - 1) / (256 * u))), b(256);
-                const uint32_t n32 = (uint32_t)nf;
-                if (u == 1 && v != 3) hipLaunchKernelGGL((mmse_ref_elem_kernel<true, 1>), g, b, 0, s, st, a, f0, n32);
-                else if (v == 3) hipLaunchKernelGGL((mmse_ref_elem_kernel<false, 1>), g, b, 0, s, st, a, f0, n32);
-                else if (u == 2) hipLaunchKernelGGL((mmse_ref_elem_kernel<true, 2>), g, b, 0, s, st, a, f0, n32);
-                else hipLaunchKernelGGL((mmse_ref_elem_kernel<true, 4>), g, b, 0, s, st, a, f0, n32);
+            if (v == 3 || (v == 0 && nf > REF_ELEM_FROM)) {
+                hipLaunchKernelGGL(mmse_ref_elem_kernel, dim3((unsigned)((nf * NSC + 255) / 256)), dim3(256), 0, s, st,
+                                   a, f0, (uint32_t)nf);
                 continue;
             }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
             int64_t fb = (chunks + LS_WAVES - 1) / LS_WAVES;
-            if (fb > 256 * 8 && v == 1) fb = 256 * 8;
+            if (fb > 256 * 8 && v != 2) fb = 256 * 8;
             hipLaunchKernelGGL(mmse_ref_flat_kernel, dim3((unsigned)fb), dim3(256), 0, s, st, a, f0, (uint32_t)nf);
         }
         return hip_status(hipGetLastError());
@@ -3217,6 +3190,7 @@ const char *lr_kernel_name(int k0, int rank, int taps, int64_t units)
 
 int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs &a, void *stream)
 {
+    if (a.mmse_done) return WCE_EINVAL;
     if (a.n <= 0) return WCE_OK;
     const int64_t waves = a.split ? a.n * a.nblk : a.n;
     if (waves > 0x7fffffffll) return WCE_EINVAL;
@@ -3296,6 +3270,7 @@ int launch_avg_blocks(const double *X, int64_t xs, double *H, int64_t hs, int64_
 
 int launch_fc_finish(const SolveArgs &a, const double *dots, double *H, int64_t hs, void *stream)
 {
+    if (a.mmse_done) return WCE_EINVAL;
     if (a.n <= 0) return WCE_OK;
     hipLaunchKernelGGL(fc_finish_kernel, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a,
                        dots, H, hs);
@@ -3869,6 +3844,7 @@ int launch_matvec(const double *M1, const double *M2, const double *X, int64_t x
 int launch_ref_fc(const State *st, const SolveArgs &a, const double *rx_pre, int64_t ps, const double *tx_pre,
                   void *stream)
 {
+    if (a.mmse_done) return WCE_EINVAL;
     if (a.n <= 0) return WCE_OK;
     if (a.split || !rx_pre || !a.w) return WCE_EINVAL;
     const int64_t blocks = tile_blocks((a.n + 15) / 16, APPLY_WAVES * FC_WG_PER_CU);
@@ -3902,6 +3878,7 @@ int launch_ref_w(const State *st, const double *X, int64_t xs, double *W, int64_
 
 int launch_cm(const State *st, const SolveArgs &a, uint8_t *flags, void *stream)
 {
+    if (a.mmse_done) return WCE_EINVAL;
     if (a.n <= 0) return WCE_OK;
     if (a.split || !flags) return WCE_EINVAL;
     const int64_t blocks = (a.n + 16 * APPLY_WAVES - 1) / (16 * APPLY_WAVES);

@@ -223,7 +223,7 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
             }
     };
     put(st->C, C);
-    // per-frame covariance operators (State::Mg/Mu/Mw), products in 80 bits
+    // per-frame covariance operators (State::Mu, State::Wp), products in 80 bits
     {
         std::vector<cld> Mu(n * n), rhs(n * n);
         if (mode == WCE_MMSE_REF) {
@@ -233,8 +233,6 @@ int host_build_state(State *st, const ldc *Fl, const ldc *invFl, const ldc *H_LS
             for (int j = 0; j < n; j++)
                 for (int c = 0; c < n; c++)
                     Mw[j * n + c] = mk((long double)(creal_d(F[j * n + c]) - cimag_d(F[j * n + c])), 0.0L);
-            put(st->Mg, invF);
-            put(st->Mw, Mw);
             // w_P folded: q(g) = re g - im g is real-linear in (re h, im h)
             for (int p = 0; p < 4; p++)
                 for (int k = 0; k < n; k++) {

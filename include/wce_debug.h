@@ -31,9 +31,10 @@ int wce_debug_set_border_dot(struct wce_ctx *ctx, int on);
 int wce_debug_set_flat_chunk(long long frames);
 /* Kernel variant knobs for interleaved A/B timing and the gate's cross-checks
  * in one process (same buffers, same placement).  which 0: REF PS_MMSE (0 =
- * one element per thread, mmse_ref_elem_kernel, default; 3 = the same with
- * plain stores; 1 = 512-element chunks on a capped grid, round 5's default;
- * 2 = the chunks on an uncapped grid).
+ * by batch size, default: one element per thread, mmse_ref_elem_kernel, past
+ * 196,608 frames, else 512-element chunks on a capped grid; 1 = always the
+ * capped chunks; 2 = the chunks on an uncapped grid; 3 = always one element
+ * per thread).
  * which 1: LT_LS + PS_Linear in C semantics (2 = one element per thread,
  * ls_elem_kernel, default; 3 = the per-frame LIGHT kernel).  which 2: REF
  * PS_MMSE with LS outputs in one call (0 = one element per thread,

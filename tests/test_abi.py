@@ -240,7 +240,7 @@ def test_ref_pilot_row_map(wce, golden, oracle):
     = re F[r][c] - im F[r][c]) on random h: within 1e-15 of the chain's scale."""
     r = golden["ref"]
     blob = wce.state_blob(r["pre_tx"][0], r["pre_rx"][0], r["ow2"], wce.MMSE_REF)
-    off = 4 * 64 * 64 * 16                                   # past C, Mg, Mu, Mw
+    off = 2 * 64 * 64 * 16                                   # past C, Mu
     Wp = blob[off:off + 4 * 64 * 16].view(np.float64).reshape(4, 64, 2)
     assert not np.any(Wp[:, N:])
     F, invF = from_split(r["F"]), from_split(r["invF"])

@@ -36,10 +36,19 @@ def _run(wce, ctx, n, mask, pre):
     return outs
 
 
-@pytest.mark.parametrize("mode,mask,per_frame_pre", [(0, 0b00011, True), (0, 0b10000, False)],
-                         ids=["ls_flat_config2", "ref_flat_mmse"])
-def test_multi_launch_bit_identical(gpu_wce, golden, chunked, mode, mask, per_frame_pre):
+@pytest.mark.parametrize("mode,mask,per_frame_pre,ref_form", [(0, 0b00011, True, 0), (0, 0b10000, False, 1),
+                                                             (0, 0b10000, False, 3)],
+                         ids=["ls_flat_config2", "ref_flat_mmse", "ref_elem_mmse"])
+def test_multi_launch_bit_identical(gpu_wce, golden, chunked, mode, mask, per_frame_pre, ref_form):
     wce = gpu_wce
+    assert wce.load().wce_debug_set_variant(0, ref_form) == 0   # REF read-out form (which 0)
+    try:
+        _multi_launch(wce, golden, chunked, mode, mask, per_frame_pre)
+    finally:
+        assert wce.load().wce_debug_set_variant(0, 0) == 0
+
+
+def _multi_launch(wce, golden, chunked, mode, mask, per_frame_pre):
     inp = golden["inputs"]
     ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], mode, device=0)
     n = 2500                                                   # 1024 + 1024 + 452 at chunk 1024

@@ -133,15 +133,19 @@ def test_frame_cov_errors(gpu_wce, golden):
 @pytest.mark.parametrize("mask_name", ["MMSE", "ALL", "MMSE_LIN"])
 @pytest.mark.parametrize("f32", [False, True])
 def test_ref_fused_factor_kernel_equals_four_launches(gpu_wce, golden, oracle, mask_name, f32):
-    """REF + FRAME_COV in C semantics runs ref_fc_kernel (round 4): LT_LS of
-    the frame's preamble, g = invF h and u = F invF h on MFMA, w = Mw q(g)
-    at the 4 pilot rows only, and (PS_MMSE alone) s and H = u s, in one
-    launch.  It rounds every value as the four launches it replaces (LT_LS
-    pass, two matvec launches, REF read-out: variant WCE_VARIANT_REF_FC = 1),
-    so H and every LS output are bit-identical, on a ragged batch (not a
-    multiple of 16 frames), block 2 of the frame, a caller tx_pre, and a
-    non-dense output stride; frames vs the bit-exact oracle of main.c's
-    PS_MMSE with the frame's own LT_LS (main.c:37-53, 148-205)."""
+    """REF + FRAME_COV in C semantics runs ref_fc_kernel (round 5 form): LT_LS
+    of the frame's preamble, u = Mu h (Mu = F invF_ref) on MFMA, w at the 4
+    pilot rows from the folded 80-bit real map State::Wp (g = invF h is never
+    formed), s and H = u s -- H is always written by this launch; when the
+    call also asks for LS outputs they come from a second launch,
+    ref_ls_elem_kernel with mmse_done = 1.  The four-launch variant path
+    (WCE_VARIANT_REF_FC = 1: LT_LS pass, matvec launches, ref_w_kernel from the
+    same Wp, REF read-out) rounds alike, so H and every LS output are
+    bit-identical between the two, on a ragged batch (not a multiple of 16
+    frames), block 2 of the frame, a caller tx_pre, and a non-dense output
+    stride.  Against main.c's PS_MMSE with the frame's own LT_LS (the oracle,
+    main.c:37-53, 148-205) parity is held by tolerance, not bitwise: the Wp
+    fold rounds once where main.c rounds g, q(g) and w separately."""
     wce = gpu_wce
     lib = wce.load()
     r = golden["ref"]

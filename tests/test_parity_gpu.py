@@ -572,11 +572,23 @@ def oracle_lt(inp, rp, sem):
     return h
 
 
-def test_ref_flat_batch_edges(gpu_wce, golden, oracle):
-    """REF-mode PS_MMSE runs mmse_ref_flat_kernel (flat (frame, subcarrier)
-    elements, 512 per wave-chunk, <= 11 frames per chunk): batch sizes around
-    the chunk and the grid-stride sweep, sampled frames vs the bit-exact REF
+@pytest.mark.parametrize("variant", [1, 3])
+def test_ref_flat_batch_edges(gpu_wce, golden, oracle, variant):
+    """REF-mode PS_MMSE: mmse_ref_flat_kernel (variant 1: flat (frame,
+    subcarrier) elements, 512 per wave-chunk, <= 11 frames per chunk) and
+    mmse_ref_elem_kernel (variant 3: one element per thread, <= 3 frames per
+    wave; the default past 196,608 frames): batch sizes around the chunk, the
+    wave and the grid-stride sweep, sampled frames vs the bit-exact REF
     oracle, output rows padded to 60 with the padding left untouched."""
+    lib = gpu_wce.load()
+    assert lib.wce_debug_set_variant(0, variant) == 0
+    try:
+        _ref_batch_edges(gpu_wce, golden, oracle)
+    finally:
+        assert lib.wce_debug_set_variant(0, 0) == 0
+
+
+def _ref_batch_edges(gpu_wce, golden, oracle):
     r = golden["ref"]
     inp = golden["inputs"]
     ctx = gpu_wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], gpu_wce.MMSE_REF)
@@ -586,7 +598,7 @@ def test_ref_flat_batch_edges(gpu_wce, golden, oracle):
     F, invF = from_split(r["F"]), from_split(r["invF"])
     hls = oracle.lt_ls(inp["tx_pre"], inp["rx_pre"])
     os_ = 60
-    for B in (1, 3, 10, 11, 12, 97, 4096, Bmax):
+    for B in (1, 2, 3, 10, 11, 12, 97, 4096, Bmax):
         H = gpu_wce.DeviceArray((B, os_), zero=True)
         ctx.estimate(ctx.frames(tx, rx, B), gpu_wce.Outputs(None, None, None, None, H.addr, None, os_, 0, 0, 0, 0),
                      gpu_wce.PS_MMSE)
