@@ -754,10 +754,26 @@ def compact(res, extras_path):
     for k in ("small_batch", "ldc_convert"):
         if isinstance(res.get(k), dict) and "error" in res[k]:
             legs[k] = {"error": res[k]["error"]}
-    out["legs"] = legs
+    # the driver's record keeps the last 2,000 characters of stdout: the legs a
+    # reader checks first (configs[3] and [4], REF past the MALL, the dense and
+    # tap-domain COV solves, configs[1]) go last, so they are the ones it keeps
+    last = ("ls_config2", "cov_mode", "lowrank_L24", "lowrank_L53", "ref_mode", "config5_sharded", "config4")
+    ordered = {k: v for k, v in legs.items() if k not in last}
+    ordered.update({k: legs[k] for k in last if k in legs})
     out["dist_check"] = res.get("dist_check")
     out["extras_file"] = extras_path
+    out["legs"] = _round_sig(ordered)
     return out
+
+
+def _round_sig(x, sig=5):
+    """floats of the leg summaries to `sig` significant digits (the line is
+    read from a 2,000-character tail; the full values are in the extras file)"""
+    if isinstance(x, dict):
+        return {k: _round_sig(v, sig) for k, v in x.items()}
+    if isinstance(x, float) and x == x and x not in (float("inf"), float("-inf")) and x != 0.0:
+        return float(f"{x:.{sig}g}")
+    return x
 
 
 def emit(res, extras_path):

@@ -7,7 +7,7 @@ legs (bench.py field -> kernel, frames per launch):
   headline   roofline            mmse_solve_fc_kernel             65,536 (TEXTBOOK, 1 wave/frame)
   apply      apply_kernel        apply_kernel                     65,536 (COV H = C W, persistent since round 5)
   cov_solve  cov_mode            mmse_solve_kernel<false>         65,536 (COV dense solve)
-  ref        ref_mode.b1048576   mmse_ref_flat_kernel          1,048,576 (REF, main.c semantics)
+  ref        ref_mode.b1048576   mmse_ref_elem_kernel          1,048,576 (REF, main.c semantics)
   ls         ls_config2          ls_flat_kernel                1,048,576 (LT_LS + PS_Linear)
   ls_pilots  (calibration)       ls_flat_kernel                1,048,576 (PS_Linear only: pilot reads)
   front_*    front_end           front_kernel<false/true>         65,536 frames (x 15 blocks / 1 LTF)
@@ -35,7 +35,7 @@ LEGS = {
     "apply": ("apply_kernel", 65536),                # round 5: the streaming kernel at every size
     "apply1m": ("apply_kernel", 1 << 20),             # the same at configs[3]'s batch
     "cov_solve": ("mmse_solve_kernel<false>", 65536),
-    "ref": ("mmse_ref_flat_kernel", 1 << 20),
+    "ref": ("mmse_ref_elem_kernel", 1 << 20),          # round 6: one element per thread past the MALL
     "ls": ("ls_elem_kernel", 1 << 20),
     "ls_pilots": ("ls_elem_kernel", 1 << 20),      # PS_Linear only: calibrates the pilot-sector reads
     "front_blocks": ("front_kernel<false>", 65536),
