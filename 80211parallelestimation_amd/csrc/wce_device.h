@@ -128,4 +128,78 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+
+// ---------------------------------------------------------------- shared by the kernel files
+// 1/sqrt(d) from v_rsq_f64 (relative error ~2^-24).  One third-order
+// (Householder) step y += y e (1/2 + 3e/8), e = 1 - d y^2: error ~2^-72
+// before rounding, 5 VALU on a 4-deep chain (two Newton steps: 7 on 6, 2.1%
+// slower, retired in round 4).
+__device__ __forceinline__ double rsq_nr(double d)
+{
+    const double y = __builtin_amdgcn_rsq(d);
+    const double e = fma(-d * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
+}
+
+// 53-point DFTs on lane m: E[k m mod 53] gathered by byte offset, the step m * 16
+// added, 848 subtracted when it
+// wraps -- min_u32(o + s, o + s - 848) (the wrapped value underflows to a huge
+// unsigned when no wrap is due): three integer ops and no shift per gather
+__device__ __forceinline__ uint32_t dft_step(uint32_t o, uint32_t s, uint32_t s_wrap)
+{
+    return min(o + s, o + s_wrap);
+}
+__device__ __forceinline__ double2 ld_e(const double2 *e, uint32_t o)
+{
+    return *reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(e) + o);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    // every lane of the 16-lane row reads a valid source lane for the controls
+    // used here (row_newbcast, quad_perm, mirrors), so no "old" value is needed:
+    // mov_dpp is one v_mov_b32_dpp per half, where update_dpp(0, ...) also
+    // materialised the zero (a v_mov_b32 per half)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+template <int N>
+__device__ __forceinline__ double2 row_bcast(double2 v)   // lane N of each 16-lane row, to the row
+{
+    return make_double2(dpp_f64<0x150 + N>(v.x), dpp_f64<0x150 + N>(v.y));
+}
+__device__ __forceinline__ double row16_sum(double v)   // over a 16-lane row, the same bits in every lane
+{
+    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);   // row_half_mirror
+    v += dpp_f64<0x140>(v);   // row_mirror
+    return v;
+}
+__device__ __forceinline__ double2 row16_sum(double2 v) { return make_double2(row16_sum(v.x), row16_sum(v.y)); }
+
+__device__ __forceinline__ double2 row_bcast_n(double2 v, int n)   // n a constant after unrolling
+{
+    switch (n) {
+    case 0: return row_bcast<0>(v);
+    case 1: return row_bcast<1>(v);
+    case 2: return row_bcast<2>(v);
+    case 3: return row_bcast<3>(v);
+    case 4: return row_bcast<4>(v);
+    case 5: return row_bcast<5>(v);
+    case 6: return row_bcast<6>(v);
+    case 7: return row_bcast<7>(v);
+    case 8: return row_bcast<8>(v);
+    case 9: return row_bcast<9>(v);
+    case 10: return row_bcast<10>(v);
+    case 11: return row_bcast<11>(v);
+    case 12: return row_bcast<12>(v);
+    case 13: return row_bcast<13>(v);
+    case 14: return row_bcast<14>(v);
+    default: return row_bcast<15>(v);
+    }
+}
+
 }  // namespace wce

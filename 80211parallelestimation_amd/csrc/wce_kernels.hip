@@ -454,6 +454,16 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
 // bit-identical.  Measured (1,048,576 frames, profiles/r06_ab_ref_elem.txt):
 // 381 -> 337 us against the capped chunks; 2 or 4 elements per lane (462, 440),
 // plain stores (371), 128 / 512 / 1,024-thread blocks (375 / 340 / 365) lose.
+// XCD: blocks dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
+// dispatch) are remapped so that each XCD walks one contiguous run of the
+// elements -- a frame whose pilots two neighbouring blocks both read then sits
+// in one XCD's L2 instead of being fetched by two (bijective for any grid).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+{
+    const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+template <bool XCD>
 __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
                                                             uint32_t nfr)
 {
@@ -461,7 +471,8 @@ __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restr
     const int lane = threadIdx.x & 63;
     const bool shared = a.cs == 0;
     const uint32_t E = nfr * (uint32_t)NSC;
-    const uint32_t e0 = blockIdx.x * 256u + (threadIdx.x & ~63u);     // the wave's first element
+    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t e0 = blk * 256u + (threadIdx.x & ~63u);     // the wave's first element
     const uint32_t ff = min(e0 / NSC, nfr - 1);
     const int pj = lane & 3;
     const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
@@ -627,16 +638,6 @@ static_assert(sizeof(TapsLds) == 12288, "12 waves of the tap kernel per CU");
 // free (an XOR swizzle of an unpadded buffer measured 1% slower: address VALU).
 
 
-// 1/sqrt(d) from v_rsq_f64 (relative error ~2^-24).  One third-order
-// (Householder) step y += y e (1/2 + 3e/8), e = 1 - d y^2: error ~2^-72
-// before rounding, 5 VALU on a 4-deep chain (two Newton steps: 7 on 6, 2.1%
-// slower, retired in round 4).
-__device__ __forceinline__ double rsq_nr(double d)
-{
-    const double y = __builtin_amdgcn_rsq(d);
-    const double e = fma(-d * y, y, 1.0);
-    return fma(y * e, fma(e, 0.375, 0.5), y);
-}
 
 // acc -= l conj(c) on the lanes of the (compile-time) lane mask m only.  The
 // other lanes carry elements that are never read (upper halves of diagonal
@@ -1585,18 +1586,6 @@ __device__ __forceinline__ void dft_pairs(const double2 *c, double2 *pa, double2
         pb[lane] = csub(u, w);
     }
 }
-// lane m: sum_k c_k E[k m] (CONJ: conj(E[k m])) = c_0 + sum over the pairs
-// E[k m mod 53] by byte offset: the step m * 16 added, 848 subtracted when it
-// wraps -- min_u32(o + s, o + s - 848) (the wrapped value underflows to a huge
-// unsigned when no wrap is due): three integer ops and no shift per gather
-__device__ __forceinline__ uint32_t dft_step(uint32_t o, uint32_t s, uint32_t s_wrap)
-{
-    return min(o + s, o + s_wrap);
-}
-__device__ __forceinline__ double2 ld_e(const double2 *e, uint32_t o)
-{
-    return *reinterpret_cast<const double2 *>(reinterpret_cast<const char *>(e) + o);
-}
 // y(m) = c_0 + sum_k (pa_k Re E[k m] + i pb_k Im E[k m]) over the pairs (k, 53 - k), outputs m and 53 - m together (E[k (53 - m)] =
 // conj(E[k m]): A = sum pa_k Re E, B = i sum pb_k Im E (CONJ: -Im), y(m) = c_0 + A
 // + B, y(53 - m) = c_0 + A - B), half-wave h over the pairs k = 1 + 13 h ..
@@ -2282,53 +2271,6 @@ __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_
 //   H_k = U_k s for the lane's 4 subcarriers: 16 lanes store 256 B of one frame.
 // Same algebra as mmse_lr_kernel, summed in another order (~1e-15).
 // ---------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v)
-{
-    // every lane of the 16-lane row reads a valid source lane for the controls
-    // used here (row_newbcast, quad_perm, mirrors), so no "old" value is needed:
-    // mov_dpp is one v_mov_b32_dpp per half, where update_dpp(0, ...) also
-    // materialised the zero (a v_mov_b32 per half)
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
-    return __hiloint2double(hi, lo);
-}
-template <int N>
-__device__ __forceinline__ double2 row_bcast(double2 v)   // lane N of each 16-lane row, to the row
-{
-    return make_double2(dpp_f64<0x150 + N>(v.x), dpp_f64<0x150 + N>(v.y));
-}
-__device__ __forceinline__ double row16_sum(double v)   // over a 16-lane row, the same bits in every lane
-{
-    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
-    v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
-    v += dpp_f64<0x141>(v);   // row_half_mirror
-    v += dpp_f64<0x140>(v);   // row_mirror
-    return v;
-}
-__device__ __forceinline__ double2 row16_sum(double2 v) { return make_double2(row16_sum(v.x), row16_sum(v.y)); }
-
-__device__ __forceinline__ double2 row_bcast_n(double2 v, int n)   // n a constant after unrolling
-{
-    switch (n) {
-    case 0: return row_bcast<0>(v);
-    case 1: return row_bcast<1>(v);
-    case 2: return row_bcast<2>(v);
-    case 3: return row_bcast<3>(v);
-    case 4: return row_bcast<4>(v);
-    case 5: return row_bcast<5>(v);
-    case 6: return row_bcast<6>(v);
-    case 7: return row_bcast<7>(v);
-    case 8: return row_bcast<8>(v);
-    case 9: return row_bcast<9>(v);
-    case 10: return row_bcast<10>(v);
-    case 11: return row_bcast<11>(v);
-    case 12: return row_bcast<12>(v);
-    case 13: return row_bcast<13>(v);
-    case 14: return row_bcast<14>(v);
-    default: return row_bcast<15>(v);
-    }
-}
 template <int R, int C>
 __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
 {
@@ -3102,9 +3044,10 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
             // capped grid (flat): 65,536 frames 20.3 / 25.0 us, 131,072 43.1 / 49.2,
             // 262,144 102.7 / 89.3, 1,048,576 380.9 / 338.7 (flat / elem)
             const int v = variant(WCE_VARIANT_REF);
-            if (v == 3 || (v == 0 && nf > REF_ELEM_FROM)) {
-                hipLaunchKernelGGL(mmse_ref_elem_kernel, dim3((unsigned)((nf * NSC + 255) / 256)), dim3(256), 0, s, st,
-                                   a, f0, (uint32_t)nf);
+            if (v == 3 || v == 4 || (v == 0 && nf > REF_ELEM_FROM)) {
+                const dim3 g((unsigned)((nf * NSC + 255) / 256));
+                if (v == 4) hipLaunchKernelGGL(mmse_ref_elem_kernel<true>, g, dim3(256), 0, s, st, a, f0, (uint32_t)nf);
+                else hipLaunchKernelGGL(mmse_ref_elem_kernel<false>, g, dim3(256), 0, s, st, a, f0, (uint32_t)nf);
                 continue;
             }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
@@ -3122,8 +3065,13 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
 
 // Which low-rank kernel a (rank, units) launch runs: one decision shared by
 // launch_mmse_lr and lr_kernel_name (wce_debug_lr_kernel: bench labels, tests)
-enum class LrForm { Direct, Staged64, Staged, StagedMW, Quad, Wave };
-static LrForm lr_form(int rank, int64_t units)
+enum class LrForm { Direct, Staged64, Staged, StagedMW, Quad, Quad2, Wave };
+// taps: bit 0 State::cov_taps (a diagonal Rhh: the wave kernel's tap-domain
+// Gram), bit 1 State::taps_contig (kept taps 0..r-1: the quad and lane
+// kernels' Toeplitz form).  Variant 5 runs the product Gram everywhere (A/B).
+static bool lr_taps(int taps) { return (taps & 1) && variant(WCE_VARIANT_LR) != 5; }
+static bool lr_contig(int taps) { return (taps & 2) && variant(WCE_VARIANT_LR) != 5; }
+static LrForm lr_form(int rank, int64_t units, int taps)
 {
     int lv = variant(WCE_VARIANT_LR);
     if (lv == 5) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), not the kernel form
@@ -3141,14 +3089,12 @@ static LrForm lr_form(int rank, int64_t units)
         return rank >= 7 && LR_STAGED_MINWG > 1 && many ? LrForm::StagedMW : LrForm::Staged;
     }
     if (rank > LRL_RMAX && rank <= 16 && lv == 0) return LrForm::Quad;
+    // ranks 17..32 with taps 0..r-1: two rows per lane (the Toeplitz Gram only;
+    // other covariances keep the wave kernel's product / tap-domain Gram)
+    if (rank > 16 && rank <= 32 && lv == 0 && lr_contig(taps)) return LrForm::Quad2;
     return LrForm::Wave;
 }
 
-// taps: bit 0 State::cov_taps (a diagonal Rhh: the wave kernel's tap-domain
-// Gram), bit 1 State::taps_contig (kept taps 0..r-1: the quad and lane
-// kernels' Toeplitz form).  Variant 5 runs the product Gram everywhere (A/B).
-static bool lr_taps(int taps) { return (taps & 1) && variant(WCE_VARIANT_LR) != 5; }
-static bool lr_contig(int taps) { return (taps & 2) && variant(WCE_VARIANT_LR) != 5; }
 
 const char *lr_kernel_name(int k0, int rank, int taps, int64_t units)
 {
@@ -3164,6 +3110,8 @@ const char *lr_kernel_name(int k0, int rank, int taps, int64_t units)
         {"mmse_lr_quad_kernel<9, true>", "mmse_lr_quad_kernel<10, true>", "mmse_lr_quad_kernel<11, true>",
          "mmse_lr_quad_kernel<12, true>", "mmse_lr_quad_kernel<13, true>", "mmse_lr_quad_kernel<14, true>",
          "mmse_lr_quad_kernel<15, true>", "mmse_lr_quad_kernel<16, true>"}};
+    static const char *quad2[4] = {"mmse_lr_quad2_kernel<20>", "mmse_lr_quad2_kernel<24>", "mmse_lr_quad2_kernel<28>",
+                                   "mmse_lr_quad2_kernel<32>"};
     static const char *wave[2][7] = {
         {"mmse_lr_kernel<0>", "mmse_lr_kernel<1>", "mmse_lr_kernel<2>", "mmse_lr_kernel<3>", "mmse_lr_kernel<4>",
          "mmse_lr_kernel<5>", "mmse_lr_kernel<6>"},
@@ -3178,12 +3126,13 @@ const char *lr_kernel_name(int k0, int rank, int taps, int64_t units)
         "mmse_lr_lane_staged_kernel<7, 1, true>", "mmse_lr_lane_staged_kernel<8, 1, true>"};
     static_assert(LR_STAGED_MINWG == 2 || LR_STAGED_MINWG <= 1, "lr_kernel_name spells MW = 2");
     const int r = rank < 1 ? 1 : (rank > LRL_RMAX ? LRL_RMAX : rank);
-    switch (lr_form(rank, units)) {
+    switch (lr_form(rank, units, taps)) {
     case LrForm::Direct: return lane[0][r];
     case LrForm::Staged64:
     case LrForm::Staged: return lr_contig(taps) && lr_staged_threads(r) == 256 ? lanetq[r] : lane[1][r];
     case LrForm::StagedMW: return mw[lr_contig(taps) ? 1 : 0][r >= 8 ? 1 : 0];
     case LrForm::Quad: return quad[lr_contig(taps) ? 1 : 0][(rank > 16 ? 16 : rank) - 9];
+    case LrForm::Quad2: return quad2[(rank > 32 ? 32 - 17 : rank - 17) / 4];
     default: return k0 >= 0 && k0 <= 6 ? wave[lr_taps(taps) ? 1 : 0][k0] : "";
     }
 }
@@ -3196,7 +3145,7 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
     if (waves > 0x7fffffffll) return WCE_EINVAL;
     if (a.nblk > 1 && !a.split) return WCE_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    const LrForm form = lr_form(rank, waves);
+    const LrForm form = lr_form(rank, waves, taps);
     if (form == LrForm::Direct || form == LrForm::Staged64 || form == LrForm::Staged || form == LrForm::StagedMW) {
         // direct form: fewer units per wave on a small batch (latency-bound at one wave per SIMD)
         const int fpw = waves <= LR_FPW_BELOW ? LR_FPW : 64;
@@ -3245,6 +3194,7 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
 #undef WCE_LRQ
         return hip_status(hipGetLastError());
     }
+    if (form == LrForm::Quad2) return launch_lr_quad2(st, rank, a, stream);   // wce_lr_quad2.hip
     const dim3 g((unsigned)waves), b(64);
     const bool tp = lr_taps(taps);
 #define WCE_LRW(K)                                                                               \

@@ -1,0 +1,255 @@
+// wce_lr_quad2.hip -- WCE_MMSE_COV at ranks 17..32 of a power-delay profile
+// with taps 0..r-1 (round 6): mmse_lr_quad2_kernel, its own translation unit
+// (its unrolled 20..32-row Cholesky compiles in parallel with wce_kernels.hip).
+#include "wce_internal.h"
+#include "wce_device.h"
+
+namespace wce {
+
+// ---------------------------------------------------------------------
+// Ranks 17..32 of a power-delay profile with taps 0..R-1 (State::taps_contig,
+// round 6): the quad kernel's 16-lane Toeplitz form with TWO rows per lane.
+// Lane i of a 16-lane DPP row holds row i of the R x R system in Ar (columns
+// 0..15 only: row i < 16 needs j <= i) and row i + 16 in Br (lanes i < R - 16).
+// Every broadcast stays inside the DPP row (row_newbcast:n from lane n of the
+// set that holds the source row), so the 53-row block-cyclic machinery of the
+// wave kernel (0.33 ms per 65,536 frames at rank 24, 20% of FP64 peak) is not
+// needed:
+//   Gram     Q(i), Q(i + 16) and beta_i, beta_{i+16}: two DFTs per lane over
+//            the frame's |x|^2 and conj(x) rx, E[k d mod 53] from LDS by the
+//            exact index recurrence (as the quad kernel)
+//   Cholesky pivot C < 16 updates Ar[j] (j < 16) and Br[j]; C >= 16 Br only
+//   z = L^-1 beta by broadcasts, t = L^-H z by 16-lane DPP sums
+//   complex x: the quad kernel's correction term; H_k = sum_j s_j t_j E[k j]
+// Same algebra as mmse_lr_quad_kernel / mmse_lr_kernel, summed in another
+// order (~1e-15).
+// ---------------------------------------------------------------------
+template <int R, int C>
+__device__ __forceinline__ void lrq2_chol(double2 (&Ar)[16], double2 (&Br)[R], double &lda, double &ldb, int i)
+{
+    if constexpr (C < R) {
+        if constexpr (C < 16) {
+            const double rs = rsq_nr(row_bcast<C>(Ar[C]).x);   // pivot (C, C) from lane C's row
+            Ar[C] = cscale(Ar[C], rs);                        // L[i][C], L[i + 16][C]
+            Br[C] = cscale(Br[C], rs);
+            lda = i == C ? rs : lda;
+#pragma unroll
+            for (int j = C + 1; j < 16; ++j) {                // rows i >= j of both sets
+                const double2 lj = row_bcast_n(Ar[C], j);
+                cmsub_conj(Ar[j], Ar[C], lj);
+                cmsub_conj(Br[j], Br[C], lj);
+            }
+#pragma unroll
+            for (int j = 16; j < R; ++j) {                    // rows i + 16 >= j only
+                const double2 lj = row_bcast_n(Br[C], j - 16);
+                cmsub_conj(Br[j], Br[C], lj);
+            }
+        } else {
+            const double rs = rsq_nr(row_bcast<C - 16>(Br[C]).x);
+            Br[C] = cscale(Br[C], rs);
+            ldb = i == C - 16 ? rs : ldb;
+#pragma unroll
+            for (int j = C + 1; j < R; ++j) {
+                const double2 lj = row_bcast_n(Br[C], j - 16);
+                cmsub_conj(Br[j], Br[C], lj);
+            }
+        }
+        lrq2_chol<R, C + 1>(Ar, Br, lda, ldb, i);
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
+{
+    static_assert(R > 16 && R <= 32, "two rows per lane");
+    constexpr int R2 = R - 16;
+    const int i = threadIdx.x & 15;                   // rows i and i + 16 of the system
+    const int rw = (threadIdx.x >> 4) & 15;           // the unit's 16-lane row in the workgroup
+    const int64_t units = a.split ? a.n * a.nblk : a.n;
+    const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    __shared__ double2 sE[64];
+    __shared__ double2 sQ[16][32];    // one unit's Q(0..31)
+    __shared__ double2 sV[16][56];    // the unit's frame: conj(x_k) rx_k ...
+    __shared__ double sW[16][56];     // ... and |x_k|^2
+    if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
+    __syncthreads();
+    if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows
+    const int64_t f = a.split ? g / a.nblk : g;
+    const int b = a.split ? (int)(g - f * a.nblk) : 0;
+    const int64_t base = f * a.fs + (int64_t)(a.blk + b) * a.bs;
+    const double ac = st->acoef, bc = st->bcoef;
+    const uint64_t xm = st->xmask;
+    const bool rowb = i < R2;
+    bool cplx = false;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {   // the frame through LDS: 256 B per row and instruction
+        const int k = i + 16 * m;
+        if (k < NSC) {
+            double2 x = ld2(a.tx, base + k);
+            const double2 r = ld2(a.rx, base + k);
+            if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+            cplx |= x.y != 0.0;
+            sW[rw][k] = fma(x.x, x.x, x.y * x.y);
+            sV[rw][k] = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+        }
+    }
+    wave_lds_sync();
+    // Q(d) = sum_k p_k conj(E[k d]) and sum_k v_k conj(E[k d]) at d = i and d = i + 16
+    double2 qa = make_double2(0.0, 0.0), qb = qa, ba = qa, bb = qa;
+    {
+        const uint32_t sa = 16u * (uint32_t)i, swa = sa - 16u * NSC;
+        const uint32_t sb = 16u * (uint32_t)(i + 16), swb = sb - 16u * NSC;
+        uint32_t oa = 0, ob = 0;
+#pragma unroll 4
+        for (int k = 0; k < NSC; ++k) {
+            const double2 ea = ld_e(sE, oa), eb = ld_e(sE, ob), v = sV[rw][k];
+            const double w = sW[rw][k];
+            qa.x = fma(w, ea.x, qa.x);
+            qa.y = fma(-w, ea.y, qa.y);
+            qb.x = fma(w, eb.x, qb.x);
+            qb.y = fma(-w, eb.y, qb.y);
+            ba.x = fma(v.x, ea.x, fma(v.y, ea.y, ba.x));
+            ba.y = fma(v.y, ea.x, fma(-v.x, ea.y, ba.y));
+            bb.x = fma(v.x, eb.x, fma(v.y, eb.y, bb.x));
+            bb.y = fma(v.y, eb.x, fma(-v.x, eb.y, bb.y));
+            oa = dft_step(oa, sa, swa);
+            ob = dft_step(ob, sb, swb);
+        }
+    }
+    const double sia = st->col_s[i], sib = rowb ? st->col_s[i + 16] : 0.0;
+    sQ[rw][i] = qa;
+    sQ[rw][i + 16] = qb;
+    wave_lds_sync();
+    double2 Ar[16], Br[R];   // a s_r s_j Q(r - j) + b [r == j]  (Q(-d) = conj(Q(d)))
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const double2 qd = j <= i ? sQ[rw][(i - j) & 31] : cconj(sQ[rw][(j - i) & 31]);
+        Ar[j] = cscale(qd, ac * sia * st->col_s[j]);
+        Ar[j].x += i == j ? bc : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int d = i + 16 - j;
+        const double2 qd = d >= 0 ? sQ[rw][d & 31] : cconj(sQ[rw][(-d) & 31]);
+        Br[j] = cscale(qd, ac * sib * st->col_s[j]);   // zero on lanes without a second row
+        Br[j].x += (rowb && i + 16 == j) ? bc : 0.0;
+    }
+    double lda = 1.0, ldb = 1.0;
+    lrq2_chol<R, 0>(Ar, Br, lda, ldb, i);
+    // z = L^-1 beta (beta_r = s_r sum_k v_k conj(E[k r])): lane i keeps z_i, z_{i+16}
+    double2 za = cscale(ba, sia), zb = cscale(bb, sib);
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+        if (c < 16) {
+            const double2 zc = row_bcast_n(cscale(za, lda), c);
+            if (i == c) za = zc;
+            else if (i > c) za = csub(za, cmul(Ar[c], zc));
+            zb = csub(zb, cmul(Br[c], zc));
+        } else {
+            const double2 zc = row_bcast_n(cscale(zb, ldb), c - 16);
+            if (i == c - 16) zb = zc;
+            else if (i + 16 > c) zb = csub(zb, cmul(Br[c], zc));
+        }
+    }
+    // t = L^-H z: t_c = (z_c - sum_{m > c} conj(L[m][c]) t_m) / L_cc, the sum over both sets of the row
+    double2 ta = make_double2(0.0, 0.0), tb = ta;
+#pragma unroll
+    for (int c = R - 1; c >= 0; --c) {
+        double2 term = rowb && i + 16 > c ? cmul(cconj(Br[c]), tb) : make_double2(0.0, 0.0);
+        if (c < 16 && i > c) term = cadd(term, cmul(cconj(Ar[c < 16 ? c : 0]), ta));
+        const double2 sum = row16_sum(term);
+        if (c < 16) {
+            if (i == c) ta = cscale(csub(za, sum), lda);
+        } else if (i == c - 16) {
+            tb = cscale(csub(zb, sum), ldb);
+        }
+    }
+    double *W = a.w + 2 * g * a.ws;
+    const double2 *__restrict__ UT = reinterpret_cast<const double2 *>(st->UT);
+    if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
+        double2 vk[4], rk[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = i + 16 * m;
+            const int kc = k < NSC ? k : 0;
+            double2 x = ld2(a.tx, base + kc);
+            const double2 r = ld2(a.rx, base + kc);
+            if (!((xm >> kc) & 1ull) || k >= NSC) x = make_double2(0.0, 0.0);
+            vk[m] = x;
+            rk[m] = r;
+        }
+        double2 uy[4] = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double2 tj = j < 16 ? row_bcast_n(ta, j) : row_bcast_n(tb, j - 16);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int k = i + 16 * m;
+                uy[m] = cadd(uy[m], cmul(UT[j * CLD + (k < NSC ? k : 0)], tj));
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double2 x = vk[m];
+            const double2 rho = csub(rk[m], cscale(cmul(x, uy[m]), ac));
+            vk[m] = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
+        }
+        const double rb = 1.0 / bc;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            double2 cp = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int k = i + 16 * m;
+                cp = cadd(cp, cmul(cconj(UT[j * CLD + (k < NSC ? k : 0)]), vk[m]));
+            }
+            const double2 cj = row16_sum(cp);
+            if (j < 16 && i == j) ta = cadd(ta, cscale(cj, rb));
+            if (j >= 16 && i == j - 16) tb = cadd(tb, cscale(cj, rb));
+        }
+    }
+    // H_k = sum_j s_j t_j E[k j] at k = i + 16 m: E from LDS by the index recurrence over j
+    double2 y[4];
+    uint32_t eo[4], es[4], ew[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int k = i + 16 * m;
+        y[m] = make_double2(0.0, 0.0);
+        es[m] = 16u * (uint32_t)(k < NSC ? k : 0);
+        ew[m] = es[m] - 16u * NSC;
+        eo[m] = 0;
+    }
+    const double2 ca = cscale(ta, sia), cb = cscale(tb, sib);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const double2 cj = j < 16 ? row_bcast_n(ca, j) : row_bcast_n(cb, j - 16);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double2 u = ld_e(sE, eo[m]);
+            y[m].x = fma(u.x, cj.x, fma(-u.y, cj.y, y[m].x));
+            y[m].y = fma(u.x, cj.y, fma(u.y, cj.x, y[m].y));
+            eo[m] = dft_step(eo[m], es[m], ew[m]);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        if (i + 16 * m < NSC) st2(W, i + 16 * m, y[m]);
+}
+
+int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream)
+{
+    // instantiated at 20, 24, 28, 32 rows: a rank r below runs the next size
+    // up with rows r.. as b I (col_s = 0 past the rank: no coupling, t = 0
+    // there), bitwise the same arithmetic on the live rows
+    if (rank <= 16 || rank > 32) return WCE_EINVAL;
+    const int64_t units = a.split ? a.n * a.nblk : a.n;
+    const dim3 gq((unsigned)((units + 15) / 16)), bq(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20>), gq, bq, 0, s, st, a);
+    else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24>), gq, bq, 0, s, st, a);
+    else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28>), gq, bq, 0, s, st, a);
+    else hipLaunchKernelGGL((mmse_lr_quad2_kernel<32>), gq, bq, 0, s, st, a);
+    return hipGetLastError() == hipSuccess ? WCE_OK : WCE_EHIP;
+}
+
+}  // namespace wce

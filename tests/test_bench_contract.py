@@ -176,7 +176,8 @@ def test_multirank_rehearsal_self_explaining():
     assert dc["all_ranks_agree"] is True and dc["group_size"] == 2 == dc["world_size_env"]
     c4 = reh["legs"]["config4"] if "legs" in reh else reh["config4"]   # round 5+: the compact line
     assert c4["n_gpus"] == 2 and c4["scaling"] == "strong"
-    assert abs(c4["frames_per_s_per_gpu"] * 2 - c4["frames_per_s"]) / c4["frames_per_s"] < 1e-9
+    # round 6+: leg summaries carry 5 significant digits (full values in the extras file)
+    assert abs(c4["frames_per_s_per_gpu"] * 2 - c4["frames_per_s"]) / c4["frames_per_s"] < 1e-4
 
 
 def test_launcherless_rehearsal_spans_two_ranks():

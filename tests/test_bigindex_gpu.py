@@ -51,7 +51,7 @@ def _run(wce, ctx, fr, mask, f32=False):
     ("COV8", "PS_MMSE", False, "C"),                 # 8-tap PDP: one frame per lane, mmse_lr_lane_staged_kernel<8, 1, true>
     ("COV8", "PS_MMSE", False, "MATLAB"),            # the same, split per-block solves + block mean
     ("COV12", "PS_MMSE", False, "C"),                # 12 taps: 16 lanes per frame, mmse_lr_quad_kernel<12, true>
-    ("COV24", "PS_MMSE", False, "C"),                # 24 taps: one frame per wave, mmse_lr_kernel<3, true>
+    ("COV24", "PS_MMSE", False, "C"),                # 24 taps: 16 lanes, two rows each, mmse_lr_quad2_kernel<24>
     ("COV24", "PS_MMSE", False, "MATLAB"),           # the same, split per-block solves
     ("REF", "ALL", True, "C"),                       # ref_ls_elem_kernel, fp32 LS / eq
     ("TEXTBOOK", "PS_MMSE|FRAME_COV", False, "C"),   # per-frame covariance: factor matvecs + solve
@@ -73,7 +73,7 @@ def test_64bit_frame_indexing(layouts, mode, mask, f32, sem):
         assert ctx.cov_info()[:2] == (L, True)
         units = B * (4 if sem == "MATLAB" else 1)
         assert ctx.lr_kernel(units) == {8: "mmse_lr_lane_staged_kernel<8, 1, true>", 12: "mmse_lr_quad_kernel<12, true>",
-                                        24: "mmse_lr_kernel<3, true>"}[L]
+                                        24: "mmse_lr_quad2_kernel<24>"}[L]
     else:
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], getattr(wce, "MMSE_" + mode))
     m = 0

@@ -82,10 +82,11 @@ def c_ld(oracle, R):
     return F @ oracle._ld(R) @ F.conj().T
 
 
-# (taps, decay, per-frame kernel): quad (rank 16), Gram wave kernel (24, K0 = 3;
-# a full-rank spectrum wider than 1e5, K0 = 0), dense solve + H = C W
-PROFILES = [(16, 0.5, "mmse_lr_quad_kernel<16, true>"), (24, 0.3, "mmse_lr_kernel<3, true>"), (53, 0.5, "mmse_lr_kernel<0, true>"),
-            (53, 0.12, "")]
+# (taps, decay, per-frame kernel): quad (rank 16), two rows per lane (rank 24,
+# round 6), Gram wave kernel (a full-rank spectrum wider than 1e5, K0 = 0),
+# dense solve + H = C W
+PROFILES = [(16, 0.5, "mmse_lr_quad_kernel<16, true>"), (24, 0.3, "mmse_lr_quad2_kernel<24>"),
+            (53, 0.5, "mmse_lr_kernel<0, true>"), (53, 0.12, "")]
 
 
 @pytest.mark.parametrize("L,decay,kern", PROFILES)

@@ -41,6 +41,19 @@ def product_gram(wce, fn):
         assert lib.wce_debug_set_variant(3, 0) == 0
 
 
+def wave_kernel(wce, fn, on=True):
+    """Ranks 17..32 with taps 0..r-1 run mmse_lr_quad2_kernel by default
+    (round 6); variant 3 = 1 keeps them on the wave kernel tested here."""
+    if not on:
+        return fn()
+    lib = wce.load()
+    assert lib.wce_debug_set_variant(3, 1) == 0
+    try:
+        return fn()
+    finally:
+        assert lib.wce_debug_set_variant(3, 0) == 0
+
+
 # (taps, decay, K0): the wave kernel's ranks (> 16) and a spectrum wider than 1e5 at full rank
 PROFILES = [(53, 0.5, 0), (46, 0.1, 0), (40, 0.1, 1), (33, 0.2, 2), (24, 0.3, 3), (17, 0.4, 4)]
 
@@ -51,12 +64,13 @@ def test_taps_vs_long_double_and_product_gram(gpu_wce, golden, oracle, L, decay,
     inp = golden["inputs"]
     R = pdp_rhh(L, decay)
     ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
-    assert ctx.lr_kernel(1 << 20) == f"mmse_lr_kernel<{k0}, true>"
+    wv = L <= 32
+    assert wave_kernel(wce, lambda: ctx.lr_kernel(1 << 20), wv) == f"mmse_lr_kernel<{k0}, true>"
     assert product_gram(wce, lambda: ctx.lr_kernel(1 << 20)) == f"mmse_lr_kernel<{k0}>"
     B = 1025
     tx, rx = synth(ctx, wce, B, seed=0x7A + L)
     tx[0], rx[0] = inp["tx_symb"], inp["rx_symb"]
-    got = ctx.estimate_host(tx, rx, mask=wce.PS_MMSE)["ps_mmse"]
+    got = wave_kernel(wce, lambda: ctx.estimate_host(tx, rx, mask=wce.PS_MMSE)["ps_mmse"], wv)
     prod = product_gram(wce, lambda: ctx.estimate_host(tx, rx, mask=wce.PS_MMSE)["ps_mmse"])
     exp = solve_ld(oracle, c_ld(oracle, R), tx[:, 0], rx[:, 0], inp["ow2"])
     err, errp, d = normrel(got, exp), normrel(prod, exp), normrel(got, prod)
