@@ -453,17 +453,8 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
 // Arithmetic and summation order are mmse_ref_flat_kernel's: outputs
 // bit-identical.  Measured (1,048,576 frames, profiles/r06_ab_ref_elem.txt):
 // 381 -> 337 us against the capped chunks; 2 or 4 elements per lane (462, 440),
-// plain stores (371), 128 / 512 / 1,024-thread blocks (375 / 340 / 365) lose.
-// XCD: blocks dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
-// dispatch) are remapped so that each XCD walks one contiguous run of the
-// elements -- a frame whose pilots two neighbouring blocks both read then sits
-// in one XCD's L2 instead of being fetched by two (bijective for any grid).
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
-{
-    const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-template <bool XCD>
+// plain stores (371), 128 / 512 / 1,024-thread blocks (375 / 340 / 365) lose, and
+// an XCD-aware block remap (each XCD one contiguous run) changes nothing (342).
 __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
                                                             uint32_t nfr)
 {
@@ -471,8 +462,7 @@ __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restr
     const int lane = threadIdx.x & 63;
     const bool shared = a.cs == 0;
     const uint32_t E = nfr * (uint32_t)NSC;
-    const uint32_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t e0 = blk * 256u + (threadIdx.x & ~63u);     // the wave's first element
+    const uint32_t e0 = blockIdx.x * 256u + (threadIdx.x & ~63u);     // the wave's first element
     const uint32_t ff = min(e0 / NSC, nfr - 1);
     const int pj = lane & 3;
     const int pil = pj == 0 ? WCE_P0 : pj == 1 ? WCE_P1 : pj == 2 ? WCE_P2 : WCE_P3;
@@ -3044,10 +3034,9 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
             // capped grid (flat): 65,536 frames 20.3 / 25.0 us, 131,072 43.1 / 49.2,
             // 262,144 102.7 / 89.3, 1,048,576 380.9 / 338.7 (flat / elem)
             const int v = variant(WCE_VARIANT_REF);
-            if (v == 3 || v == 4 || (v == 0 && nf > REF_ELEM_FROM)) {
-                const dim3 g((unsigned)((nf * NSC + 255) / 256));
-                if (v == 4) hipLaunchKernelGGL(mmse_ref_elem_kernel<true>, g, dim3(256), 0, s, st, a, f0, (uint32_t)nf);
-                else hipLaunchKernelGGL(mmse_ref_elem_kernel<false>, g, dim3(256), 0, s, st, a, f0, (uint32_t)nf);
+            if (v == 3 || (v == 0 && nf > REF_ELEM_FROM)) {
+                hipLaunchKernelGGL(mmse_ref_elem_kernel, dim3((unsigned)((nf * NSC + 255) / 256)), dim3(256), 0, s, st,
+                                   a, f0, (uint32_t)nf);
                 continue;
             }
             const int64_t chunks = (nf * NSC + FLAT_CHUNK - 1) / FLAT_CHUNK;
@@ -3074,7 +3063,7 @@ static bool lr_contig(int taps) { return (taps & 2) && variant(WCE_VARIANT_LR) !
 static LrForm lr_form(int rank, int64_t units, int taps)
 {
     int lv = variant(WCE_VARIANT_LR);
-    if (lv == 5) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), not the kernel form
+    if (lv == 5 || lv == 6) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), 6 only quad2's broadcasts
     if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
         // the LDS-staged form at every size by default (LR_STAGE_FROM = 0);
         // the direct form runs only as variant 2, the gate's independent check
@@ -3194,7 +3183,8 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
 #undef WCE_LRQ
         return hip_status(hipGetLastError());
     }
-    if (form == LrForm::Quad2) return launch_lr_quad2(st, rank, a, stream);   // wce_lr_quad2.hip
+    if (form == LrForm::Quad2)   // wce_lr_quad2.hip; variant 6: the Cholesky's broadcasts as separate movs (A/B)
+        return launch_lr_quad2(st, rank, a, stream, variant(WCE_VARIANT_LR) != 6);
     const dim3 g((unsigned)waves), b(64);
     const bool tp = lr_taps(taps);
 #define WCE_LRW(K)                                                                               \

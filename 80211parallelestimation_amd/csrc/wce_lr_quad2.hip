@@ -24,7 +24,57 @@ namespace wce {
 // Same algebra as mmse_lr_quad_kernel / mmse_lr_kernel, summed in another
 // order (~1e-15).
 // ---------------------------------------------------------------------
-template <int R, int C>
+// acc -= l conj(R[lane N of the 16-lane row]): gfx950's DPP64 row_newbcast on
+// v_fmac_f64 hands the broadcast operand straight to the FMA (4 VALU instead
+// of 2 v_mov_b64_dpp + 4 FMAs), the products and their order those of
+// cmsub_conj.  R must not have been written by a VALU instruction in the 2
+// wait states before (dpp_ready below).
+template <int N>
+__device__ __forceinline__ void cmsub_dpp(double2 &acc, double2 l, double2 R)
+{
+    asm("v_fmac_f64_dpp %[ax], -%[cx], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ax], -%[cy], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], -%[cx], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], %[cy], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf"
+        : [ax] "+v"(acc.x), [ay] "+v"(acc.y)
+        : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(R.x), [cy] "v"(R.y), [n] "i"(N));
+}
+__device__ __forceinline__ void cmsub_dpp_n(int n, double2 &acc, double2 l, double2 R)   // n constant after unrolling
+{
+    switch (n) {
+    case 0: cmsub_dpp<0>(acc, l, R); break;
+    case 1: cmsub_dpp<1>(acc, l, R); break;
+    case 2: cmsub_dpp<2>(acc, l, R); break;
+    case 3: cmsub_dpp<3>(acc, l, R); break;
+    case 4: cmsub_dpp<4>(acc, l, R); break;
+    case 5: cmsub_dpp<5>(acc, l, R); break;
+    case 6: cmsub_dpp<6>(acc, l, R); break;
+    case 7: cmsub_dpp<7>(acc, l, R); break;
+    case 8: cmsub_dpp<8>(acc, l, R); break;
+    case 9: cmsub_dpp<9>(acc, l, R); break;
+    case 10: cmsub_dpp<10>(acc, l, R); break;
+    case 11: cmsub_dpp<11>(acc, l, R); break;
+    case 12: cmsub_dpp<12>(acc, l, R); break;
+    case 13: cmsub_dpp<13>(acc, l, R); break;
+    case 14: cmsub_dpp<14>(acc, l, R); break;
+    default: cmsub_dpp<15>(acc, l, R); break;
+    }
+}
+// the 2 wait states between the VALU write of a DPP source and its first DPP
+// read, tied to the values so nothing moves across it
+__device__ __forceinline__ void dpp_ready(double2 &a, double2 &b)
+{
+    asm volatile("s_nop 1" : "+v"(a.x), "+v"(a.y), "+v"(b.x), "+v"(b.y));
+}
+// acc -= l conj(L[j][C]) with L[j][C] from lane (j mod 16) of column register R
+template <bool FD>
+__device__ __forceinline__ void chol_upd(int n, double2 &acc, double2 l, double2 R)
+{
+    if constexpr (FD) cmsub_dpp_n(n, acc, l, R);
+    else cmsub_conj(acc, l, row_bcast_n(R, n));
+}
+
+template <int R, int C, bool FD>
 __device__ __forceinline__ void lrq2_chol(double2 (&Ar)[16], double2 (&Br)[R], double &lda, double &ldb, int i)
 {
     if constexpr (C < R) {
@@ -33,32 +83,28 @@ __device__ __forceinline__ void lrq2_chol(double2 (&Ar)[16], double2 (&Br)[R], d
             Ar[C] = cscale(Ar[C], rs);                        // L[i][C], L[i + 16][C]
             Br[C] = cscale(Br[C], rs);
             lda = i == C ? rs : lda;
+            if constexpr (FD) dpp_ready(Ar[C], Br[C]);
 #pragma unroll
             for (int j = C + 1; j < 16; ++j) {                // rows i >= j of both sets
-                const double2 lj = row_bcast_n(Ar[C], j);
-                cmsub_conj(Ar[j], Ar[C], lj);
-                cmsub_conj(Br[j], Br[C], lj);
+                chol_upd<FD>(j, Ar[j], Ar[C], Ar[C]);
+                chol_upd<FD>(j, Br[j], Br[C], Ar[C]);
             }
 #pragma unroll
-            for (int j = 16; j < R; ++j) {                    // rows i + 16 >= j only
-                const double2 lj = row_bcast_n(Br[C], j - 16);
-                cmsub_conj(Br[j], Br[C], lj);
-            }
+            for (int j = 16; j < R; ++j)                      // rows i + 16 >= j only
+                chol_upd<FD>(j - 16, Br[j], Br[C], Br[C]);
         } else {
             const double rs = rsq_nr(row_bcast<C - 16>(Br[C]).x);
             Br[C] = cscale(Br[C], rs);
             ldb = i == C - 16 ? rs : ldb;
+            if constexpr (FD) dpp_ready(Br[C], Br[C]);
 #pragma unroll
-            for (int j = C + 1; j < R; ++j) {
-                const double2 lj = row_bcast_n(Br[C], j - 16);
-                cmsub_conj(Br[j], Br[C], lj);
-            }
+            for (int j = C + 1; j < R; ++j) chol_upd<FD>(j - 16, Br[j], Br[C], Br[C]);
         }
-        lrq2_chol<R, C + 1>(Ar, Br, lda, ldb, i);
+        lrq2_chol<R, C + 1, FD>(Ar, Br, lda, ldb, i);
     }
 }
 
-template <int R>
+template <int R, bool FD = true>
 __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
 {
     static_assert(R > 16 && R <= 32, "two rows per lane");
@@ -121,21 +167,25 @@ __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restr
     sQ[rw][i + 16] = qb;
     wave_lds_sync();
     double2 Ar[16], Br[R];   // a s_r s_j Q(r - j) + b [r == j]  (Q(-d) = conj(Q(d)))
+    // one LDS read per element: |r - j| indexes Q, the sign picks the conjugate
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const double2 qd = j <= i ? sQ[rw][(i - j) & 31] : cconj(sQ[rw][(j - i) & 31]);
+        const int d = i - j;
+        double2 qd = sQ[rw][d >= 0 ? d : -d];
+        qd.y = d >= 0 ? qd.y : -qd.y;
         Ar[j] = cscale(qd, ac * sia * st->col_s[j]);
         Ar[j].x += i == j ? bc : 0.0;
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int d = i + 16 - j;
-        const double2 qd = d >= 0 ? sQ[rw][d & 31] : cconj(sQ[rw][(-d) & 31]);
+        double2 qd = sQ[rw][d >= 0 ? d : -d];
+        qd.y = d >= 0 ? qd.y : -qd.y;
         Br[j] = cscale(qd, ac * sib * st->col_s[j]);   // zero on lanes without a second row
         Br[j].x += (rowb && i + 16 == j) ? bc : 0.0;
     }
     double lda = 1.0, ldb = 1.0;
-    lrq2_chol<R, 0>(Ar, Br, lda, ldb, i);
+    lrq2_chol<R, 0, FD>(Ar, Br, lda, ldb, i);
     // z = L^-1 beta (beta_r = s_r sum_k v_k conj(E[k r])): lane i keeps z_i, z_{i+16}
     double2 za = cscale(ba, sia), zb = cscale(bb, sib);
 #pragma unroll
@@ -236,7 +286,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restr
         if (i + 16 * m < NSC) st2(W, i + 16 * m, y[m]);
 }
 
-int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream)
+int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream, bool fused_dpp)
 {
     // instantiated at 20, 24, 28, 32 rows: a rank r below runs the next size
     // up with rows r.. as b I (col_s = 0 past the rank: no coupling, t = 0
@@ -245,7 +295,9 @@ int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream)
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const dim3 gq((unsigned)((units + 15) / 16)), bq(256);
     hipStream_t s = (hipStream_t)stream;
-    if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20>), gq, bq, 0, s, st, a);
+    if (!fused_dpp && rank > 20 && rank <= 24)   // A/B: the broadcasts as separate v_mov_b64_dpp (round 6 first form)
+        hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, false>), gq, bq, 0, s, st, a);
+    else if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20>), gq, bq, 0, s, st, a);
     else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24>), gq, bq, 0, s, st, a);
     else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28>), gq, bq, 0, s, st, a);
     else hipLaunchKernelGGL((mmse_lr_quad2_kernel<32>), gq, bq, 0, s, st, a);

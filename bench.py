@@ -1318,7 +1318,7 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
             f()
         t = time_events(wce, stream, f, reps)
         lane = lr and 1 <= r <= 8
-        quad = lr and 9 <= r <= 16
+        quad = lr and 9 <= r <= 32      # mmse_lr_quad_kernel (9..16), mmse_lr_quad2_kernel (17..32, taps 0..r-1)
         leg = {"rank": r, "path": "low-rank" if lr else "dense",
                "kernel": c.lr_kernel(B) if lr else "mmse_solve_kernel<false> + H = C W",
                "ms_per_step": t, "frames_per_s": B / (t * 1e-3),
@@ -1352,14 +1352,18 @@ def bench_cov_lowrank(wce, make_ctx, stream, tx, rx, B, reps, big=1 << 20):
             # s2): r x r Cholesky + triangular solves + the Q / D / read-out DFTs (20 N^2)
             fl = flop_lr_taps(r)
             ach = fl * B / (t * 1e-3) / 1e12
-            kw, wsrc = pmc_leg("lowrank%d" % L, B, N * 16.0 * B, waves=B)
+            kn = c.lr_kernel(B)
+            kw, wsrc = pmc_leg("lowrank%d" % L, B, N * 16.0 * B,
+                               waves=4 * ((B + 15) // 16) if "quad" in kn else B)   # quad forms: 16 units per 4-wave group
             leg["roofline"] = {"bound": "valu-f64", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / PEAK_FP64_TFLOPS, "flops_per_frame": fl,
                                "traffic": hbm_bytes(kw) if kw else None, "pmc_source": wsrc}
             if kw:
-                leg["pmc_per_wave"] = {k: kw[k] / B for k in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_LDS",
-                                                              "SQ_WAIT_INST_LDS", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES")
-                                       if k in kw}
+                # per frame (= per wave for the wave kernel; a quad-form wave holds 4 frames)
+                leg["pmc_per_frame"] = {k: kw[k] / B for k in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_LDS",
+                                                               "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT",
+                                                               "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES")
+                                        if k in kw}
         if L in (16, 53):
             # constant-modulus frames (the synthetic BPSK: +-A, DC null) on the shared
             # operator K = (a C P + b I)^-1 C (wce_ctx_set_modulus): two f64-MFMA

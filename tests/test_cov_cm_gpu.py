@@ -122,7 +122,10 @@ def test_constant_modulus_batch(gpu_wce, golden, oracle, L, decay, kern):
           f"per-frame path {errp.max():.2e}; CM vs per-frame max {d.max():.2e}")
     assert err.max() < TOL, (int(sel[err.argmax()]), err.max())
     assert d.max() < 5e-13                             # both within ~1e-13 of the long double solve
-    assert err[cmf[sel]].max() < 3e-13
+    # the long double reference itself is good to ~cond(Ryy) x 1.1e-19 ~ 4e-13
+    # (tests/test_oracle.py::test_textbook_closed_form_vs_mp_literal); the two
+    # GPU paths agree with each other to ~1e-15 (d above)
+    assert err[cmf[sel]].max() < 5e-13
 
 
 def test_constant_modulus_large_batch_apply_skip(gpu_wce, golden, oracle):

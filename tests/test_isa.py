@@ -1,7 +1,8 @@
 """Static checks on the compiled gfx950 code (CPU: hipcc cross-compiles).
 
 The rank-1 solve issues DPP64 FMAs from inline asm (wce_kernels.hip
-cmsub_bc); the compiler's hazard recognizer does not look inside them, so
+cmsub_bc), and so does the rank 17..32 Cholesky (wce_lr_quad2.hip cmsub_dpp,
+round 6); the compiler's hazard recognizer does not look inside them, so
 the emitted code is checked for a VALU write of a DPP source VGPR within the
 2 wait states the hardware needs (tools/isa_check.py)."""
 import os

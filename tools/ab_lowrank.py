@@ -42,9 +42,10 @@ def main():
         R[np.arange(L), np.arange(L)] = p / p.sum() * 1.1e-4     # bench.py bench_cov_lowrank's profile
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
         run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
-        names, times, outs = {}, {0: [], 1: []}, {}
+        vs = (0, 6, 1) if 20 < L <= 24 else (0, 1)     # 6: quad2 with its Cholesky broadcasts as separate movs
+        names, times, outs = {}, {v: [] for v in vs}, {}
         for r in range(args.rounds):
-            for v in (0, 1):
+            for v in vs:
                 assert lib.wce_debug_set_variant(3, v) == 0
                 names[v] = ctx.lr_kernel(n)
                 for _ in range(3):
@@ -54,10 +55,12 @@ def main():
                     outs[v] = H.numpy()
         assert lib.wce_debug_set_variant(3, 0) == 0
         d = np.max(np.abs(outs[0] - outs[1]), axis=1) / np.maximum(np.max(np.abs(outs[1]), axis=1), 1e-300)
+        if 6 in outs:
+            print(f"L={L} fused-DPP Cholesky bit-identical to the separate movs: {bool(np.array_equal(outs[0], outs[6]))}")
         fl = bench.flop_lr_taps(L)
-        for v in (0, 1):
+        for v in vs:
             t = float(np.median(times[v]))
-            print(f"L={L} {names[v]:28s} median {t * 1e3:7.1f} us  {fl * n / (t * 1e-3) / 1e12:5.1f} TF "
+            print(f"L={L} v{v} {names[v]:28s} median {t * 1e3:7.1f} us  {fl * n / (t * 1e-3) / 1e12:5.1f} TF "
                   f"({100 * fl * n / (t * 1e-3) / 1e12 / bench.PEAK_FP64_TFLOPS:4.1f}% of FP64 peak)  "
                   f"({', '.join(f'{x * 1e3:.0f}' for x in times[v])})")
         print(f"L={L} outputs: max norm-rel diff {d.max():.2e}, finite {bool(np.isfinite(outs[0]).all())}")

@@ -19,6 +19,8 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "80211parallelestimation_amd", "csrc", "wce_kernels.hip")
+# every translation unit with DPP64 FMAs from inline asm (round 6: the quad2 Cholesky)
+SRCS = (SRC, os.path.join(REPO, "80211parallelestimation_amd", "csrc", "wce_lr_quad2.hip"))
 REG = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)\b")
 
 
@@ -97,15 +99,18 @@ def dpp_hazards(text: str):
     return out
 
 
-def compile_asm(flags=()):
-    fd, path = tempfile.mkstemp(suffix=".s")
-    os.close(fd)
-    cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(REPO, "include"),
-           "--cuda-device-only", "-S", SRC, "-o", path, *flags]
-    subprocess.run(cmd, check=True, capture_output=True)
-    text = open(path).read()
-    os.unlink(path)
-    return text
+def compile_asm(flags=(), srcs=SRCS):
+    """gfx950 assembly of the kernel sources, concatenated"""
+    out = []
+    for src in srcs:
+        fd, path = tempfile.mkstemp(suffix=".s")
+        os.close(fd)
+        cmd = ["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(REPO, "include"),
+               "--cuda-device-only", "-S", src, "-o", path, *flags]
+        subprocess.run(cmd, check=True, capture_output=True)
+        out.append(open(path).read())
+        os.unlink(path)
+    return "\n".join(out)
 
 
 def kernel_bodies(text: str):

@@ -16,7 +16,8 @@ legs (bench.py field -> kernel, frames per launch):
   config5_ref_fc(_factors)       ref_ls_elem_kernel<true> / ref_fc_kernel<false>  1,048,576 (the same | FRAME_COV)
   frame_cov_ref frame_cov.ref    ref_fc_kernel<false>             65,536 (REF PS_MMSE | FRAME_COV: one launch)
   lowrank<L> cov_lowrank.L<L>    mmse_lr_lane_staged_kernel<L, 1, true> (L <= 8) / mmse_lr_quad_kernel<L, true> (L <= 16) /
-                                 mmse_lr_kernel<K0, true> (tap-domain Gram)  65,536 (COV, L-tap PDP: rank L)
+                                 mmse_lr_quad2_kernel<24> (L = 24, round 6) / mmse_lr_kernel<0, true> (53, tap-domain Gram)
+                                 65,536 (COV, L-tap PDP: rank L)
   lowrank8_1m cov_lowrank.L8.frames_1048576  mmse_lr_lane_staged_kernel<8, 2, true>  1,048,576 (block 0 only)
 """
 import argparse
@@ -49,7 +50,7 @@ LEGS = {
     "lowrank4": ("mmse_lr_lane_staged_kernel<4, 1, true>", 65536),     # Toeplitz Gram (taps 0..3, round 4)
     "lowrank8": ("mmse_lr_lane_staged_kernel<8, 1, true>", 65536),
     "lowrank16": ("mmse_lr_quad_kernel<16, true>", 65536),
-    "lowrank24": ("mmse_lr_kernel<3, true>", 65536),     # tap-domain Gram (diagonal Rhh, round 4)
+    "lowrank24": ("mmse_lr_quad2_kernel<24>", 65536),    # round 6: two Gram rows per lane (taps 0..23)
     "lowrank53": ("mmse_lr_kernel<0, true>", 65536),     # the same at full rank, spectrum 2e11
     "lowrank8_1m": ("mmse_lr_lane_staged_kernel<8, 2, true>", 1 << 20),   # block 0 only, frame_stride 53
     "cm16": ("cm_real_kernel", 65536),         # constant-modulus operator path, 16-tap PDP (round 4)
