@@ -225,7 +225,7 @@ int launch_synth(const State *st, const SynthArgs &a, void *stream);
 // the Gram system embedded at block row k0 (State::cov_k0)
 // (rank = State::cov_rank: ranks 1..LRL_RMAX run one frame per lane instead)
 // ranks 17..32, taps 0..r-1: 16 lanes per unit, two rows each (wce_lr_quad2.hip)
-int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream, bool fused_dpp = true);
+int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream, int form = 0);
 int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs &a, void *stream);
 // the kernel launch_mmse_lr runs for `units` (frame, block) units (wce_debug_lr_kernel)
 const char *lr_kernel_name(int k0, int rank, int taps, int64_t units);

@@ -3063,7 +3063,7 @@ static bool lr_contig(int taps) { return (taps & 2) && variant(WCE_VARIANT_LR) !
 static LrForm lr_form(int rank, int64_t units, int taps)
 {
     int lv = variant(WCE_VARIANT_LR);
-    if (lv == 5 || lv == 6) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), 6 only quad2's broadcasts
+    if (lv >= 5 && lv <= 7) lv = 0;   // 5 changes only the Gram form (lr_taps / lr_contig), 6 / 7 only quad2's build
     if (rank >= 1 && rank <= LRL_RMAX && lv != 1) {
         // the LDS-staged form at every size by default (LR_STAGE_FROM = 0);
         // the direct form runs only as variant 2, the gate's independent check
@@ -3183,8 +3183,10 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
 #undef WCE_LRQ
         return hip_status(hipGetLastError());
     }
-    if (form == LrForm::Quad2)   // wce_lr_quad2.hip; variant 6: the Cholesky's broadcasts as separate movs (A/B)
-        return launch_lr_quad2(st, rank, a, stream, variant(WCE_VARIANT_LR) != 6);
+    if (form == LrForm::Quad2) {   // wce_lr_quad2.hip; A/B: variant 6 the Cholesky's broadcasts as separate movs,
+        const int lv = variant(WCE_VARIANT_LR);   // 7 every size held to 2 waves per SIMD
+        return launch_lr_quad2(st, rank, a, stream, lv == 6 ? 1 : lv == 7 ? 2 : 0);
+    }
     const dim3 g((unsigned)waves), b(64);
     const bool tp = lr_taps(taps);
 #define WCE_LRW(K)                                                                               \

@@ -21,6 +21,7 @@ namespace wce {
 //   Cholesky pivot C < 16 updates Ar[j] (j < 16) and Br[j]; C >= 16 Br only
 //   z = L^-1 beta by broadcasts, t = L^-H z by 16-lane DPP sums
 //   complex x: the quad kernel's correction term; H_k = sum_j s_j t_j E[k j]
+//            over the pairs (k, 53 - k), the DFTs' broadcasts fused into DPP64 FMAs
 // Same algebra as mmse_lr_quad_kernel / mmse_lr_kernel, summed in another
 // order (~1e-15).
 // ---------------------------------------------------------------------
@@ -66,6 +67,39 @@ __device__ __forceinline__ void dpp_ready(double2 &a, double2 &b)
 {
     asm volatile("s_nop 1" : "+v"(a.x), "+v"(a.y), "+v"(b.x), "+v"(b.y));
 }
+// A += c[lane N] Re e, B += c[lane N] Im e (the read-out pairs), c as the DPP64
+// row_newbcast operand of the four FMAs; c ready as for cmsub_dpp
+template <int N>
+__device__ __forceinline__ void cfma_dpp(double2 &A, double2 &B, double2 c, double2 e)
+{
+    asm("v_fmac_f64_dpp %[ax], %[cx], %[er] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[ay], %[cy], %[er] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[bx], %[cx], %[ei] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %[by], %[cy], %[ei] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf"
+        : [ax] "+v"(A.x), [ay] "+v"(A.y), [bx] "+v"(B.x), [by] "+v"(B.y)
+        : [cx] "v"(c.x), [cy] "v"(c.y), [er] "v"(e.x), [ei] "v"(e.y), [n] "i"(N));
+}
+__device__ __forceinline__ void cfma_dpp_n(int n, double2 &A, double2 &B, double2 c, double2 e)
+{
+    switch (n) {
+    case 0: cfma_dpp<0>(A, B, c, e); break;
+    case 1: cfma_dpp<1>(A, B, c, e); break;
+    case 2: cfma_dpp<2>(A, B, c, e); break;
+    case 3: cfma_dpp<3>(A, B, c, e); break;
+    case 4: cfma_dpp<4>(A, B, c, e); break;
+    case 5: cfma_dpp<5>(A, B, c, e); break;
+    case 6: cfma_dpp<6>(A, B, c, e); break;
+    case 7: cfma_dpp<7>(A, B, c, e); break;
+    case 8: cfma_dpp<8>(A, B, c, e); break;
+    case 9: cfma_dpp<9>(A, B, c, e); break;
+    case 10: cfma_dpp<10>(A, B, c, e); break;
+    case 11: cfma_dpp<11>(A, B, c, e); break;
+    case 12: cfma_dpp<12>(A, B, c, e); break;
+    case 13: cfma_dpp<13>(A, B, c, e); break;
+    case 14: cfma_dpp<14>(A, B, c, e); break;
+    default: cfma_dpp<15>(A, B, c, e); break;
+    }
+}
 // acc -= l conj(L[j][C]) with L[j][C] from lane (j mod 16) of column register R
 template <bool FD>
 __device__ __forceinline__ void chol_upd(int n, double2 &acc, double2 l, double2 R)
@@ -104,8 +138,30 @@ __device__ __forceinline__ void lrq2_chol(double2 (&Ar)[16], double2 (&Br)[R], d
     }
 }
 
-template <int R, bool FD = true>
-__global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
+// the read-out's column j (compile-time, so each DPP lane select is an
+// immediate): c_j from lane j of ca (j < 16) or lane j - 16 of cb
+template <int R, int J>
+__device__ __forceinline__ void lrq2_readout(const double2 *sE, double2 ca, double2 cb, uint32_t &o1, uint32_t &o2,
+                                             uint32_t s1, uint32_t w1, uint32_t s2, uint32_t w2, double2 &A1,
+                                             double2 &B1, double2 &A2, double2 &B2)
+{
+    if constexpr (J < R) {
+        const double2 e1 = ld_e(sE, o1), e2 = ld_e(sE, o2);
+        if constexpr (J < 16) {
+            cfma_dpp<J>(A1, B1, ca, e1);
+            cfma_dpp<J>(A2, B2, ca, e2);
+        } else {
+            cfma_dpp<J - 16>(A1, B1, cb, e1);
+            cfma_dpp<J - 16>(A2, B2, cb, e2);
+        }
+        o1 = dft_step(o1, s1, w1);
+        o2 = dft_step(o2, s2, w2);
+        lrq2_readout<R, J + 1>(sE, ca, cb, o1, o2, s1, w1, s2, w2, A1, B1, A2, B2);
+    }
+}
+
+template <int R, bool FD = true, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
 {
     static_assert(R > 16 && R <= 32, "two rows per lane");
     constexpr int R2 = R - 16;
@@ -117,6 +173,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restr
     __shared__ double2 sQ[16][32];    // one unit's Q(0..31)
     __shared__ double2 sV[16][56];    // the unit's frame: conj(x_k) rx_k ...
     __shared__ double sW[16][56];     // ... and |x_k|^2
+    __shared__ double2 sPA[16][32], sPB[16][32], sRP[16][32];   // the unit's pair tables (k = 1..26)
     if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
     __syncthreads();
     if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows
@@ -140,24 +197,39 @@ __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restr
         }
     }
     wave_lds_sync();
+    // pair tables over (k, 53 - k), k = 1..26: conj(E[(53 - k) d]) = E[k d], so
+    //   p_k conj(E) + p_{53-k} E = (p_k + p_{53-k}) Re E - i (p_k - p_{53-k}) Im E
+    //   v_k conj(E) + v_{53-k} E = (v_k + v_{53-k}) Re E - i (v_k - v_{53-k}) Im E
+    // -- one gather and half the FMAs per pair (the wave kernel's dft_pairs)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int k = i + 1 + 16 * h;
+        if (k <= NSC / 2) {
+            const double2 u = sV[rw][k], w = sV[rw][NSC - k];
+            const double pu = sW[rw][k], pw = sW[rw][NSC - k];
+            sPA[rw][k] = cadd(u, w);
+            sPB[rw][k] = csub(u, w);
+            sRP[rw][k] = make_double2(pu + pw, pu - pw);
+        }
+    }
+    wave_lds_sync();
     // Q(d) = sum_k p_k conj(E[k d]) and sum_k v_k conj(E[k d]) at d = i and d = i + 16
-    double2 qa = make_double2(0.0, 0.0), qb = qa, ba = qa, bb = qa;
+    double2 qa = make_double2(sW[rw][0], 0.0), qb = qa, ba = sV[rw][0], bb = ba;   // the k = 0 terms
     {
         const uint32_t sa = 16u * (uint32_t)i, swa = sa - 16u * NSC;
         const uint32_t sb = 16u * (uint32_t)(i + 16), swb = sb - 16u * NSC;
-        uint32_t oa = 0, ob = 0;
-#pragma unroll 4
-        for (int k = 0; k < NSC; ++k) {
-            const double2 ea = ld_e(sE, oa), eb = ld_e(sE, ob), v = sV[rw][k];
-            const double w = sW[rw][k];
-            qa.x = fma(w, ea.x, qa.x);
-            qa.y = fma(-w, ea.y, qa.y);
-            qb.x = fma(w, eb.x, qb.x);
-            qb.y = fma(-w, eb.y, qb.y);
-            ba.x = fma(v.x, ea.x, fma(v.y, ea.y, ba.x));
-            ba.y = fma(v.y, ea.x, fma(-v.x, ea.y, ba.y));
-            bb.x = fma(v.x, eb.x, fma(v.y, eb.y, bb.x));
-            bb.y = fma(v.y, eb.x, fma(-v.x, eb.y, bb.y));
+        uint32_t oa = sa, ob = sb;   // k = 1
+#pragma unroll 2
+        for (int k = 1; k <= NSC / 2; ++k) {
+            const double2 ea = ld_e(sE, oa), eb = ld_e(sE, ob), pa = sPA[rw][k], pb = sPB[rw][k], pp = sRP[rw][k];
+            qa.x = fma(pp.x, ea.x, qa.x);
+            qa.y = fma(-pp.y, ea.y, qa.y);
+            qb.x = fma(pp.x, eb.x, qb.x);
+            qb.y = fma(-pp.y, eb.y, qb.y);
+            ba.x = fma(pa.x, ea.x, fma(pb.y, ea.y, ba.x));
+            ba.y = fma(pa.y, ea.x, fma(-pb.x, ea.y, ba.y));
+            bb.x = fma(pa.x, eb.x, fma(pb.y, eb.y, bb.x));
+            bb.y = fma(pa.y, eb.x, fma(-pb.x, eb.y, bb.y));
             oa = dft_step(oa, sa, swa);
             ob = dft_step(ob, sb, swb);
         }
@@ -245,6 +317,9 @@ __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restr
             vk[m] = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
         }
         const double rb = 1.0 / bc;
+        // reload UT below instead of keeping the first loop's 4R values live (a
+        // memory clobber: no load is reused across it)
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             double2 cp = make_double2(0.0, 0.0);
@@ -258,46 +333,49 @@ __global__ __launch_bounds__(256) void mmse_lr_quad2_kernel(const State *__restr
             if (j >= 16 && i == j - 16) tb = cadd(tb, cscale(cj, rb));
         }
     }
-    // H_k = sum_j s_j t_j E[k j] at k = i + 16 m: E from LDS by the index recurrence over j
-    double2 y[4];
-    uint32_t eo[4], es[4], ew[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int k = i + 16 * m;
-        y[m] = make_double2(0.0, 0.0);
-        es[m] = 16u * (uint32_t)(k < NSC ? k : 0);
-        ew[m] = es[m] - 16u * NSC;
-        eo[m] = 0;
-    }
+    // H_k = sum_j s_j t_j E[k j] over the pairs (k, 53 - k): with c_j = s_j t_j,
+    // A = sum_j c_j Re E[k j], B = sum_j c_j Im E[k j], H_k = A + i B and
+    // H_{53-k} = A - i B.  Lane i: k = i + 1 and i + 17 (<= 26); H_0 = sum_j c_j
+    // over the row.  c_j reaches the FMAs as their DPP64 row_newbcast operand.
     const double2 ca = cscale(ta, sia), cb = cscale(tb, sib);
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        const double2 cj = j < 16 ? row_bcast_n(ca, j) : row_bcast_n(cb, j - 16);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const double2 u = ld_e(sE, eo[m]);
-            y[m].x = fma(u.x, cj.x, fma(-u.y, cj.y, y[m].x));
-            y[m].y = fma(u.x, cj.y, fma(u.y, cj.x, y[m].y));
-            eo[m] = dft_step(eo[m], es[m], ew[m]);
-        }
+    const double2 h0 = row16_sum(cadd(ca, cb));
+    const int k1 = i + 1, k2 = i + 17;
+    const bool two = k2 <= NSC / 2;
+    const uint32_t s1 = 16u * (uint32_t)k1, w1 = s1 - 16u * NSC;
+    const uint32_t s2 = 16u * (uint32_t)(two ? k2 : k1), w2 = s2 - 16u * NSC;
+    uint32_t o1 = 0, o2 = 0;
+    double2 A1 = make_double2(0.0, 0.0), B1 = A1, A2 = A1, B2 = A1;
+    double2 cav = ca, cbv = cb;
+    dpp_ready(cav, cbv);
+    lrq2_readout<R, 0>(sE, cav, cbv, o1, o2, s1, w1, s2, w2, A1, B1, A2, B2);
+    if (i == 0) st2(W, 0, h0);
+    st2(W, k1, make_double2(A1.x - B1.y, A1.y + B1.x));
+    st2(W, NSC - k1, make_double2(A1.x + B1.y, A1.y - B1.x));
+    if (two) {
+        st2(W, k2, make_double2(A2.x - B2.y, A2.y + B2.x));
+        st2(W, NSC - k2, make_double2(A2.x + B2.y, A2.y - B2.x));
     }
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-        if (i + 16 * m < NSC) st2(W, i + 16 * m, y[m]);
 }
 
-int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream, bool fused_dpp)
+int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream, int form)
 {
     // instantiated at 20, 24, 28, 32 rows: a rank r below runs the next size
     // up with rows r.. as b I (col_s = 0 past the rank: no coupling, t = 0
-    // there), bitwise the same arithmetic on the live rows
+    // there), bitwise the same arithmetic on the live rows.  form (A/B): 0 the
+    // product, 1 the Cholesky's broadcasts as separate movs (rank 21..24 only),
+    // 2 every size held to 2 waves per SIMD (256 VGPRs, spilling)
     if (rank <= 16 || rank > 32) return WCE_EINVAL;
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const dim3 gq((unsigned)((units + 15) / 16)), bq(256);
     hipStream_t s = (hipStream_t)stream;
-    if (!fused_dpp && rank > 20 && rank <= 24)   // A/B: the broadcasts as separate v_mov_b64_dpp (round 6 first form)
+    if (form == 1 && rank > 20 && rank <= 24)
         hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, false>), gq, bq, 0, s, st, a);
-    else if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20>), gq, bq, 0, s, st, a);
+    else if (form == 2) {
+        if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20, true, 2>), gq, bq, 0, s, st, a);
+        else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, true, 2>), gq, bq, 0, s, st, a);
+        else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28, true, 2>), gq, bq, 0, s, st, a);
+        else hipLaunchKernelGGL((mmse_lr_quad2_kernel<32, true, 2>), gq, bq, 0, s, st, a);
+    } else if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20>), gq, bq, 0, s, st, a);
     else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24>), gq, bq, 0, s, st, a);
     else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28>), gq, bq, 0, s, st, a);
     else hipLaunchKernelGGL((mmse_lr_quad2_kernel<32>), gq, bq, 0, s, st, a);
