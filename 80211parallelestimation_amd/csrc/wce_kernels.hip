@@ -3184,7 +3184,7 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
         return hip_status(hipGetLastError());
     }
     if (form == LrForm::Quad2) {   // wce_lr_quad2.hip; A/B: variant 6 the Cholesky's broadcasts as separate movs,
-        const int lv = variant(WCE_VARIANT_LR);   // 7 every size held to 2 waves per SIMD
+        const int lv = variant(WCE_VARIANT_LR);   // 7 every size at 1 wave per SIMD (no spills)
         return launch_lr_quad2(st, rank, a, stream, lv == 6 ? 1 : lv == 7 ? 2 : 0);
     }
     const dim3 g((unsigned)waves), b(64);

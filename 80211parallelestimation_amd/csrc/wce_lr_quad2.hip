@@ -160,7 +160,7 @@ __device__ __forceinline__ void lrq2_readout(const double2 *sE, double2 ca, doub
     }
 }
 
-template <int R, bool FD = true, int MINW = 1>
+template <int R, bool FD = true, int MINW = 2>
 __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
 {
     static_assert(R > 16 && R <= 32, "two rows per lane");
@@ -300,10 +300,16 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
             vk[m] = x;
             rk[m] = r;
         }
+        // t through LDS (sQ is free after the Gram build) so that the j loops stay
+        // rolled: unrolled, the scheduler hoists all 4R UT loads of a loop at once
+        // and that branch alone would set the kernel's register budget
+        sQ[rw][i] = ta;
+        sQ[rw][i + 16] = tb;
+        wave_lds_sync();
         double2 uy[4] = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
-#pragma unroll
+#pragma unroll 2
         for (int j = 0; j < R; ++j) {
-            const double2 tj = j < 16 ? row_bcast_n(ta, j) : row_bcast_n(tb, j - 16);
+            const double2 tj = sQ[rw][j];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const int k = i + 16 * m;
@@ -317,10 +323,10 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
             vk[m] = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
         }
         const double rb = 1.0 / bc;
-        // reload UT below instead of keeping the first loop's 4R values live (a
+        // reload UT below instead of keeping the first loop's values live (a
         // memory clobber: no load is reused across it)
         asm volatile("" ::: "memory");
-#pragma unroll
+#pragma unroll 2
         for (int j = 0; j < R; ++j) {
             double2 cp = make_double2(0.0, 0.0);
 #pragma unroll
@@ -361,20 +367,23 @@ int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream,
 {
     // instantiated at 20, 24, 28, 32 rows: a rank r below runs the next size
     // up with rows r.. as b I (col_s = 0 past the rank: no coupling, t = 0
-    // there), bitwise the same arithmetic on the live rows.  form (A/B): 0 the
-    // product, 1 the Cholesky's broadcasts as separate movs (rank 21..24 only),
-    // 2 every size held to 2 waves per SIMD (256 VGPRs, spilling)
+    // there), bitwise the same arithmetic on the live rows.  Built for 2 waves
+    // per SIMD (256 VGPRs; ranks 21..32 spill 72-236 B per lane): 65,536 frames
+    // at rank 24 154.5 us against 225.6 us left at 1 wave per SIMD (20 / 28 /
+    // 32: 130 / 241 / 278 against 133 / 255 / 278; profiles/r06_ab_lowrank.txt).
+    // form (A/B): 0 the product, 1 the Cholesky's broadcasts as separate movs
+    // (rank 21..24 only), 2 every size at 1 wave per SIMD (no spills)
     if (rank <= 16 || rank > 32) return WCE_EINVAL;
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const dim3 gq((unsigned)((units + 15) / 16)), bq(256);
     hipStream_t s = (hipStream_t)stream;
     if (form == 1 && rank > 20 && rank <= 24)
-        hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, false>), gq, bq, 0, s, st, a);
+        hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, false, 2>), gq, bq, 0, s, st, a);
     else if (form == 2) {
-        if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20, true, 2>), gq, bq, 0, s, st, a);
-        else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, true, 2>), gq, bq, 0, s, st, a);
-        else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28, true, 2>), gq, bq, 0, s, st, a);
-        else hipLaunchKernelGGL((mmse_lr_quad2_kernel<32, true, 2>), gq, bq, 0, s, st, a);
+        if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20, true, 1>), gq, bq, 0, s, st, a);
+        else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24, true, 1>), gq, bq, 0, s, st, a);
+        else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28, true, 1>), gq, bq, 0, s, st, a);
+        else hipLaunchKernelGGL((mmse_lr_quad2_kernel<32, true, 1>), gq, bq, 0, s, st, a);
     } else if (rank <= 20) hipLaunchKernelGGL((mmse_lr_quad2_kernel<20>), gq, bq, 0, s, st, a);
     else if (rank <= 24) hipLaunchKernelGGL((mmse_lr_quad2_kernel<24>), gq, bq, 0, s, st, a);
     else if (rank <= 28) hipLaunchKernelGGL((mmse_lr_quad2_kernel<28>), gq, bq, 0, s, st, a);
