@@ -2261,7 +2261,9 @@ __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_
 //   H_k = U_k s for the lane's 4 subcarriers: 16 lanes store 256 B of one frame.
 // Same algebra as mmse_lr_kernel, summed in another order (~1e-15).
 // ---------------------------------------------------------------------
-template <int R, int C>
+// FD (round 6): L[j][C] as the DPP64 row_newbcast operand of the update FMAs
+// (cmsub_dpp: 4 VALU per update instead of 2 movs + 4 FMAs), bit-identical
+template <int R, int C, bool FD = true>
 __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
 {
     if constexpr (C < R) {
@@ -2269,12 +2271,17 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
         const double rs = rsq_nr(d);
         Ar[C] = cscale(Ar[C], rs);                 // L[i][C] (for i >= C)
         ldi = i == C ? rs : ldi;                   // 1 / L_ii
+        if constexpr (FD) dpp_ready(Ar[C]);
 #pragma unroll
         for (int j = C + 1; j < R; ++j) {          // A[i][j] -= L[i][C] conj(L[j][C])
-            const double2 lj = row_bcast_n(Ar[C], j);
-            cmsub_conj(Ar[j], Ar[C], lj);
+            if constexpr (FD) {
+                cmsub_dpp_n(j, Ar[j], Ar[C], Ar[C]);
+            } else {
+                const double2 lj = row_bcast_n(Ar[C], j);
+                cmsub_conj(Ar[j], Ar[C], lj);
+            }
         }
-        lrq_chol<R, C + 1>(Ar, ldi, i);
+        lrq_chol<R, C + 1, FD>(Ar, ldi, i);
     }
 }
 
@@ -2288,7 +2295,7 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
 // subcarrier, E[k i mod 53] from an LDS copy of State::dft by the exact index
 // recurrence), instead of its row of R products (4R FMAs): the row's values
 // meet in LDS and lane i reads Q(|i - j|) (conjugated for j > i).
-template <int R, bool TQ = false>
+template <int R, bool TQ = false, bool FD = true>
 __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restrict__ st, SolveArgs a)
 {
     const int i = threadIdx.x & 15;   // the row of the R x R system this lane holds
@@ -2385,7 +2392,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         }
     }
     double ldi = 1.0;
-    lrq_chol<R, 0>(Ar, ldi, i);
+    lrq_chol<R, 0, FD>(Ar, ldi, i);
     // z = L^-1 beta: lane i keeps z_i
     double2 z = bt;
 #pragma unroll
@@ -3173,7 +3180,9 @@ int launch_mmse_lr(const State *st, int k0, int rank, int taps, const SolveArgs 
         const bool tq = lr_contig(taps);
 #define WCE_LRQ(RR)                                                                              \
     case RR:                                                                                     \
-        if (tq) hipLaunchKernelGGL((mmse_lr_quad_kernel<RR, true>), gq, bq, 0, s, st, a);        \
+        if (tq && RR == 16 && variant(WCE_VARIANT_LR) == 6)   /* A/B: separate DPP movs */        \
+            hipLaunchKernelGGL((mmse_lr_quad_kernel<16, true, false>), gq, bq, 0, s, st, a);     \
+        else if (tq) hipLaunchKernelGGL((mmse_lr_quad_kernel<RR, true>), gq, bq, 0, s, st, a);   \
         else hipLaunchKernelGGL((mmse_lr_quad_kernel<RR, false>), gq, bq, 0, s, st, a);          \
         break;
         switch (rank) {

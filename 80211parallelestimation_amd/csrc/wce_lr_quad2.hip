@@ -25,81 +25,6 @@ namespace wce {
 // Same algebra as mmse_lr_quad_kernel / mmse_lr_kernel, summed in another
 // order (~1e-15).
 // ---------------------------------------------------------------------
-// acc -= l conj(R[lane N of the 16-lane row]): gfx950's DPP64 row_newbcast on
-// v_fmac_f64 hands the broadcast operand straight to the FMA (4 VALU instead
-// of 2 v_mov_b64_dpp + 4 FMAs), the products and their order those of
-// cmsub_conj.  R must not have been written by a VALU instruction in the 2
-// wait states before (dpp_ready below).
-template <int N>
-__device__ __forceinline__ void cmsub_dpp(double2 &acc, double2 l, double2 R)
-{
-    asm("v_fmac_f64_dpp %[ax], -%[cx], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ax], -%[cy], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ay], -%[cx], %[ly] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ay], %[cy], %[lx] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf"
-        : [ax] "+v"(acc.x), [ay] "+v"(acc.y)
-        : [lx] "v"(l.x), [ly] "v"(l.y), [cx] "v"(R.x), [cy] "v"(R.y), [n] "i"(N));
-}
-__device__ __forceinline__ void cmsub_dpp_n(int n, double2 &acc, double2 l, double2 R)   // n constant after unrolling
-{
-    switch (n) {
-    case 0: cmsub_dpp<0>(acc, l, R); break;
-    case 1: cmsub_dpp<1>(acc, l, R); break;
-    case 2: cmsub_dpp<2>(acc, l, R); break;
-    case 3: cmsub_dpp<3>(acc, l, R); break;
-    case 4: cmsub_dpp<4>(acc, l, R); break;
-    case 5: cmsub_dpp<5>(acc, l, R); break;
-    case 6: cmsub_dpp<6>(acc, l, R); break;
-    case 7: cmsub_dpp<7>(acc, l, R); break;
-    case 8: cmsub_dpp<8>(acc, l, R); break;
-    case 9: cmsub_dpp<9>(acc, l, R); break;
-    case 10: cmsub_dpp<10>(acc, l, R); break;
-    case 11: cmsub_dpp<11>(acc, l, R); break;
-    case 12: cmsub_dpp<12>(acc, l, R); break;
-    case 13: cmsub_dpp<13>(acc, l, R); break;
-    case 14: cmsub_dpp<14>(acc, l, R); break;
-    default: cmsub_dpp<15>(acc, l, R); break;
-    }
-}
-// the 2 wait states between the VALU write of a DPP source and its first DPP
-// read, tied to the values so nothing moves across it
-__device__ __forceinline__ void dpp_ready(double2 &a, double2 &b)
-{
-    asm volatile("s_nop 1" : "+v"(a.x), "+v"(a.y), "+v"(b.x), "+v"(b.y));
-}
-// A += c[lane N] Re e, B += c[lane N] Im e (the read-out pairs), c as the DPP64
-// row_newbcast operand of the four FMAs; c ready as for cmsub_dpp
-template <int N>
-__device__ __forceinline__ void cfma_dpp(double2 &A, double2 &B, double2 c, double2 e)
-{
-    asm("v_fmac_f64_dpp %[ax], %[cx], %[er] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[ay], %[cy], %[er] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[bx], %[cx], %[ei] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %[by], %[cy], %[ei] row_newbcast:%c[n] row_mask:0xf bank_mask:0xf"
-        : [ax] "+v"(A.x), [ay] "+v"(A.y), [bx] "+v"(B.x), [by] "+v"(B.y)
-        : [cx] "v"(c.x), [cy] "v"(c.y), [er] "v"(e.x), [ei] "v"(e.y), [n] "i"(N));
-}
-__device__ __forceinline__ void cfma_dpp_n(int n, double2 &A, double2 &B, double2 c, double2 e)
-{
-    switch (n) {
-    case 0: cfma_dpp<0>(A, B, c, e); break;
-    case 1: cfma_dpp<1>(A, B, c, e); break;
-    case 2: cfma_dpp<2>(A, B, c, e); break;
-    case 3: cfma_dpp<3>(A, B, c, e); break;
-    case 4: cfma_dpp<4>(A, B, c, e); break;
-    case 5: cfma_dpp<5>(A, B, c, e); break;
-    case 6: cfma_dpp<6>(A, B, c, e); break;
-    case 7: cfma_dpp<7>(A, B, c, e); break;
-    case 8: cfma_dpp<8>(A, B, c, e); break;
-    case 9: cfma_dpp<9>(A, B, c, e); break;
-    case 10: cfma_dpp<10>(A, B, c, e); break;
-    case 11: cfma_dpp<11>(A, B, c, e); break;
-    case 12: cfma_dpp<12>(A, B, c, e); break;
-    case 13: cfma_dpp<13>(A, B, c, e); break;
-    case 14: cfma_dpp<14>(A, B, c, e); break;
-    default: cfma_dpp<15>(A, B, c, e); break;
-    }
-}
 // acc -= l conj(L[j][C]) with L[j][C] from lane (j mod 16) of column register R
 template <bool FD>
 __device__ __forceinline__ void chol_upd(int n, double2 &acc, double2 l, double2 R)
