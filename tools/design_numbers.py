@@ -57,7 +57,7 @@ row("MMSE frames/s, REF (diagonal Ryy: no factorisation), 65,536 frames (MALL-re
 rb = d["ref_mode"].get("b1048576")
 if rb:
     rr = rb["roofline"]
-    row("REF, 1,048,576 frames (past the MALL), `mmse_ref_flat_kernel`",
+    row("REF, 1,048,576 frames (past the MALL), `mmse_ref_elem_kernel` (round 6: one element per thread)",
         f"{rb['frames_per_s']:.3g} frames/s; {rr['achieved'] / 1000:.2f} TB/s algorithmic (976 B/frame) = "
         f"{100 * rr['frac']:.0f}% of 8 TB/s; {rr['achieved_sector_GBs'] / 1000:.2f} TB/s on the 1,360-B sector floor = "
         f"{100 * rr['frac_sector']:.0f}%; PMC traffic {rr['traffic'] / rb['frames']:.0f} B/frame")
