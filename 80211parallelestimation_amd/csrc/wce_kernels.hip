@@ -496,6 +496,38 @@ __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restr
     if (e < E) st2_nt(a.w, (f_begin + f) * a.ws + k, ref_out(shared ? s_u[k] : uf, s));
 }
 
+// One frame per wave (A/B against mmse_ref_elem_kernel, wce_debug_set_variant(0, 4)):
+// lane k = subcarrier k, lanes 0..3 load the frame's pilot pairs, so no frame's
+// pilot sectors are fetched by two waves; 11 of 64 lanes idle on the store.
+__global__ __launch_bounds__(256) void mmse_ref_wave_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
+                                                            uint32_t nfr)
+{
+    __shared__ double2 s_u[64];
+    const int lane = threadIdx.x & 63;
+    const bool shared = a.cs == 0;
+    const uint32_t fl = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t f = min(fl, nfr - 1);
+    const int pil = lane == 0 ? WCE_P0 : lane == 1 ? WCE_P1 : lane == 2 ? WCE_P2 : WCE_P3;
+    double2 xt = make_double2(0, 0), xr = xt, wp = xt, uf = xt;
+    if (lane < 4) {
+        const int64_t o = (f_begin + f) * a.fs + (int64_t)a.blk * a.bs + pil;
+        xt = ld2(a.tx, o);
+        xr = ld2(a.rx, o);
+        const int64_t wo = shared ? pil : (f_begin + f) * a.cs + pil;
+        wp = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
+    }
+    if (!shared && lane < NSC) uf = ld2(a.cu, (f_begin + f) * a.cs + lane);
+    if (shared && threadIdx.x < NSC) s_u[threadIdx.x] = ld2(a.cu, threadIdx.x);
+    __syncthreads();
+    const double rb = 1.0 / st->bcoef;
+    const double2 sj = ref_sum4(quad_sum_c(ref_term(wp, xt, xr)), make_double2(0, 0), make_double2(0, 0),
+                                make_double2(0, 0), rb);
+    const double2 sv = make_double2(
+        __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.x), 0), __builtin_amdgcn_readlane(__double2loint(sj.x), 0)),
+        __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.y), 0), __builtin_amdgcn_readlane(__double2loint(sj.y), 0)));
+    if (fl < nfr && lane < NSC) st2_nt(a.w, (f_begin + f) * a.ws + lane, ref_out(shared ? s_u[lane] : uf, sv));
+}
+
 // =====================================================================
 // BASELINE configs[4] in main.c semantics (round 3): REF PS_MMSE with any of
 // LT_LS / PS_Linear / PS_Cubic / PS_Sinc and equalization, one pass over HBM
@@ -2307,6 +2339,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     __shared__ double2 sQ[TQ ? 16 : 1][TQ ? 16 : 1];   // one 16-lane row's Q(0..15)
     __shared__ double2 sV[TQ ? 16 : 1][TQ ? 56 : 1];   // the row's frame: conj(x_k) rx_k ...
     __shared__ double sW[TQ ? 16 : 1][TQ ? 56 : 1];    // ... and |x_k|^2
+    __shared__ double2 sPA[TQ ? 16 : 1][TQ ? 32 : 1], sPB[TQ ? 16 : 1][TQ ? 32 : 1], sRP[TQ ? 16 : 1][TQ ? 32 : 1];
     if constexpr (TQ) {
         if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
         __syncthreads();
@@ -2341,18 +2374,31 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
             }
         }
         wave_lds_sync();   // the row's 16 lanes are one wave's
+        // pair tables over (k, 53 - k), k = 1..26 (round 6, as mmse_lr_quad2_kernel):
+        // one gather and half the FMAs per pair
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kp = i + 1 + 16 * h;
+            if (kp <= NSC / 2) {
+                const double2 u = sV[rw][kp], w = sV[rw][NSC - kp];
+                const double pu = sW[rw][kp], pw = sW[rw][NSC - kp];
+                sPA[rw][kp] = cadd(u, w);
+                sPB[rw][kp] = csub(u, w);
+                sRP[rw][kp] = make_double2(pu + pw, pu - pw);
+            }
+        }
+        wave_lds_sync();
         // Q(i) = sum_k p_k conj(E[k i]), beta_i = s_i sum_k v_k conj(E[k i]) (U[k][i] = s_i E[k i])
-        double2 q = make_double2(0.0, 0.0), bq = make_double2(0.0, 0.0);
+        double2 q = make_double2(sW[rw][0], 0.0), bq = sV[rw][0];   // the k = 0 terms
         const uint32_t qs = 16u * (uint32_t)i, qw = qs - 16u * NSC;
-        uint32_t qo = 0;   // 16 (k i mod 53)
-#pragma unroll 4
-        for (int k = 0; k < NSC; ++k) {
-            const double2 e = ld_e(sE, qo), v = sV[rw][k];
-            const double w = sW[rw][k];
-            q.x = fma(w, e.x, q.x);                        // += p_k conj(E[k i])
-            q.y = fma(-w, e.y, q.y);
-            bq.x = fma(v.x, e.x, fma(v.y, e.y, bq.x));     // += v_k conj(E[k i])
-            bq.y = fma(v.y, e.x, fma(-v.x, e.y, bq.y));
+        uint32_t qo = qs;   // 16 (k i mod 53), k = 1
+#pragma unroll 2
+        for (int kp = 1; kp <= NSC / 2; ++kp) {
+            const double2 e = ld_e(sE, qo), pa = sPA[rw][kp], pb = sPB[rw][kp], pp = sRP[rw][kp];
+            q.x = fma(pp.x, e.x, q.x);
+            q.y = fma(-pp.y, e.y, q.y);
+            bq.x = fma(pa.x, e.x, fma(pb.y, e.y, bq.x));
+            bq.y = fma(pa.y, e.x, fma(-pb.x, e.y, bq.y));
             qo = dft_step(qo, qs, qw);
         }
         const double si = row ? st->col_s[i] : 0.0;
@@ -2454,28 +2500,26 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     double2 y[4];   // H_k = U_k s at k = i + 16 m: t_j broadcast once per j
 #pragma unroll
     for (int m = 0; m < 4; ++m) y[m] = make_double2(0.0, 0.0);
-    if constexpr (TQ) {   // U[k][j] = s_j E[k j]: E from LDS by the index recurrence over j
-        uint32_t eo[4], es[4], ew[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int k = i + 16 * m;
-            es[m] = 16u * (uint32_t)(k < NSC ? k : 0);
-            ew[m] = es[m] - 16u * NSC;
-            eo[m] = 0;
-        }
+    if constexpr (TQ) {   // U[k][j] = s_j E[k j]: the pair-form read-out of mmse_lr_quad2_kernel (round 6)
         const double ts = row ? st->col_s[i] : 0.0;
-        const double2 c = cscale(t, ts);   // s_i t_i on lane i
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const double2 cj = row_bcast_n(c, j);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const double2 u = ld_e(sE, eo[m]);
-                y[m].x = fma(u.x, cj.x, fma(-u.y, cj.y, y[m].x));
-                y[m].y = fma(u.x, cj.y, fma(u.y, cj.x, y[m].y));
-                eo[m] = dft_step(eo[m], es[m], ew[m]);
-            }
+        double2 c = cscale(t, ts);   // s_i t_i on lane i
+        const double2 h0 = row16_sum(c);
+        const int k1 = i + 1, k2 = i + 17;
+        const bool two = k2 <= NSC / 2;
+        const uint32_t s1 = 16u * (uint32_t)k1, w1 = s1 - 16u * NSC;
+        const uint32_t s2 = 16u * (uint32_t)(two ? k2 : k1), w2 = s2 - 16u * NSC;
+        uint32_t o1 = 0, o2 = 0;
+        double2 A1 = make_double2(0.0, 0.0), B1 = A1, A2 = A1, B2 = A1;
+        dpp_ready(c);
+        lrq2_readout<R, 0>(sE, c, c, o1, o2, s1, w1, s2, w2, A1, B1, A2, B2);
+        if (i == 0) st2(W, 0, h0);
+        st2(W, k1, make_double2(A1.x - B1.y, A1.y + B1.x));
+        st2(W, NSC - k1, make_double2(A1.x + B1.y, A1.y - B1.x));
+        if (two) {
+            st2(W, k2, make_double2(A2.x - B2.y, A2.y + B2.x));
+            st2(W, NSC - k2, make_double2(A2.x + B2.y, A2.y - B2.x));
         }
+        return;
     } else {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -3041,6 +3085,11 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
             // capped grid (flat): 65,536 frames 20.3 / 25.0 us, 131,072 43.1 / 49.2,
             // 262,144 102.7 / 89.3, 1,048,576 380.9 / 338.7 (flat / elem)
             const int v = variant(WCE_VARIANT_REF);
+            if (v == 4) {   // A/B: one frame per wave
+                hipLaunchKernelGGL(mmse_ref_wave_kernel, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s, st, a, f0,
+                                   (uint32_t)nf);
+                continue;
+            }
             if (v == 3 || (v == 0 && nf > REF_ELEM_FROM)) {
                 hipLaunchKernelGGL(mmse_ref_elem_kernel, dim3((unsigned)((nf * NSC + 255) / 256)), dim3(256), 0, s, st,
                                    a, f0, (uint32_t)nf);

@@ -63,28 +63,6 @@ __device__ __forceinline__ void lrq2_chol(double2 (&Ar)[16], double2 (&Br)[R], d
     }
 }
 
-// the read-out's column j (compile-time, so each DPP lane select is an
-// immediate): c_j from lane j of ca (j < 16) or lane j - 16 of cb
-template <int R, int J>
-__device__ __forceinline__ void lrq2_readout(const double2 *sE, double2 ca, double2 cb, uint32_t &o1, uint32_t &o2,
-                                             uint32_t s1, uint32_t w1, uint32_t s2, uint32_t w2, double2 &A1,
-                                             double2 &B1, double2 &A2, double2 &B2)
-{
-    if constexpr (J < R) {
-        const double2 e1 = ld_e(sE, o1), e2 = ld_e(sE, o2);
-        if constexpr (J < 16) {
-            cfma_dpp<J>(A1, B1, ca, e1);
-            cfma_dpp<J>(A2, B2, ca, e2);
-        } else {
-            cfma_dpp<J - 16>(A1, B1, cb, e1);
-            cfma_dpp<J - 16>(A2, B2, cb, e2);
-        }
-        o1 = dft_step(o1, s1, w1);
-        o2 = dft_step(o2, s2, w2);
-        lrq2_readout<R, J + 1>(sE, ca, cb, o1, o2, s1, w1, s2, w2, A1, B1, A2, B2);
-    }
-}
-
 template <int R, bool FD = true, int MINW = 2>
 __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
 {
