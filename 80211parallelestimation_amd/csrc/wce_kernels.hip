@@ -454,7 +454,9 @@ __global__ __launch_bounds__(256) void mmse_ref_flat_kernel(const State *__restr
 // bit-identical.  Measured (1,048,576 frames, profiles/r06_ab_ref_elem.txt):
 // 381 -> 337 us against the capped chunks; 2 or 4 elements per lane (462, 440),
 // plain stores (371), 128 / 512 / 1,024-thread blocks (375 / 340 / 365) lose, and
-// an XCD-aware block remap (each XCD one contiguous run) changes nothing (342).
+// an XCD-aware block remap (each XCD one contiguous run) changes nothing (342),
+// and neither does one frame per wave (344 vs 343: no frame's pilot sectors
+// fetched by two waves, so that re-fetch is not what holds it).
 __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
                                                             uint32_t nfr)
 {
@@ -494,38 +496,6 @@ __global__ __launch_bounds__(256) void mmse_ref_elem_kernel(const State *__restr
     const uint32_t j = f - ff;
     const double2 s = make_double2(j == 0 ? sr[0] : j == 1 ? sr[1] : sr[2], j == 0 ? si[0] : j == 1 ? si[1] : si[2]);
     if (e < E) st2_nt(a.w, (f_begin + f) * a.ws + k, ref_out(shared ? s_u[k] : uf, s));
-}
-
-// One frame per wave (A/B against mmse_ref_elem_kernel, wce_debug_set_variant(0, 4)):
-// lane k = subcarrier k, lanes 0..3 load the frame's pilot pairs, so no frame's
-// pilot sectors are fetched by two waves; 11 of 64 lanes idle on the store.
-__global__ __launch_bounds__(256) void mmse_ref_wave_kernel(const State *__restrict__ st, SolveArgs a, int64_t f_begin,
-                                                            uint32_t nfr)
-{
-    __shared__ double2 s_u[64];
-    const int lane = threadIdx.x & 63;
-    const bool shared = a.cs == 0;
-    const uint32_t fl = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t f = min(fl, nfr - 1);
-    const int pil = lane == 0 ? WCE_P0 : lane == 1 ? WCE_P1 : lane == 2 ? WCE_P2 : WCE_P3;
-    double2 xt = make_double2(0, 0), xr = xt, wp = xt, uf = xt;
-    if (lane < 4) {
-        const int64_t o = (f_begin + f) * a.fs + (int64_t)a.blk * a.bs + pil;
-        xt = ld2(a.tx, o);
-        xr = ld2(a.rx, o);
-        const int64_t wo = shared ? pil : (f_begin + f) * a.cs + pil;
-        wp = a.cw ? ld2(a.cw, wo) : cconj(ld2(a.cu, wo));
-    }
-    if (!shared && lane < NSC) uf = ld2(a.cu, (f_begin + f) * a.cs + lane);
-    if (shared && threadIdx.x < NSC) s_u[threadIdx.x] = ld2(a.cu, threadIdx.x);
-    __syncthreads();
-    const double rb = 1.0 / st->bcoef;
-    const double2 sj = ref_sum4(quad_sum_c(ref_term(wp, xt, xr)), make_double2(0, 0), make_double2(0, 0),
-                                make_double2(0, 0), rb);
-    const double2 sv = make_double2(
-        __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.x), 0), __builtin_amdgcn_readlane(__double2loint(sj.x), 0)),
-        __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sj.y), 0), __builtin_amdgcn_readlane(__double2loint(sj.y), 0)));
-    if (fl < nfr && lane < NSC) st2_nt(a.w, (f_begin + f) * a.ws + lane, ref_out(shared ? s_u[lane] : uf, sv));
 }
 
 // =====================================================================
@@ -3085,11 +3055,6 @@ int launch_mmse_solve(const State *st, const SolveArgs &a, void *stream)
             // capped grid (flat): 65,536 frames 20.3 / 25.0 us, 131,072 43.1 / 49.2,
             // 262,144 102.7 / 89.3, 1,048,576 380.9 / 338.7 (flat / elem)
             const int v = variant(WCE_VARIANT_REF);
-            if (v == 4) {   // A/B: one frame per wave
-                hipLaunchKernelGGL(mmse_ref_wave_kernel, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s, st, a, f0,
-                                   (uint32_t)nf);
-                continue;
-            }
             if (v == 3 || (v == 0 && nf > REF_ELEM_FROM)) {
                 hipLaunchKernelGGL(mmse_ref_elem_kernel, dim3((unsigned)((nf * NSC + 255) / 256)), dim3(256), 0, s, st,
                                    a, f0, (uint32_t)nf);
