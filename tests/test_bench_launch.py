@@ -72,3 +72,19 @@ def test_launcher_parent_never_imports_torch():
     assert main.index("check_world(") < main.index("Dist()")
     head = src[:src.index("def main():")]
     assert "\nimport torch" not in head and "\nfrom torch" not in head
+
+
+@pytest.mark.gpu
+def test_gpus_2_without_launcher_runs_the_headline_on_the_device():
+    """The launcher path end to end on the GPU: `bench.py --gpus 2` with no
+    torch.distributed.run starts two ranks (gloo, both on device 0 of a
+    one-GPU box), each estimates its shard of the headline batch on the
+    device, and the relayed line spans both ranks with a measured value."""
+    p = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--prewarm-s", "0.05", "--no-extras",
+              "--no-cpu-baseline", "--frames-per-gpu", "4096", "--extras-out", ""], timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = _line(p)
+    assert r["n_gpus"] == 2 and r["launcher"] == "bench.py --gpus 2"
+    assert r["dist_check"]["group_size"] == 2 and r["dist_check"]["all_ranks_agree"]
+    assert r["config"]["global_frames"] == 2 * 4096
+    assert r["value"] > 0 and r["nonfinite_frames"] == 0

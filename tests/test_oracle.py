@@ -250,3 +250,21 @@ def test_textbook_mp_fixture_inputs_regenerate():
     for i in np.nonzero(d["kind"] == "bench")[0]:
         t, r = m.synth_block0(int(d["bench_frame"][i]), d["h_shared"], float(d["ow2"]))
         assert np.array_equal(t, d["tx"][i]) and np.array_equal(r, d["rx"][i])
+
+
+def test_cov_unified_solve_vs_mp_literal(oracle, golden):
+    """The oracle's long double unified solve with C = F Rhh F^H (the
+    reference's F) against the .m formula evaluated literally in mpmath with a
+    model Rhh (tests/golden/make_cov_mp.py), 7 profiles x 4 frames at the
+    operating ow2: measured <= 9.1e-14."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_cov_lowrank_gpu import c_ld, solve_ld
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cov_mp_pins.npz"))
+    inp = golden["inputs"]
+    worst = 0.0
+    for pi in range(len(d["taps"])):
+        exp = solve_ld(oracle, c_ld(oracle, np.diag(d["pdp"][pi]).astype(np.complex128)), d["tx"], d["rx"], inp["ow2"])
+        Hm = d["H_hi"][pi].astype(np.clongdouble) + d["H_lo"][pi]
+        worst = max(worst, max(float(oracle.normrel(exp[f], Hm[f])) for f in range(len(d["tx"]))))
+    assert worst < 2e-13, worst
