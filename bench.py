@@ -100,6 +100,12 @@ def launch_ranks(n: int, argv) -> int:
     env.setdefault("OMP_NUM_THREADS", "1")
     print("bench: launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    import signal
+
+    def forward(sig, _frame):   # a SIGTERM / SIGINT to this parent reaches the ranks (torch.distributed.run
+        p.send_signal(sig)      # tears its workers down on it) instead of orphaning them
+    for sg in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sg, forward)
     last = None
     for ln in p.stdout:
         s = ln.strip()
@@ -151,11 +157,14 @@ def dry_run(args, dist):
     """--dry-run: the N-rank control path without a device -- the process
     group, the barriers and the max over ranks every timed leg uses -- and a
     contract-shaped line (value null) from rank 0.  WCE_DRY_FAIL_RANK=r makes
-    rank r exit 1 after the group forms (the launcher's failure path)."""
+    rank r exit 1 after the group forms (the launcher's failure path);
+    WCE_DRY_HOLD_S=t keeps every rank alive t seconds (its signal path)."""
     dist.barrier()
     if os.environ.get("WCE_DRY_FAIL_RANK") == str(dist.rank):
         print(f"bench: dry run: rank {dist.rank} failing on request", file=sys.stderr, flush=True)
         sys.exit(1)
+    if os.environ.get("WCE_DRY_HOLD_S"):   # tests: ranks that stay alive until stopped
+        time.sleep(float(os.environ["WCE_DRY_HOLD_S"]))
     t0 = time.perf_counter()
     dist.barrier()
     el = dist.max(time.perf_counter() - t0)

@@ -88,3 +88,55 @@ def test_gpus_2_without_launcher_runs_the_headline_on_the_device():
     assert r["dist_check"]["group_size"] == 2 and r["dist_check"]["all_ranks_agree"]
     assert r["config"]["global_frames"] == 2 * 4096
     assert r["value"] > 0 and r["nonfinite_frames"] == 0
+
+
+def test_sigterm_to_the_parent_reaches_the_ranks():
+    """A driver that stops the parent with SIGTERM must not leave ranks
+    behind: the parent forwards the signal to torch.distributed.run, which
+    stops its workers, and the parent exits non-zero."""
+    import signal
+    import time
+    e = dict(os.environ, WCE_DIST_BACKEND="gloo", OMP_NUM_THREADS="1", WCE_DRY_HOLD_S="60")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e, cwd=REPO)
+    t0, seen = time.time(), 0
+    while time.time() - t0 < 60 and p.poll() is None:   # wait until both ranks run
+        time.sleep(1)
+        seen = _ranks_of(p.pid)
+        if seen >= 2:
+            break
+    assert seen == 2, "the two ranks never started"
+    time.sleep(3)                      # past the process group's formation
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=120)
+    assert p.returncode != 0
+    assert _ranks_of(p.pid) == 0
+
+
+def _ranks_of(ppid):
+    """live bench.py rank processes below ppid (via /proc)"""
+    import glob
+    kids = {ppid}
+    found = 0
+    changed = True
+    procs = {}
+    for d in glob.glob("/proc/[0-9]*"):
+        try:
+            st = open(d + "/stat").read()
+            pid = int(d.rsplit("/", 1)[1])
+            procs[pid] = (int(st.rsplit(")", 1)[1].split()[1]), open(d + "/cmdline").read())
+        except (OSError, ValueError, IndexError):
+            continue
+    while changed:
+        changed = False
+        for pid, (pp, _) in procs.items():
+            if pp in kids and pid not in kids:
+                kids.add(pid)
+                changed = True
+    for pid in kids - {ppid}:
+        cmd = procs[pid][1]
+        if "bench.py" in cmd and "torch.distributed.run" not in cmd:
+            found += 1
+    return found
