@@ -49,7 +49,7 @@ LEGS = {
     "frame_cov_ref": ("ref_fc_kernel<false>", 65536),        # REF + FRAME_COV, PS_MMSE only: the whole step
     "lowrank4": ("mmse_lr_lane_staged_kernel<4, 1, true>", 65536),     # Toeplitz Gram (taps 0..3, round 4)
     "lowrank8": ("mmse_lr_lane_staged_kernel<8, 1, true>", 65536),
-    "lowrank16": ("mmse_lr_quad_kernel<16, true>", 65536),
+    "lowrank16": ("mmse_lr_quad_kernel<16, true, true>", 65536),   # round 6: fused-DPP Cholesky, pair-form DFTs
     "lowrank24": ("mmse_lr_quad2_kernel<24, true, 2>", 65536),    # round 6: two Gram rows per lane (taps 0..23)
     "lowrank53": ("mmse_lr_kernel<0, true>", 65536),     # the same at full rank, spectrum 2e11
     "lowrank8_1m": ("mmse_lr_lane_staged_kernel<8, 2, true>", 1 << 20),   # block 0 only, frame_stride 53
