@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void ref_ls_elem_kernel(const State *__restric
 // factorisation of [[Ryy, rx], [rx', *]] also runs the forward solve.
 //
 // Cholesky (Ryy = L L'): pivot k publishes c_k = u_k / sqrt(d_k) (one
-// v_rsq_f64 and a third-order refinement step, rsq_nr / rsq_uniform), so both
+// v_rsq_f64 and a third-order refinement step, rsq_nr / rsq_lane), so both
 // rank-1 operands are read as published.  Each 8-column panel runs row-per-lane
 // (chol_panel: lane l holds A[l][8 KB + c], one full-wave store publishes the
 // pivot column, in-panel operands by DPP64 row_newbcast); the trailing blocks
@@ -691,19 +691,20 @@ __device__ __forceinline__ void upd_col_live(double2 (&A)[RB][RB], const double2
         cmsub_live(cm & kRows55, A[RB - 1][BB], Ur[RB - 1], v);
     }
 }
-// 1/sqrt(d) of a wave-uniform pivot d.  The kernel is power-capped, so the
-// 6-op chain runs on one lane alone (EXEC = that lane inside the asm) and
-// comes back as a scalar (v_readlane): the same arithmetic as rsq_nr (one
-// third-order step after v_rsq_f64), bit-identical, at 1/64 of its energy.
-// The lane is the lowest ACTIVE one (s_ff1 of EXEC), so under divergent
-// control flow the asm never writes a lane that is switched off.
-__device__ __forceinline__ double rsq_uniform(double d)
+// 1/sqrt(d) of the pivot d that lane L holds, as a wave-uniform scalar.  The
+// kernel is power-capped, so the 6-op chain runs on lane L alone (EXEC = that
+// lane inside the asm, ANDed with the incoming EXEC so that a switched-off lane
+// is never written) and comes back through v_readlane: the same arithmetic as
+// rsq_nr (one third-order step after v_rsq_f64), bit-identical, at 1/64 of its
+// energy.  L is a constant after unrolling and every caller runs on the full
+// wave.  (Rounds 2-5 read d out to an SGPR first and ran the chain on the
+// lowest active lane: two more v_readlane per pivot; round 6, 470 -> 454 us per
+// 65,536 frames, profiles/r06_ab_rsq_lane.txt.)
+__device__ __forceinline__ double rsq_lane(double dv, int L)
 {
     double y, t, e;
     uint64_t sv;
     const double c38 = 0.375;
-    const uint64_t ex = __builtin_amdgcn_read_exec();
-    const int l0 = __builtin_ctzll(ex);
     asm("s_mov_b64 %[sv], exec\n\t"
         "s_mov_b64 exec, %[m]\n\t"
         "v_rsq_f64 %[y], %[d]\n\t"
@@ -715,8 +716,8 @@ __device__ __forceinline__ double rsq_uniform(double d)
         "v_fma_f64 %[y], %[t], %[e], %[y]\n\t"
         "s_mov_b64 exec, %[sv]"
         : [y] "=&v"(y), [t] "=&v"(t), [e] "=&v"(e), [sv] "=&s"(sv)
-        : [d] "s"(d), [c] "s"(c38), [m] "s"(ex & (0 - ex)));
-    return readlane_f64(y, l0);   // the lane that computed it
+        : [d] "v"(dv), [c] "s"(c38), [m] "s"((1ull << L) & __builtin_amdgcn_read_exec()));
+    return readlane_f64(y, L);
 }
 
 // (Round 1's block-cyclic square-root-free LDL^H -- ldl_step / ldl_panel, a
@@ -978,7 +979,7 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
         if (kq < 7) {
             // row lane of column 8KB+c is live for 8KB+c <= lane <= 54
             cmsub_panel<KB>(kq + 1, P[kq + 1], P[kq], R);   // lookahead
-            const double rs = rsq_uniform(readlane_f64(P[kq + 1].x, k + 1));
+            const double rs = rsq_lane(P[kq + 1].x, k + 1);
             P[kq + 1] = cscale(P[kq + 1], rs);
             next[lane] = P[kq + 1];                               // publish c_{k+1}: one store
             if (KEEP) keep_rsel_lane(rsel, k + 1, rs);
@@ -996,14 +997,14 @@ __device__ __forceinline__ void chol_panel(double2 (&A)[RB][RB], double2 (&P)[8]
             if (KEEP) to_blocks<KB>(A, P, s, p, q, lane);
             if constexpr (KB + 2 < RB) {
                 to_rows<KB + 1>(A, P, s, p, q, lane);
-                const double rs = rsq_uniform(readlane_f64(P[0].x, k + 1));
+                const double rs = rsq_lane(P[0].x, k + 1);
                 P[0] = cscale(P[0], rs);
                 next[lane] = P[0];
                 if (KEEP) keep_rsel_lane(rsel, k + 1, rs);
                 wave_lds_sync();
                 R = next[8 * (KB + 1) + (lane & 7)];
             } else {   // block column 6 stays block-cyclic: the 8 owners of column 48 publish
-                const double rs = rsq_uniform(readlane_f64(A[KB + 1][KB + 1].x, 0));
+                const double rs = rsq_lane(A[KB + 1][KB + 1].x, 0);
                 const double2 cs = cscale(A[KB + 1][KB + 1], rs);
                 if (q == 0) next[p + 8 * (KB + 1)] = cs;
                 if (KEEP) {
@@ -1030,7 +1031,7 @@ __device__ __forceinline__ double2 chol_last(double2 (&A)[RB][RB], L &s, int p, 
         const double2 *col = s.u[k & 1];
         double2 *next = s.u[(k + 1) & 1];
         cmsub_live(lanes_lower(kq), A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
-        const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
+        const double rs = rsq_lane(A[RB - 1][RB - 1].x, 9 * (kq + 1));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;
         wave_lds_sync();
@@ -1054,7 +1055,7 @@ __device__ __forceinline__ void chol_last_keep(double2 (&A)[RB][RB], L &s, int p
         const double2 *col = s.u[k & 1];
         double2 *next = s.u[(k + 1) & 1];
         cmsub_live(lanes_lower(kq), A[RB - 1][RB - 1], col[p + B6], col[q + B6]);
-        const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 9 * (kq + 1)));
+        const double rs = rsq_lane(A[RB - 1][RB - 1].x, 9 * (kq + 1));
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == kq + 1) next[p + B6] = cs;
         keep_rsel_lane(rsel, k + 1, rs);
@@ -1099,7 +1100,7 @@ __device__ __forceinline__ void dense_chol(double2 (&A)[RB][RB], L &s, int p, in
         double2 R = s.u[0][8 * K0 + (lane & 7)];
         chol_panels_keep<K0>(A, P, R, s, p, q, lane, rsel);
     } else {   // the system is block (6, 6) alone: pivot 48 opens the block-cyclic last panel
-        const double rs = rsq_uniform(readlane_f64(A[RB - 1][RB - 1].x, 0));
+        const double rs = rsq_lane(A[RB - 1][RB - 1].x, 0);
         const double2 cs = cscale(A[RB - 1][RB - 1], rs);
         if (q == 0) s.u[0][p + 8 * (RB - 1)] = cs;
         keep_rsel_lane(rsel, 8 * (RB - 1), rs);
@@ -1636,7 +1637,6 @@ __device__ __forceinline__ void lr_gram_taps(const State *__restrict__ st, L &s,
 {
     constexpr int RMAX = NSC - 8 * K0;   // Gram column of the border (row 53)
     constexpr int NB = RB - K0;
-    const bool act = lane < NSC;
     {   // tables: E, p = |x|^2, v = x o conj(rx)
         const double2 xl = s.x[lane], rl = s.rx[lane];
         s.u[1][lane] = cmul(xl, cconj(rl));   // (E is in u[0] since the frame's staging)

@@ -196,6 +196,25 @@ if h:
            f"- VALU active {v['SQ_ACTIVE_INST_VALU']:,.0f} of {v['SQ_WAVE_CYCLES']:,.0f} quad-cycles per wave. Over 3 "
            f"co-resident waves that is ≈{100 * busy:.0f}% of SIMD time.\n"
            f"- HBM: FETCH_SIZE×2 + WRITE_SIZE = {traffic:.0f} MB per 65,536-frame launch, against 167 MB algorithmic.\n")
+    for leg, what, prev in (
+            ("lowrank24", "`mmse_lr_quad2_kernel<24>` (leg `lowrank24`)",
+             "The wave kernel it replaces at rank 24 issued 2,105 VALU and 432 LDS instructions per frame "
+             "(`r04_pmc_legs.json`)."),
+            ("lowrank16", "`mmse_lr_quad_kernel<16, true>` (leg `lowrank16`)", "")):
+        q = legs.get(leg)
+        if not q:
+            continue
+        u = {c: x / q["frames"] for c, x in q["counters"].items()}
+        pmc += (f"- Round 6, {what}, per frame (4 frames per wave): {u['SQ_INSTS_VALU']:,.0f} VALU instructions, "
+                f"{u['SQ_INSTS_VALU_FMA_F64']:,.0f} of them `FMA_F64`; {u['SQ_INSTS_LDS']:,.0f} LDS instructions, "
+                f"{u['SQ_LDS_BANK_CONFLICT']:,.0f} bank-conflict cycles; `SQ_WAIT_INST_LDS` "
+                f"{u['SQ_WAIT_INST_LDS']:,.0f}. {prev}\n")
+    q = legs.get("ref")
+    if q:
+        fb, wb = (q["counters"][c] * 1024 / q["frames"] for c in ("FETCH_SIZE", "WRITE_SIZE"))
+        pmc += (f"- Round 6, `mmse_ref_elem_kernel` (leg `ref`, {q['frames']:,} frames): FETCH_SIZE {fb:.0f} B and "
+                f"WRITE_SIZE {wb:.0f} B per frame ({fb + wb:,.0f} B against the 1,360-B sector floor; the pilot "
+                f"sectors of a frame that straddles two waves are read by both).\n")
 p = os.path.join(REPO, "DESIGN.md")
 s = open(p).read()
 a = s.index("| Quantity | Value |")

@@ -70,6 +70,11 @@ def pdp_rhh():
     return np.diag(p / p.sum()).astype(np.complex128) * 1.1e-4
 
 
+def same_kernel(label, full):
+    """the library's label (default template arguments left out) names LEGS' full demangled name"""
+    return label == full or full.startswith(label[:-1] + ", ")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", choices=sorted(LEGS), required=True)
@@ -106,7 +111,7 @@ def main():
         ctx.synth(tx0, rx0, None, B, seed=0x80211)
         tx, rx, fr = bench.tile_block0(wce, tx0, rx0, B, n)
         del tx0, rx0
-        assert ctx.lr_kernel(n) == LEGS[leg][0]
+        assert same_kernel(ctx.lr_kernel(n), LEGS[leg][0])
         H = wce.DeviceArray((n, N), zero=True)
         run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
                                    wce.PS_MMSE)
@@ -126,7 +131,7 @@ def main():
         ctx.synth(tx, rx, None, n, seed=0x80211)
         H = wce.DeviceArray((n, N), zero=True)
         fr = ctx.frames(tx, rx, n)
-        assert ctx.lr_kernel(n) == LEGS[leg][0]
+        assert same_kernel(ctx.lr_kernel(n), LEGS[leg][0])
         run = lambda: ctx.estimate(fr, wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0),
                                    wce.PS_MMSE)
     elif leg == "frame_cov_ref":
