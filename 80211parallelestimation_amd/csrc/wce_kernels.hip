@@ -2306,10 +2306,12 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);   // wave-uniform: scalar loads
     constexpr int uld = CLD;
     __shared__ double2 sE[TQ ? 64 : 1];
-    __shared__ double2 sQ[TQ ? 16 : 1][TQ ? 16 : 1];   // one 16-lane row's Q(0..15)
+    // odd row pitches in 16-B slots (272 / 528 B): two units' same-index reads in
+    // one ds_read_b128 lane group land on different banks
+    __shared__ double2 sQ[TQ ? 16 : 1][TQ ? 17 : 1];   // one 16-lane row's Q(0..15)
     __shared__ double2 sV[TQ ? 16 : 1][TQ ? 56 : 1];   // the row's frame: conj(x_k) rx_k ...
     __shared__ double sW[TQ ? 16 : 1][TQ ? 56 : 1];    // ... and |x_k|^2
-    __shared__ double2 sPA[TQ ? 16 : 1][TQ ? 32 : 1], sPB[TQ ? 16 : 1][TQ ? 32 : 1], sRP[TQ ? 16 : 1][TQ ? 32 : 1];
+    __shared__ double2 sPA[TQ ? 16 : 1][TQ ? 33 : 1], sPB[TQ ? 16 : 1][TQ ? 33 : 1], sRP[TQ ? 16 : 1][TQ ? 33 : 1];
     if constexpr (TQ) {
         if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
         __syncthreads();

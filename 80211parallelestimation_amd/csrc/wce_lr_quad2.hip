@@ -73,10 +73,13 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     __shared__ double2 sE[64];
-    __shared__ double2 sQ[16][32];    // one unit's Q(0..31)
+    // rows of 33 (528 B): the 16-lane rows of two units share a ds_read_b128
+    // lane group, and at a 512-B pitch their same-index reads (the pair tables'
+    // broadcasts, Q(|i - j|)) hit the same banks
+    __shared__ double2 sQ[16][33];    // one unit's Q(0..31)
     __shared__ double2 sV[16][56];    // the unit's frame: conj(x_k) rx_k ...
     __shared__ double sW[16][56];     // ... and |x_k|^2
-    __shared__ double2 sPA[16][32], sPB[16][32], sRP[16][32];   // the unit's pair tables (k = 1..26)
+    __shared__ double2 sPA[16][33], sPB[16][33], sRP[16][33];   // the unit's pair tables (k = 1..26)
     if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
     __syncthreads();
     if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows

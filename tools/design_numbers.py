@@ -199,8 +199,11 @@ if h:
     for leg, what, prev in (
             ("lowrank24", "`mmse_lr_quad2_kernel<24>` (leg `lowrank24`)",
              "The wave kernel it replaces at rank 24 issued 2,105 VALU and 432 LDS instructions per frame "
-             "(`r04_pmc_legs.json`)."),
-            ("lowrank16", "`mmse_lr_quad_kernel<16, true>` (leg `lowrank16`)", "")):
+             "(`r04_pmc_legs.json`). Its LDS tables at odd 16-B-slot row pitches: 227 → 168 conflict cycles, "
+             "164.5 → 160.2 µs (`r06_ab_lowrank_pad.txt`); what is left is the E[k d] gathers of the DFTs (16 lanes, "
+             "16 different entries)."),
+            ("lowrank16", "`mmse_lr_quad_kernel<16, true>` (leg `lowrank16`)",
+             "Odd row pitches: 178 → 100 conflict cycles, 92.0 → 88.1 µs.")):
         q = legs.get(leg)
         if not q:
             continue
