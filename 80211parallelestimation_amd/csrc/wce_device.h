@@ -129,6 +129,22 @@ __device__ __forceinline__ void wave_lds_sync()
 }
 
 
+// a = c on the lanes of mask m (a constant) that are active: two v_mov_b64 under EXEC
+__device__ __forceinline__ void keep_where_mask(uint64_t m, bool sel, double2 &a, double2 c)
+{
+    uint64_t sv;
+    asm volatile("s_mov_b64 %[sv], exec\n\t"
+                 "s_mov_b64 exec, %[m]\n\t"
+                 "v_mov_b64 %[ax], %[cx]\n\t"
+                 "v_mov_b64 %[ay], %[cy]\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [ax] "+v"(a.x), [ay] "+v"(a.y), [sv] "=&s"(sv)
+                 : [m] "s"(m & __builtin_amdgcn_read_exec()), [cx] "v"(c.x), [cy] "v"(c.y));
+}
+// lanes with (lane & 15) <= c / == c in every 16-lane row
+constexpr uint64_t rows16_upto(int c) { return ((2ull << c) - 1) * 0x0001000100010001ull; }
+constexpr uint64_t rows16_at(int c) { return 0x0001000100010001ull << c; }
+
 // ---------------------------------------------------------------- shared by the kernel files
 // 1/sqrt(d) from v_rsq_f64 (relative error ~2^-24).  One third-order
 // (Householder) step y += y e (1/2 + 3e/8), e = 1 - d y^2: error ~2^-72

@@ -928,18 +928,6 @@ __device__ __forceinline__ void keep_rsel_lane(double &rsel, int L, double rs)
                  : [r] "+v"(rsel), [sv] "=&s"(sv)
                  : [m] "s"((1ull << L) & __builtin_amdgcn_read_exec()), [v] "s"(rs));
 }
-// a = c on the lanes of mask m (a constant) that are active: two v_mov_b64 under EXEC
-__device__ __forceinline__ void keep_where_mask(uint64_t m, bool sel, double2 &a, double2 c)
-{
-    uint64_t sv;
-    asm volatile("s_mov_b64 %[sv], exec\n\t"
-                 "s_mov_b64 exec, %[m]\n\t"
-                 "v_mov_b64 %[ax], %[cx]\n\t"
-                 "v_mov_b64 %[ay], %[cy]\n\t"
-                 "s_mov_b64 exec, %[sv]"
-                 : [ax] "+v"(a.x), [ay] "+v"(a.y), [sv] "=&s"(sv)
-                 : [m] "s"(m & __builtin_amdgcn_read_exec()), [cx] "v"(c.x), [cy] "v"(c.y));
-}
 constexpr uint64_t lanes_q(int qq) { return 0x0101010101010101ull << qq; }   // lanes with q == qq
 
 // KEEP (the dense-C path, which back-substitutes): every finished panel is
@@ -2256,8 +2244,9 @@ __global__ __launch_bounds__(lr_staged_threads(R), MW) void mmse_lr_lane_staged_
 //   Cholesky on the rows: pivot c's scale and column by row_newbcast:c inside
 //                       the 16-lane row (DPP, no LDS), the trailing rows updated
 //                       by each lane for its own row
-//   z = L^-1 beta by broadcasts; t = L^-H z by 16-lane DPP sums (column c of L
-//                       is spread over the rows, one element per lane)
+//   z = L^-1 beta column by column, z_c as the DPP64 row_newbcast operand of
+//                       the FMAs (round 6); t = L^-H z by 16-lane DPP sums
+//                       (column c of L is spread over the rows, one per lane)
 //   complex x (a wave-uniform branch): the correction term from the lane's 4
 //                       subcarriers k = i, i + 16, ..., summed over the row
 //   H_k = U_k s for the lane's 4 subcarriers: 16 lanes store 256 B of one frame.
@@ -2287,6 +2276,18 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
     }
 }
 
+// One 16-lane unit's LDS in mmse_lr_quad_kernel<R, true>: the Toeplitz Gram's
+// tables.  The unit pitch (200 slots of 16 B, 8 mod 16) puts two units'
+// same-index reads (the pair tables' broadcasts, Q(|i - j|)) in one
+// ds_read_b128 lane group on different banks.
+struct LrqTabs {
+    double2 Q[17];                    // Q(0..15)
+    double2 V[56];                    // conj(x_k) rx_k ...
+    double W[56];                     // ... and |x_k|^2
+    double2 PA[33], PB[33], RP[33];   // the pair tables, k = 1..26
+};
+static_assert(sizeof(LrqTabs) / 16 % 16 == 8, "unit pitch 8 mod 16 slots");
+
 // (pass 1's U_k from an LDS copy per workgroup instead of scalar loads: slower,
 // rank 16 237 -> 271 us at 65,536 frames, 3.82 -> 4.39 ms at 1M; retired in
 // round 4, profiles/r03_ab_lowrank_ldsp.txt: U, 13.6 KB at rank 16, stays in
@@ -2306,12 +2307,8 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     const double2 *__restrict__ U1 = reinterpret_cast<const double2 *>(st->U);   // wave-uniform: scalar loads
     constexpr int uld = CLD;
     __shared__ double2 sE[TQ ? 64 : 1];
-    // odd row pitches in 16-B slots (272 / 528 B): two units' same-index reads in
-    // one ds_read_b128 lane group land on different banks
-    __shared__ double2 sQ[TQ ? 16 : 1][TQ ? 17 : 1];   // one 16-lane row's Q(0..15)
-    __shared__ double2 sV[TQ ? 16 : 1][TQ ? 56 : 1];   // the row's frame: conj(x_k) rx_k ...
-    __shared__ double sW[TQ ? 16 : 1][TQ ? 56 : 1];    // ... and |x_k|^2
-    __shared__ double2 sPA[TQ ? 16 : 1][TQ ? 33 : 1], sPB[TQ ? 16 : 1][TQ ? 33 : 1], sRP[TQ ? 16 : 1][TQ ? 33 : 1];
+    __shared__ LrqTabs sU[TQ ? 16 : 1];   // the workgroup's 16 units
+    const int rw = (threadIdx.x >> 4) & 15;
     if constexpr (TQ) {
         if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
         __syncthreads();
@@ -2332,7 +2329,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     if constexpr (TQ) {
         // the row's frame through LDS: lane i loads subcarriers i, i + 16, ... (256 B
         // per row and instruction), then every lane sweeps k from broadcast reads
-        const int rw = (threadIdx.x >> 4) & 15;
+        LrqTabs &T = sU[rw];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const int k = i + 16 * m;
@@ -2341,8 +2338,8 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
                 const double2 r = ld2(a.rx, base + k);
                 if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
                 cplx |= x.y != 0.0;
-                sW[rw][k] = fma(x.x, x.x, x.y * x.y);
-                sV[rw][k] = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+                T.W[k] = fma(x.x, x.x, x.y * x.y);
+                T.V[k] = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
             }
         }
         wave_lds_sync();   // the row's 16 lanes are one wave's
@@ -2352,21 +2349,21 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         for (int h = 0; h < 2; ++h) {
             const int kp = i + 1 + 16 * h;
             if (kp <= NSC / 2) {
-                const double2 u = sV[rw][kp], w = sV[rw][NSC - kp];
-                const double pu = sW[rw][kp], pw = sW[rw][NSC - kp];
-                sPA[rw][kp] = cadd(u, w);
-                sPB[rw][kp] = csub(u, w);
-                sRP[rw][kp] = make_double2(pu + pw, pu - pw);
+                const double2 u = T.V[kp], w = T.V[NSC - kp];
+                const double pu = T.W[kp], pw = T.W[NSC - kp];
+                T.PA[kp] = cadd(u, w);
+                T.PB[kp] = csub(u, w);
+                T.RP[kp] = make_double2(pu + pw, pu - pw);
             }
         }
         wave_lds_sync();
         // Q(i) = sum_k p_k conj(E[k i]), beta_i = s_i sum_k v_k conj(E[k i]) (U[k][i] = s_i E[k i])
-        double2 q = make_double2(sW[rw][0], 0.0), bq = sV[rw][0];   // the k = 0 terms
+        double2 q = make_double2(T.W[0], 0.0), bq = T.V[0];   // the k = 0 terms
         const uint32_t qs = 16u * (uint32_t)i, qw = qs - 16u * NSC;
         uint32_t qo = qs;   // 16 (k i mod 53), k = 1
 #pragma unroll 2
         for (int kp = 1; kp <= NSC / 2; ++kp) {
-            const double2 e = ld_e(sE, qo), pa = sPA[rw][kp], pb = sPB[rw][kp], pp = sRP[rw][kp];
+            const double2 e = ld_e(sE, qo), pa = T.PA[kp], pb = T.PB[kp], pp = T.RP[kp];
             q.x = fma(pp.x, e.x, q.x);
             q.y = fma(-pp.y, e.y, q.y);
             bq.x = fma(pa.x, e.x, fma(pb.y, e.y, bq.x));
@@ -2375,11 +2372,11 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         }
         const double si = row ? st->col_s[i] : 0.0;
         bt = cscale(bq, si);
-        sQ[rw][i] = q;
+        T.Q[i] = q;
         wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < R; ++j) {   // a s_i s_j Q(i - j) + b [i == j]; rows past R: the identity (never read)
-            const double2 qd = j <= i ? sQ[rw][(i - j) & 15] : cconj(sQ[rw][(j - i) & 15]);
+            const double2 qd = j <= i ? T.Q[(i - j) & 15] : cconj(T.Q[(j - i) & 15]);
             Ar[j] = cscale(qd, ac * si * st->col_s[j]);
             Ar[j].x += (i == j || (!row && j == 0)) ? bc : 0.0;
         }
@@ -2411,20 +2408,31 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
     }
     double ldi = 1.0;
     lrq_chol<R, 0, FD>(Ar, ldi, i);
-    // z = L^-1 beta: lane i keeps z_i
-    double2 z = bt;
+    // z = L^-1 beta: lane i keeps y_i = beta_i - sum_{c < i} L[i][c] z_c, and
+    // z_c = y_c / L_cc reaches the FMAs from lane c as their DPP64 row_newbcast
+    // operand (conj(z_c) in w: cmsub_dpp subtracts l conj(R)).  L's entries on
+    // and above the diagonal are zeroed first, so that no lane needs a select
+    // here or in the back-substitution (round 6: 2 muls and 4 DPP FMAs per
+    // column where a broadcast, a product and selects took ~20 VALU).
+#pragma unroll
+    for (int c = 0; c < R; ++c) keep_where_mask(rows16_upto(c), true, Ar[c], make_double2(0.0, 0.0));
+    double2 yv = bt;
 #pragma unroll
     for (int c = 0; c < R; ++c) {
-        const double2 zc = row_bcast_n(cscale(z, ldi), c);   // z_c = (beta_c - ...) / L_cc, from lane c
-        if (i == c) z = zc;
-        else if (i > c) z = csub(z, cmul(Ar[c], zc));
+        double2 w = make_double2(yv.x * ldi, -(yv.y * ldi));
+        dpp_ready(w);
+        cmsub_dpp_n(c, yv, Ar[c], w);   // y_i -= L[i][c] z_c
     }
-    // t = L^-H z: t_c = (z_c - sum_{m > c} conj(L[m][c]) t_m) / L_cc, the sum over the row's lanes
+    const double2 z = cscale(yv, ldi);
+    // t = L^-H z: t_c = (z_c - sum_{m > c} conj(L[m][c]) t_m) / L_cc, the sum
+    // over the row's lanes (column c of L is spread over them; lanes m <= c
+    // hold a zero or a t_m still zero).  (Round 6 A/B: L's rows through LDS so
+    // that lane c reads its column, t_m as the DPP operand, measured 3-5%
+    // slower at ranks 12..20 and 12% at 24, profiles/r06_ab_lowrank_solves.txt.)
     double2 t = make_double2(0.0, 0.0);
 #pragma unroll
     for (int c = R - 1; c >= 0; --c) {
-        const double2 term = i > c && row ? cmul(cconj(Ar[c]), t) : make_double2(0.0, 0.0);
-        const double2 sum = row16_sum(term);
+        const double2 sum = row16_sum(cmul(cconj(Ar[c]), t));
         if (i == c) t = cscale(csub(z, sum), ldi);
     }
     double *W = a.w + 2 * g * a.ws;

@@ -19,7 +19,8 @@ namespace wce {
 //            the frame's |x|^2 and conj(x) rx, E[k d mod 53] from LDS by the
 //            exact index recurrence (as the quad kernel)
 //   Cholesky pivot C < 16 updates Ar[j] (j < 16) and Br[j]; C >= 16 Br only
-//   z = L^-1 beta by broadcasts, t = L^-H z by 16-lane DPP sums
+//   z = L^-1 beta column by column, z_c as the DPP64 operand of the FMAs
+//            (round 6); t = L^-H z by 16-lane DPP sums
 //   complex x: the quad kernel's correction term; H_k = sum_j s_j t_j E[k j]
 //            over the pairs (k, 53 - k), the DFTs' broadcasts fused into DPP64 FMAs
 // Same algebra as mmse_lr_quad_kernel / mmse_lr_kernel, summed in another
@@ -63,6 +64,39 @@ __device__ __forceinline__ void lrq2_chol(double2 (&Ar)[16], double2 (&Br)[R], d
     }
 }
 
+// One unit's LDS: the Gram's tables.  The unit pitch (216 slots of 16 B, 8 mod
+// 16) puts two units' same-index reads (the pair tables' broadcasts,
+// Q(|r - j|)) in one ds_read_b128 lane group on different banks.
+struct Lrq2Tabs {
+    double2 Q[33];                    // Q(0..31)
+    double2 V[56];                    // conj(x_k) rx_k ...
+    double W[56];                     // ... and |x_k|^2
+    double2 PA[33], PB[33], RP[33];   // the pair tables (k = 1..26)
+};
+static_assert(sizeof(Lrq2Tabs) / 16 % 16 == 8, "unit pitch 8 mod 16 slots");
+
+// the forward substitution's column C (compile-time, so that every DPP lane
+// select is an immediate and nothing is left to the unroller): z_C = y_C / L_CC
+// from lane C (mod 16), conjugated for cmsub_dpp, then y_r -= L[r][C] z_C
+template <int R, int C>
+__device__ __forceinline__ void lrq2_fwd(const double2 (&Ar)[16], const double2 (&Br)[R], double2 &ya, double2 &yb,
+                                         double lda, double ldb)
+{
+    if constexpr (C < R) {
+        if constexpr (C < 16) {
+            double2 w = make_double2(ya.x * lda, -(ya.y * lda));
+            dpp_ready(w);
+            cmsub_dpp<C>(ya, Ar[C], w);
+            cmsub_dpp<C>(yb, Br[C], w);
+        } else {
+            double2 w = make_double2(yb.x * ldb, -(yb.y * ldb));
+            dpp_ready(w);
+            cmsub_dpp<C - 16>(yb, Br[C], w);
+        }
+        lrq2_fwd<R, C + 1>(Ar, Br, ya, yb, lda, ldb);
+    }
+}
+
 template <int R, bool FD = true, int MINW = 2>
 __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *__restrict__ st, SolveArgs a)
 {
@@ -73,13 +107,8 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
     const int64_t units = a.split ? a.n * a.nblk : a.n;
     const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
     __shared__ double2 sE[64];
-    // rows of 33 (528 B): the 16-lane rows of two units share a ds_read_b128
-    // lane group, and at a 512-B pitch their same-index reads (the pair tables'
-    // broadcasts, Q(|i - j|)) hit the same banks
-    __shared__ double2 sQ[16][33];    // one unit's Q(0..31)
-    __shared__ double2 sV[16][56];    // the unit's frame: conj(x_k) rx_k ...
-    __shared__ double sW[16][56];     // ... and |x_k|^2
-    __shared__ double2 sPA[16][33], sPB[16][33], sRP[16][33];   // the unit's pair tables (k = 1..26)
+    __shared__ Lrq2Tabs sU[16];   // the workgroup's 16 units
+    Lrq2Tabs &T = sU[rw];
     if (threadIdx.x < 64) sE[threadIdx.x] = ld2(st->dft, threadIdx.x);
     __syncthreads();
     if (g >= units || (a.skip && a.skip[g])) return;   // whole 16-lane rows
@@ -98,8 +127,8 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
             const double2 r = ld2(a.rx, base + k);
             if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
             cplx |= x.y != 0.0;
-            sW[rw][k] = fma(x.x, x.x, x.y * x.y);
-            sV[rw][k] = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
+            T.W[k] = fma(x.x, x.x, x.y * x.y);
+            T.V[k] = make_double2(fma(x.x, r.x, x.y * r.y), fma(x.x, r.y, -x.y * r.x));   // conj(x) rx
         }
     }
     wave_lds_sync();
@@ -111,23 +140,23 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
     for (int h = 0; h < 2; ++h) {
         const int k = i + 1 + 16 * h;
         if (k <= NSC / 2) {
-            const double2 u = sV[rw][k], w = sV[rw][NSC - k];
-            const double pu = sW[rw][k], pw = sW[rw][NSC - k];
-            sPA[rw][k] = cadd(u, w);
-            sPB[rw][k] = csub(u, w);
-            sRP[rw][k] = make_double2(pu + pw, pu - pw);
+            const double2 u = T.V[k], w = T.V[NSC - k];
+            const double pu = T.W[k], pw = T.W[NSC - k];
+            T.PA[k] = cadd(u, w);
+            T.PB[k] = csub(u, w);
+            T.RP[k] = make_double2(pu + pw, pu - pw);
         }
     }
     wave_lds_sync();
     // Q(d) = sum_k p_k conj(E[k d]) and sum_k v_k conj(E[k d]) at d = i and d = i + 16
-    double2 qa = make_double2(sW[rw][0], 0.0), qb = qa, ba = sV[rw][0], bb = ba;   // the k = 0 terms
+    double2 qa = make_double2(T.W[0], 0.0), qb = qa, ba = T.V[0], bb = ba;   // the k = 0 terms
     {
         const uint32_t sa = 16u * (uint32_t)i, swa = sa - 16u * NSC;
         const uint32_t sb = 16u * (uint32_t)(i + 16), swb = sb - 16u * NSC;
         uint32_t oa = sa, ob = sb;   // k = 1
 #pragma unroll 2
         for (int k = 1; k <= NSC / 2; ++k) {
-            const double2 ea = ld_e(sE, oa), eb = ld_e(sE, ob), pa = sPA[rw][k], pb = sPB[rw][k], pp = sRP[rw][k];
+            const double2 ea = ld_e(sE, oa), eb = ld_e(sE, ob), pa = T.PA[k], pb = T.PB[k], pp = T.RP[k];
             qa.x = fma(pp.x, ea.x, qa.x);
             qa.y = fma(-pp.y, ea.y, qa.y);
             qb.x = fma(pp.x, eb.x, qb.x);
@@ -141,15 +170,15 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
         }
     }
     const double sia = st->col_s[i], sib = rowb ? st->col_s[i + 16] : 0.0;
-    sQ[rw][i] = qa;
-    sQ[rw][i + 16] = qb;
+    T.Q[i] = qa;
+    T.Q[i + 16] = qb;
     wave_lds_sync();
     double2 Ar[16], Br[R];   // a s_r s_j Q(r - j) + b [r == j]  (Q(-d) = conj(Q(d)))
     // one LDS read per element: |r - j| indexes Q, the sign picks the conjugate
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int d = i - j;
-        double2 qd = sQ[rw][d >= 0 ? d : -d];
+        double2 qd = T.Q[d >= 0 ? d : -d];
         qd.y = d >= 0 ? qd.y : -qd.y;
         Ar[j] = cscale(qd, ac * sia * st->col_s[j]);
         Ar[j].x += i == j ? bc : 0.0;
@@ -157,34 +186,34 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int d = i + 16 - j;
-        double2 qd = sQ[rw][d >= 0 ? d : -d];
+        double2 qd = T.Q[d >= 0 ? d : -d];
         qd.y = d >= 0 ? qd.y : -qd.y;
         Br[j] = cscale(qd, ac * sib * st->col_s[j]);   // zero on lanes without a second row
         Br[j].x += (rowb && i + 16 == j) ? bc : 0.0;
     }
     double lda = 1.0, ldb = 1.0;
     lrq2_chol<R, 0, FD>(Ar, Br, lda, ldb, i);
-    // z = L^-1 beta (beta_r = s_r sum_k v_k conj(E[k r])): lane i keeps z_i, z_{i+16}
-    double2 za = cscale(ba, sia), zb = cscale(bb, sib);
+    // z = L^-1 beta (beta_r = s_r sum_k v_k conj(E[k r])): lane i keeps
+    // y_i = beta_i - sum_{c < i} L[i][c] z_c and y_{i+16}; z_c = y_c / L_cc from
+    // lane c (mod 16) as the DPP64 row_newbcast operand (conj(z_c) in w:
+    // cmsub_dpp subtracts l conj(R)).  L's entries on and above the diagonal
+    // are zeroed first, so that no lane needs a select here or in the
+    // back-substitution (round 6, as mmse_lr_quad_kernel).
 #pragma unroll
-    for (int c = 0; c < R; ++c) {
-        if (c < 16) {
-            const double2 zc = row_bcast_n(cscale(za, lda), c);
-            if (i == c) za = zc;
-            else if (i > c) za = csub(za, cmul(Ar[c], zc));
-            zb = csub(zb, cmul(Br[c], zc));
-        } else {
-            const double2 zc = row_bcast_n(cscale(zb, ldb), c - 16);
-            if (i == c - 16) zb = zc;
-            else if (i + 16 > c) zb = csub(zb, cmul(Br[c], zc));
-        }
-    }
-    // t = L^-H z: t_c = (z_c - sum_{m > c} conj(L[m][c]) t_m) / L_cc, the sum over both sets of the row
+    for (int c = 0; c < 16; ++c) keep_where_mask(rows16_upto(c), true, Ar[c], make_double2(0.0, 0.0));
+#pragma unroll
+    for (int c = 16; c < R; ++c) keep_where_mask(rows16_upto(c - 16), true, Br[c], make_double2(0.0, 0.0));
+    double2 ya = cscale(ba, sia), yb = cscale(bb, sib);
+    lrq2_fwd<R, 0>(Ar, Br, ya, yb, lda, ldb);
+    const double2 za = cscale(ya, lda), zb = cscale(yb, ldb);
+    // t = L^-H z: t_c = (z_c - sum_{m > c} conj(L[m][c]) t_m) / L_cc, the sum
+    // over both sets of the row (lanes whose rows are not below c hold a zero
+    // or a t still zero)
     double2 ta = make_double2(0.0, 0.0), tb = ta;
 #pragma unroll
     for (int c = R - 1; c >= 0; --c) {
-        double2 term = rowb && i + 16 > c ? cmul(cconj(Br[c]), tb) : make_double2(0.0, 0.0);
-        if (c < 16 && i > c) term = cadd(term, cmul(cconj(Ar[c < 16 ? c : 0]), ta));
+        double2 term = cmul(cconj(Br[c]), tb);
+        if (c < 16) term = cadd(term, cmul(cconj(Ar[c < 16 ? c : 0]), ta));
         const double2 sum = row16_sum(term);
         if (c < 16) {
             if (i == c) ta = cscale(csub(za, sum), lda);
@@ -209,13 +238,13 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
         // t through LDS (sQ is free after the Gram build) so that the j loops stay
         // rolled: unrolled, the scheduler hoists all 4R UT loads of a loop at once
         // and that branch alone would set the kernel's register budget
-        sQ[rw][i] = ta;
-        sQ[rw][i + 16] = tb;
+        T.Q[i] = ta;
+        T.Q[i + 16] = tb;
         wave_lds_sync();
         double2 uy[4] = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
 #pragma unroll 2
         for (int j = 0; j < R; ++j) {
-            const double2 tj = sQ[rw][j];
+            const double2 tj = T.Q[j];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const int k = i + 16 * m;
@@ -274,9 +303,11 @@ int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream,
     // instantiated at 20, 24, 28, 32 rows: a rank r below runs the next size
     // up with rows r.. as b I (col_s = 0 past the rank: no coupling, t = 0
     // there), bitwise the same arithmetic on the live rows.  Built for 2 waves
-    // per SIMD (256 VGPRs; ranks 21..32 spill 72-236 B per lane): 65,536 frames
-    // at rank 24 154.5 us against 225.6 us left at 1 wave per SIMD (20 / 28 /
-    // 32: 130 / 241 / 278 against 133 / 255 / 278; profiles/r06_ab_lowrank.txt).
+    // per SIMD (216 / 242 / 256 / 256 VGPRs at 20 / 24 / 28 / 32; 28 and 32
+    // spill 28 / 116 B per lane since round 6's forward substitution, 192 /
+    // 236 B before): 65,536 frames at rank 24 154.5 us against 225.6 us left at
+    // 1 wave per SIMD (20 / 28 / 32: 130 / 241 / 278 against 133 / 255 / 278;
+    // profiles/r06_ab_lowrank.txt, before the solve change).
     // form (A/B): 0 the product, 1 the Cholesky's broadcasts as separate movs
     // (rank 21..24 only), 2 every size at 1 wave per SIMD (no spills)
     if (rank <= 16 || rank > 32) return WCE_EINVAL;

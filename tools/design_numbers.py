@@ -201,9 +201,11 @@ if h:
              "The wave kernel it replaces at rank 24 issued 2,105 VALU and 432 LDS instructions per frame "
              "(`r04_pmc_legs.json`). Its LDS tables at odd 16-B-slot row pitches: 227 → 168 conflict cycles, "
              "164.5 → 160.2 µs (`r06_ab_lowrank_pad.txt`); what is left is the E[k d] gathers of the DFTs (16 lanes, "
-             "16 different entries)."),
+             "16 different entries). The forward substitution as DPP64 FMAs over zeroed upper entries: 1,196 → "
+             "1,100 VALU per frame, 153 → 135 µs (`r06_ab_lowrank_solves.txt`)."),
             ("lowrank16", "`mmse_lr_quad_kernel<16, true>` (leg `lowrank16`)",
-             "Odd row pitches: 178 → 100 conflict cycles, 92.0 → 88.1 µs.")):
+             "Odd row pitches: 178 → 100 conflict cycles, 92.0 → 88.1 µs; the forward substitution as DPP64 FMAs: "
+             "590 → 543 VALU per frame, 83.0 → 77.7 µs.")):
         q = legs.get(leg)
         if not q:
             continue
