@@ -307,7 +307,8 @@ int launch_lr_quad2(const State *st, int rank, const SolveArgs &a, void *stream,
     // spill 28 / 116 B per lane since round 6's forward substitution, 192 /
     // 236 B before): 65,536 frames at rank 24 154.5 us against 225.6 us left at
     // 1 wave per SIMD (20 / 28 / 32: 130 / 241 / 278 against 133 / 255 / 278;
-    // profiles/r06_ab_lowrank.txt, before the solve change).
+    // profiles/r06_ab_lowrank.txt); after the solve change 28 / 32: 161 / 198
+    // against 232 / 256 us (profiles/r06_ab_lowrank_minw.txt).
     // form (A/B): 0 the product, 1 the Cholesky's broadcasts as separate movs
     // (rank 21..24 only), 2 every size at 1 wave per SIMD (no spills)
     if (rank <= 16 || rank > 32) return WCE_EINVAL;
