@@ -3,7 +3,7 @@
 Runs one leg (headline TEXTBOOK solve by default, 65,536 frames) in a loop on
 one thread for --seconds, and samples `amd-smi metric` (power, clocks) from
 the main thread.  Read-only SMI queries; nothing is set.
-usage: python tools/power_probe.py [--leg headline|ls|idle] [--seconds 8]"""
+usage: python tools/power_probe.py [--leg headline|ls|config5|cov|lowrank|idle] [--taps 24] [--seconds 8]"""
 import argparse
 import json
 import os
@@ -34,7 +34,8 @@ def smi():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "config5", "cov", "idle"])
+    ap.add_argument("--leg", default="headline", choices=["headline", "ls", "config5", "cov", "lowrank", "idle"])
+    ap.add_argument("--taps", type=int, default=24, help="lowrank: an L-tap power-delay profile (taps 0..L-1)")
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--frames", type=int, default=65536)
     ap.add_argument("--lib", default=None, help="libwce.so to load (default: the in-tree build)")
@@ -75,6 +76,15 @@ def main():
         fr = ctx.frames(tx, rx, n)
         W = wce.DeviceArray((n, N), zero=True)
         run = lambda: ctx.mmse_solve(fr, W, N, s)
+    elif args.leg == "lowrank":   # WCE_MMSE_COV with an L-tap PDP (the bench's cov_lowrank legs)
+        import prof_leg
+        ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=prof_leg.pdp_rank(args.taps))
+        tx, rx = wce.DeviceArray((n, NBLK, N)), wce.DeviceArray((n, NBLK, N))
+        ctx.synth(tx, rx, None, n, seed=0x80211)
+        fr = ctx.frames(tx, rx, n)
+        H = wce.DeviceArray((n, N), zero=True)
+        o = wce.Outputs(None, None, None, None, H.addr, None, N, 0, 0, 0, 0)
+        run = lambda: ctx.estimate(fr, o, wce.PS_MMSE, s)
     elif args.leg == "ls":
         ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], wce.MMSE_REF)
         bufs, fr = bench.ls_frames(wce, ctx, n)
