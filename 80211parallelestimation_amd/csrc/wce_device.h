@@ -320,4 +320,83 @@ __device__ __forceinline__ void lrq2_readout(const double2 *sE, double2 ca, doub
     }
 }
 
+// Complex symbols in the quad kernels' tap domain (U[k][j] = s_j E[k j]; round 6):
+//   s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
+// with U t the read-out DFT of c = s o t (the lane's subcarriers k1 = i + 1,
+// 53 - k1 and, for i <= 9, k2 = i + 17, 53 - k2; k = 0 on lane 0) and U^H v
+// the Gram's beta DFT of v over the (k, 53 - k) pairs: three DFTs where the
+// row form spent R broadcasts, 4R products and R 16-lane sums on each side.
+// xm: State::xmask; tx / rx: the unit's block at base.  In: ca / cb = c on rows i and i + 16 (two
+// variables; cb a copy of ca when R <= 16).  Out: ca / cb =
+// (U^H v)_i / b and (U^H v)_{i+16} / b without the s factor (the caller adds
+// s_i times it to t_i).  V, PA, PB: the unit's dead Gram tables (>= 53 / 27 / 27
+// entries).
+template <int R>
+__device__ __forceinline__ void lrq_cplx_taps(uint64_t xm, const double *tx, const double *rx, int64_t base,
+                                              const double2 *sE, double2 *V, double2 *PA, double2 *PB, double2 &ca,
+                                              double2 &cb, int i, double ac, double bc)
+{
+    constexpr int NSC = 53;
+    const int k1 = i + 1, k2 = i + 17;
+    const bool two = k2 <= NSC / 2;
+    double2 h0 = R > 16 ? row16_sum(cadd(ca, cb)) : row16_sum(ca);
+    {   // y = U t at the lane's subcarriers
+        const uint32_t s1 = 16u * (uint32_t)k1, w1 = s1 - 16u * NSC;
+        const uint32_t s2 = 16u * (uint32_t)(two ? k2 : k1), w2 = s2 - 16u * NSC;
+        uint32_t o1 = 0, o2 = 0;
+        double2 A1 = make_double2(0.0, 0.0), B1 = A1, A2 = A1, B2 = A1;
+        dpp_ready(ca, cb);
+        lrq2_readout<R, 0>(sE, ca, cb, o1, o2, s1, w1, s2, w2, A1, B1, A2, B2);
+        const int ks[5] = {k1, NSC - k1, two ? k2 : k1, two ? NSC - k2 : NSC - k1, 0};
+        const double2 ys[5] = {make_double2(A1.x - B1.y, A1.y + B1.x), make_double2(A1.x + B1.y, A1.y - B1.x),
+                               make_double2(A2.x - B2.y, A2.y + B2.x), make_double2(A2.x + B2.y, A2.y - B2.x), h0};
+        double2 xs[5], rs[5];
+#pragma unroll
+        for (int m = 0; m < 5; ++m) {   // all loads first: one memory round trip
+            xs[m] = ld2(tx, base + ks[m]);
+            rs[m] = ld2(rx, base + ks[m]);
+        }
+#pragma unroll
+        for (int m = 0; m < 5; ++m) {   // v_k = (x - conj x) (rx - a x y_k) = 2 i Im(x) rho
+            if ((m == 2 || m == 3) && !two) continue;
+            if (m == 4 && i != 0) continue;
+            const double2 x = ((xm >> ks[m]) & 1ull) ? xs[m] : make_double2(0.0, 0.0);
+            const double2 rho = csub(rs[m], cscale(cmul(x, ys[m]), ac));
+            V[ks[m]] = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
+        }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // pair tables of v, k = 1..26
+        const int kp = i + 1 + 16 * h;
+        if (kp <= NSC / 2) {
+            const double2 u = V[kp], w = V[NSC - kp];
+            PA[kp] = cadd(u, w);
+            PB[kp] = csub(u, w);
+        }
+    }
+    wave_lds_sync();
+    // (U^H v)_r / s_r = sum_k v_k conj(E[k r]) at r = i and i + 16
+    double2 ba = V[0], bb = ba;
+    const uint32_t sa = 16u * (uint32_t)i, swa = sa - 16u * NSC;
+    const uint32_t sb = 16u * (uint32_t)(i + 16), swb = sb - 16u * NSC;
+    uint32_t oa = sa, ob = sb;
+#pragma unroll 2
+    for (int k = 1; k <= NSC / 2; ++k) {
+        const double2 ea = ld_e(sE, oa), pa = PA[k], pb = PB[k];
+        ba.x = fma(pa.x, ea.x, fma(pb.y, ea.y, ba.x));
+        ba.y = fma(pa.y, ea.x, fma(-pb.x, ea.y, ba.y));
+        if (R > 16) {
+            const double2 eb = ld_e(sE, ob);
+            bb.x = fma(pa.x, eb.x, fma(pb.y, eb.y, bb.x));
+            bb.y = fma(pa.y, eb.x, fma(-pb.x, eb.y, bb.y));
+            ob = dft_step(ob, sb, swb);
+        }
+        oa = dft_step(oa, sa, swa);
+    }
+    const double rb = 1.0 / bc;
+    ca = cscale(ba, rb);
+    cb = cscale(bb, rb);
+}
+
 }  // namespace wce

@@ -2436,7 +2436,15 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         if (i == c) t = cscale(csub(z, sum), ldi);
     }
     double *W = a.w + 2 * g * a.ws;
-    if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
+    if constexpr (TQ) {
+        if (__ballot(cplx) != 0) {   // complex symbols, in the tap domain (round 6): see lrq_cplx_taps
+            LrqTabs &T = sU[rw];
+            const double si = row ? st->col_s[i] : 0.0;
+            double2 c = cscale(t, si), cb = c;   // (cb: rows i + 16, none here)
+            lrq_cplx_taps<R>(xm, a.tx, a.rx, base, sE, T.V, T.PA, T.PB, c, cb, i, ac, bc);
+            t = cadd(t, cscale(c, si));
+        }
+    } else if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
         double2 vk[4], rk[4];   // the correction's v_k at the lane's subcarriers k = i + 16 m
 #pragma unroll
         for (int m = 0; m < 4; ++m) {

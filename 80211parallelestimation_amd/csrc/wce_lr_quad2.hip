@@ -222,57 +222,11 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
         }
     }
     double *W = a.w + 2 * g * a.ws;
-    const double2 *__restrict__ UT = reinterpret_cast<const double2 *>(st->UT);
-    if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b
-        double2 vk[4], rk[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int k = i + 16 * m;
-            const int kc = k < NSC ? k : 0;
-            double2 x = ld2(a.tx, base + kc);
-            const double2 r = ld2(a.rx, base + kc);
-            if (!((xm >> kc) & 1ull) || k >= NSC) x = make_double2(0.0, 0.0);
-            vk[m] = x;
-            rk[m] = r;
-        }
-        // t through LDS (sQ is free after the Gram build) so that the j loops stay
-        // rolled: unrolled, the scheduler hoists all 4R UT loads of a loop at once
-        // and that branch alone would set the kernel's register budget
-        T.Q[i] = ta;
-        T.Q[i + 16] = tb;
-        wave_lds_sync();
-        double2 uy[4] = {make_double2(0, 0), make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
-#pragma unroll 2
-        for (int j = 0; j < R; ++j) {
-            const double2 tj = T.Q[j];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int k = i + 16 * m;
-                uy[m] = cadd(uy[m], cmul(UT[j * CLD + (k < NSC ? k : 0)], tj));
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const double2 x = vk[m];
-            const double2 rho = csub(rk[m], cscale(cmul(x, uy[m]), ac));
-            vk[m] = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
-        }
-        const double rb = 1.0 / bc;
-        // reload UT below instead of keeping the first loop's values live (a
-        // memory clobber: no load is reused across it)
-        asm volatile("" ::: "memory");
-#pragma unroll 2
-        for (int j = 0; j < R; ++j) {
-            double2 cp = make_double2(0.0, 0.0);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int k = i + 16 * m;
-                cp = cadd(cp, cmul(cconj(UT[j * CLD + (k < NSC ? k : 0)]), vk[m]));
-            }
-            const double2 cj = row16_sum(cp);
-            if (j < 16 && i == j) ta = cadd(ta, cscale(cj, rb));
-            if (j >= 16 && i == j - 16) tb = cadd(tb, cscale(cj, rb));
-        }
+    if (__ballot(cplx) != 0) {   // complex symbols, in the tap domain (round 6): see lrq_cplx_taps
+        double2 ca = cscale(ta, sia), cb = cscale(tb, sib);
+        lrq_cplx_taps<R>(xm, a.tx, a.rx, base, sE, T.V, T.PA, T.PB, ca, cb, i, ac, bc);
+        ta = cadd(ta, cscale(ca, sia));
+        tb = cadd(tb, cscale(cb, sib));
     }
     // H_k = sum_j s_j t_j E[k j] over the pairs (k, 53 - k): with c_j = s_j t_j,
     // A = sum_j c_j Re E[k j], B = sum_j c_j Im E[k j], H_k = A + i B and
