@@ -329,12 +329,12 @@ __device__ __forceinline__ void lrq2_readout(const double2 *sE, double2 ca, doub
 // xm: State::xmask; tx / rx: the unit's block at base.  In: ca / cb = c on rows i and i + 16 (two
 // variables; cb a copy of ca when R <= 16).  Out: ca / cb =
 // (U^H v)_i / b and (U^H v)_{i+16} / b without the s factor (the caller adds
-// s_i times it to t_i).  V, PA, PB: the unit's dead Gram tables (>= 53 / 27 / 27
-// entries).
+// s_i times it to t_i).  V: 53 dead entries of the unit's LDS (v, then its pair
+// tables in place).
 template <int R>
 __device__ __forceinline__ void lrq_cplx_taps(uint64_t xm, const double *tx, const double *rx, int64_t base,
-                                              const double2 *sE, double2 *V, double2 *PA, double2 *PB, double2 &ca,
-                                              double2 &cb, int i, double ac, double bc)
+                                              const double2 *sE, double2 *V, double2 &ca, double2 &cb, int i,
+                                              double ac, double bc)
 {
     constexpr int NSC = 53;
     const int k1 = i + 1, k2 = i + 17;
@@ -366,13 +366,22 @@ __device__ __forceinline__ void lrq_cplx_taps(uint64_t xm, const double *tx, con
         }
     }
     wave_lds_sync();
+    {   // pair tables of v in place, k = 1..26: V[k] = v_k + v_{53-k}, V[53-k] = v_k - v_{53-k}
+        double2 u[2], w[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {   // pair tables of v, k = 1..26
-        const int kp = i + 1 + 16 * h;
-        if (kp <= NSC / 2) {
-            const double2 u = V[kp], w = V[NSC - kp];
-            PA[kp] = cadd(u, w);
-            PB[kp] = csub(u, w);
+        for (int h = 0; h < 2; ++h) {
+            const int kp = i + 1 + 16 * h, kc = kp <= NSC / 2 ? kp : 1;
+            u[h] = V[kc];
+            w[h] = V[NSC - kc];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kp = i + 1 + 16 * h;
+            if (kp <= NSC / 2) {
+                V[kp] = cadd(u[h], w[h]);
+                V[NSC - kp] = csub(u[h], w[h]);
+            }
         }
     }
     wave_lds_sync();
@@ -383,7 +392,7 @@ __device__ __forceinline__ void lrq_cplx_taps(uint64_t xm, const double *tx, con
     uint32_t oa = sa, ob = sb;
 #pragma unroll 2
     for (int k = 1; k <= NSC / 2; ++k) {
-        const double2 ea = ld_e(sE, oa), pa = PA[k], pb = PB[k];
+        const double2 ea = ld_e(sE, oa), pa = V[k], pb = V[NSC - k];
         ba.x = fma(pa.x, ea.x, fma(pb.y, ea.y, ba.x));
         ba.y = fma(pa.y, ea.x, fma(-pb.x, ea.y, ba.y));
         if (R > 16) {

@@ -2276,17 +2276,18 @@ __device__ __forceinline__ void lrq_chol(double2 (&Ar)[R], double &ldi, int i)
     }
 }
 
-// One 16-lane unit's LDS in mmse_lr_quad_kernel<R, true>: the Toeplitz Gram's
-// tables.  The unit pitch (200 slots of 16 B, 8 mod 16) puts two units'
-// same-index reads (the pair tables' broadcasts, Q(|i - j|)) in one
-// ds_read_b128 lane group on different banks.
+// One 16-lane unit's LDS in mmse_lr_quad_kernel<R, true> (1,344 B, so that 4
+// workgroups fit a CU: the kernel needs <= 128 VGPRs since round 6): the frame's
+// v = conj(x) o rx and p = |x|^2, turned in place into the pair tables
+// (V[k] = v_k + v_{53-k}, V[53-k] = v_k - v_{53-k}, RP[k] = {p_k + p_{53-k},
+// p_k - p_{53-k}} over W), then Q(0..15) over V.  The unit pitch (84 slots of
+// 16 B, 4 mod 16) puts two units' same-index reads in one ds_read_b128 lane
+// group on different banks.
 struct LrqTabs {
-    double2 Q[17];                    // Q(0..15)
-    double2 V[56];                    // conj(x_k) rx_k ...
-    double W[56];                     // ... and |x_k|^2
-    double2 PA[33], PB[33], RP[33];   // the pair tables, k = 1..26
+    double2 V[56];
+    double W[56];
 };
-static_assert(sizeof(LrqTabs) / 16 % 16 == 8, "unit pitch 8 mod 16 slots");
+static_assert(sizeof(LrqTabs) / 16 % 16 != 0, "unit pitch not 0 mod 16 slots");
 
 // (pass 1's U_k from an LDS copy per workgroup instead of scalar loads: slower,
 // rank 16 237 -> 271 us at 65,536 frames, 3.82 -> 4.39 ms at 1M; retired in
@@ -2344,16 +2345,26 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         }
         wave_lds_sync();   // the row's 16 lanes are one wave's
         // pair tables over (k, 53 - k), k = 1..26 (round 6, as mmse_lr_quad2_kernel):
-        // one gather and half the FMAs per pair
+        // one gather and half the FMAs per pair; in place, so every read first
+        double2 *RP = reinterpret_cast<double2 *>(T.W);   // RP[k] over W[2k], W[2k + 1], k >= 1
+        double2 u[2], w[2];
+        double pu[2], pw[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kp = i + 1 + 16 * h, kc = kp <= NSC / 2 ? kp : 1;
+            u[h] = T.V[kc];
+            w[h] = T.V[NSC - kc];
+            pu[h] = T.W[kc];
+            pw[h] = T.W[NSC - kc];
+        }
+        wave_lds_sync();
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int kp = i + 1 + 16 * h;
             if (kp <= NSC / 2) {
-                const double2 u = T.V[kp], w = T.V[NSC - kp];
-                const double pu = T.W[kp], pw = T.W[NSC - kp];
-                T.PA[kp] = cadd(u, w);
-                T.PB[kp] = csub(u, w);
-                T.RP[kp] = make_double2(pu + pw, pu - pw);
+                T.V[kp] = cadd(u[h], w[h]);
+                T.V[NSC - kp] = csub(u[h], w[h]);
+                RP[kp] = make_double2(pu[h] + pw[h], pu[h] - pw[h]);
             }
         }
         wave_lds_sync();
@@ -2363,7 +2374,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         uint32_t qo = qs;   // 16 (k i mod 53), k = 1
 #pragma unroll 2
         for (int kp = 1; kp <= NSC / 2; ++kp) {
-            const double2 e = ld_e(sE, qo), pa = T.PA[kp], pb = T.PB[kp], pp = T.RP[kp];
+            const double2 e = ld_e(sE, qo), pa = T.V[kp], pb = T.V[NSC - kp], pp = RP[kp];
             q.x = fma(pp.x, e.x, q.x);
             q.y = fma(-pp.y, e.y, q.y);
             bq.x = fma(pa.x, e.x, fma(pb.y, e.y, bq.x));
@@ -2372,11 +2383,12 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
         }
         const double si = row ? st->col_s[i] : 0.0;
         bt = cscale(bq, si);
-        T.Q[i] = q;
+        wave_lds_sync();   // every lane's table reads are done: Q(i) over V
+        T.V[i] = q;
         wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < R; ++j) {   // a s_i s_j Q(i - j) + b [i == j]; rows past R: the identity (never read)
-            const double2 qd = j <= i ? T.Q[(i - j) & 15] : cconj(T.Q[(j - i) & 15]);
+            const double2 qd = j <= i ? T.V[(i - j) & 15] : cconj(T.V[(j - i) & 15]);
             Ar[j] = cscale(qd, ac * si * st->col_s[j]);
             Ar[j].x += (i == j || (!row && j == 0)) ? bc : 0.0;
         }
@@ -2441,7 +2453,7 @@ __global__ __launch_bounds__(256) void mmse_lr_quad_kernel(const State *__restri
             LrqTabs &T = sU[rw];
             const double si = row ? st->col_s[i] : 0.0;
             double2 c = cscale(t, si), cb = c;   // (cb: rows i + 16, none here)
-            lrq_cplx_taps<R>(xm, a.tx, a.rx, base, sE, T.V, T.PA, T.PB, c, cb, i, ac, bc);
+            lrq_cplx_taps<R>(xm, a.tx, a.rx, base, sE, T.V, c, cb, i, ac, bc);
             t = cadd(t, cscale(c, si));
         }
     } else if (__ballot(cplx) != 0) {   // complex symbols: s = t + U^H [(x - conj x) o (rx - a x o (U t))] / b

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256, MINW) void mmse_lr_quad2_kernel(const State *_
     double *W = a.w + 2 * g * a.ws;
     if (__ballot(cplx) != 0) {   // complex symbols, in the tap domain (round 6): see lrq_cplx_taps
         double2 ca = cscale(ta, sia), cb = cscale(tb, sib);
-        lrq_cplx_taps<R>(xm, a.tx, a.rx, base, sE, T.V, T.PA, T.PB, ca, cb, i, ac, bc);
+        lrq_cplx_taps<R>(xm, a.tx, a.rx, base, sE, T.V, ca, cb, i, ac, bc);
         ta = cadd(ta, cscale(ca, sia));
         tb = cadd(tb, cscale(cb, sib));
     }
