@@ -339,7 +339,9 @@ __device__ __forceinline__ void lrq_cplx_taps(uint64_t xm, const double *tx, con
     constexpr int NSC = 53;
     const int k1 = i + 1, k2 = i + 17;
     const bool two = k2 <= NSC / 2;
-    double2 h0 = R > 16 ? row16_sum(cadd(ca, cb)) : row16_sum(ca);
+    double2 h0;
+    if constexpr (R > 16) h0 = row16_sum(cadd(ca, cb));
+    else h0 = row16_sum(ca);
     {   // y = U t at the lane's subcarriers
         const uint32_t s1 = 16u * (uint32_t)k1, w1 = s1 - 16u * NSC;
         const uint32_t s2 = 16u * (uint32_t)(two ? k2 : k1), w2 = s2 - 16u * NSC;
@@ -395,7 +397,7 @@ __device__ __forceinline__ void lrq_cplx_taps(uint64_t xm, const double *tx, con
         const double2 ea = ld_e(sE, oa), pa = V[k], pb = V[NSC - k];
         ba.x = fma(pa.x, ea.x, fma(pb.y, ea.y, ba.x));
         ba.y = fma(pa.y, ea.x, fma(-pb.x, ea.y, ba.y));
-        if (R > 16) {
+        if constexpr (R > 16) {
             const double2 eb = ld_e(sE, ob);
             bb.x = fma(pa.x, eb.x, fma(pb.y, eb.y, bb.x));
             bb.y = fma(pa.y, eb.x, fma(-pb.x, eb.y, bb.y));
