@@ -2101,13 +2101,23 @@ __device__ __forceinline__ void lr_lane_body(const State *__restrict__ st, const
         for (int i = 0; i < R; ++i) cc[i] = make_double2(0.0, 0.0);
         lrl_sweep<STAGED, 2>(sp, a, eb, live, base, own, lane, [&](int k, double2 x, double2 r) {
             if (!((xm >> k) & 1ull)) x = make_double2(0.0, 0.0);
+            // the products accumulate as FMA chains (4 per complex term, where
+            // cadd(y, cmul(u, t)) rounds the product first: 6)
             double2 y = make_double2(0.0, 0.0);
 #pragma unroll
-            for (int j = 0; j < R; ++j) y = cadd(y, cmul(U[k * uld + j], t[j]));
+            for (int j = 0; j < R; ++j) {
+                const double2 u = U[k * uld + j];
+                y.x = fma(u.x, t[j].x, fma(-u.y, t[j].y, y.x));
+                y.y = fma(u.x, t[j].y, fma(u.y, t[j].x, y.y));
+            }
             const double2 rho = csub(r, cscale(cmul(x, y), ac));
             const double2 v = make_double2(-2.0 * x.y * rho.y, 2.0 * x.y * rho.x);
 #pragma unroll
-            for (int j = 0; j < R; ++j) cc[j] = cadd(cc[j], cmul(cconj(U[k * uld + j]), v));
+            for (int j = 0; j < R; ++j) {   // cc_j += conj(u) v
+                const double2 u = U[k * uld + j];
+                cc[j].x = fma(u.x, v.x, fma(u.y, v.y, cc[j].x));
+                cc[j].y = fma(u.x, v.y, fma(-u.y, v.x, cc[j].y));
+            }
         });
         const double rb = 1.0 / bc;
 #pragma unroll

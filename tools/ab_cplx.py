@@ -1,7 +1,7 @@
 """The COV low-rank kernels on complex symbols: the bench's BPSK frames against
 the same frames turned QPSK (tx and rx times one unit phase per symbol, so the
 channel and the noise statistics are unchanged), HIP-event timing.
-usage: python tools/ab_cplx.py [--taps 16 24] [--frames 65536]"""
+usage: python tools/ab_cplx.py [--taps 16 24] [--frames 65536] [--lib path/libwce.so]"""
 import argparse
 import importlib
 import os
@@ -20,8 +20,12 @@ def main():
     ap.add_argument("--taps", type=int, nargs="+", default=[16, 24])
     ap.add_argument("--frames", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="libwce.so to load (default: the in-tree build)")
     args = ap.parse_args()
     wce = importlib.import_module("80211parallelestimation_amd")
+    if args.lib:
+        sys.modules["80211parallelestimation_amd.wce"]._lib = None
+        wce.load(os.path.abspath(args.lib))
     import bench
     import prof_leg
     inp = dict(np.load(os.path.join(REPO, "tests", "golden", "inputs_h.npz")))
