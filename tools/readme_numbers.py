@@ -124,9 +124,10 @@ def table_of(d, src):
 
 table = "".join(render(p) for p in pick())
 table += ("The FP64 solve runs at the board's power cap, so the headline moves by about ±3% from box to box: "
-          "round 6's last three refreshes measured 0.445 ms (51.9%, `profiles/r06_bench.json`), 0.454 ms (51.0%, "
-          "`r06_bench_box1.json`) and 0.468 ms (49.4%, `r06_bench_box2.json`) per 65,536 frames with the same "
-          "kernel.\n\n")
+          "round 6's refreshes on five boxes measured 0.445 ms (51.9%, `profiles/r06_bench.json`), 0.454 ms "
+          "(`r06_bench_box1.json`), 0.458 ms (`r06_bench_box5.json`, the last build: its changes since "
+          "`r06_bench.json` are in code no bench leg runs) and 0.468 ms (49.4%, `r06_bench_box2.json`) per "
+          "65,536 frames with the same kernel.\n\n")
 p = os.path.join(REPO, "README.md")
 s = open(p).read()
 a, b = s.index("## Numbers (one MI355X"), s.index("`DESIGN.md` covers:")
