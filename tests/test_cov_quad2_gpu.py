@@ -113,3 +113,33 @@ def test_quad2_batch_edges(gpu_wce, golden):
     for B in (1, 15, 16, 17):
         part = ctx.estimate_host(tx[:B], rx[:B], mask=wce.PS_MMSE)["ps_mmse"]
         assert np.array_equal(part, full[:B]), B
+
+
+@pytest.mark.parametrize("L,kernel", [(12, "mmse_lr_quad_kernel<12, true>"), (22, "mmse_lr_quad2_kernel<24>")])
+def test_quad_kernels_complex_symbols_split_matlab(gpu_wce, golden, oracle, L, kernel):
+    """Round 6's tap-domain correction (lrq_cplx_taps: U t as the read-out DFT,
+    U^H v as the beta DFT) on 16-QAM frames with nulls, in MATLAB semantics
+    (one unit per (frame, block), blocks 0..3 averaged): against the long
+    double per-block solves and the wave kernel on the same frames."""
+    wce = gpu_wce
+    inp = golden["inputs"]
+    R = pdp_rhh(L, 0.3)
+    ctx = wce.Context(inp["tx_pre"], inp["rx_pre"], inp["ow2"], Rhh=R)
+    B = 45
+    assert ctx.lr_kernel(4 * B) == kernel
+    rng = np.random.default_rng(1200 + L)
+    tx = constellation(rng, "qam16", (B, NBLK, N))
+    tx[:, :, 26] = 0
+    tx[1, 2, [5, 33]] = 0
+    rx = channel_frames(rng, tx, inp["ow2"])
+    run = lambda: ctx.estimate_host(tx, rx, mask=wce.PS_MMSE, semantics=wce.SEM_MATLAB)["ps_mmse"]
+    out = run()
+    wav = wave_kernel(wce, run)
+    C = c_ld(oracle, R)
+    per = [solve_ld(oracle, C, tx[:, b], rx[:, b], inp["ow2"]) for b in range(4)]   # blocks 0..3 (.m:28-35)
+    exp = (((per[0] + per[1]) + per[2]) + per[3]) / 4
+    err = normrel(out, exp)
+    print(f"\nL={L} 16-QAM MATLAB: max {err.max():.2e}; vs wave kernel {normrel(out, wav).max():.2e}")
+    assert np.isfinite(out).all()
+    assert err.max() < 1e-12, (int(err.argmax()), err.max())
+    assert normrel(out, wav).max() < 1e-12
